@@ -1,0 +1,36 @@
+/* ORACLE — test infrastructure only.  Exported entry points (ctypes) for tests / bench. */
+#ifndef OR_API_H
+#define OR_API_H
+#include <stdint.h>
+#include <stddef.h>
+#include "or_machine.h"
+
+typedef struct { double t[8]; } or_timing;
+
+int or_prove_record(const or_program* prog, or_record* rec, uint8_t** out, size_t* outlen,
+                    or_timing* tm);
+int or_verify_proof(const or_program* prog, const uint8_t* proof, size_t len);
+void or_set_num_queries(int q);
+
+/* ctypes-facing API (canonical u32 field values everywhere) */
+int or_api_execute(const char* program, const uint8_t* in, size_t nin, uint8_t* out,
+                   size_t outcap, size_t* outlen, uint64_t* cycles, uint32_t* final_pc,
+                   uint32_t* final_mp);
+int or_api_prove(const char* program, const uint8_t* in, size_t nin, uint8_t** proof,
+                 size_t* len);
+int or_api_verify(const char* program, const uint8_t* proof, size_t len);
+void or_api_free(void* p);
+int or_api_trace(const char* program, const uint8_t* in, size_t nin, int chip, int prep,
+                 uint32_t** out, size_t* h, size_t* w);
+void or_api_poseidon2(uint32_t* states, size_t n);
+void or_api_hash(const uint32_t* in, size_t n, uint32_t out[8]);
+void or_api_coset_lde(const uint32_t* in, size_t n, size_t w, uint32_t shift, uint32_t* out);
+void or_api_merkle_root(const uint32_t* const* mats, const size_t* heights, const size_t* widths,
+                        int nmats, uint32_t root[8]);
+uint32_t or_api_two_adic_gen(int bits);
+void or_api_ef_mul(const uint32_t a[4], const uint32_t b[4], uint32_t out[4]);
+void or_api_ef_inv(const uint32_t a[4], uint32_t out[4]);
+/* sample a challenger transcript: observe `n` values then squeeze `m` samples */
+void or_api_challenger(const uint32_t* obs, size_t n, uint32_t* samples, size_t m);
+
+#endif

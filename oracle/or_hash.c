@@ -1,0 +1,247 @@
+/*
+ * ORACLE — test infrastructure only.
+ *
+ * Poseidon2KoalaBear<16> as configured by the reference's `my_perm()`
+ * (crates/stark/src/kb31_poseidon2.rs:35-50, identical to poseidon2_init at
+ * crates/primitives/src/lib.rs:1101-1117), its PaddingFreeSponge<Perm,16,8,8> and
+ * TruncatedPermutation<Perm,2,8,16> (kb31_poseidon2.rs:24-26), the MerkleTreeMmcs built
+ * from them (kb31_poseidon2.rs:27-28), and DuplexChallenger<Val,Perm,16,8>
+ * (kb31_poseidon2.rs:31,126-128).  The permutation / sponge / tree / challenger
+ * algorithms live in the un-vendored zkMIPS/Plonky3 fork @93967fce; they are restated
+ * from the published Plonky3 algorithms [p3-recalled]:
+ *   - S-box x^3; 4 initial external rounds, 13 internal, 4 terminal external.
+ *   - external layer "MDS light": M4 = [[2,3,1,1],[1,2,3,1],[1,1,2,3],[3,1,1,2]] on each
+ *     4-lane block, then add the lane-wise sum over blocks; applied once before round 1.
+ *   - external round: s_i = (s_i + rc_i)^3 for all i, then MDS light.
+ *   - internal round: s_0 = (s_0 + rc)^3; s_i = sum + d_i * s_i with
+ *     d = [-2,1,2,1/2,3,4,-1/2,-3,-4,1/2^8,1/8,1/2^24,-1/2^8,-1/8,-1/16,-1/2^24].
+ * Parity for this file is UNPINNED against the Rust prover (no Plonky3 source or Rust
+ * toolchain in the container); it is the reference point the GPU path is checked against.
+ */
+#include <stdlib.h>
+#include <string.h>
+#include "or_field.h"
+#include "or_hash.h"
+
+static const uint32_t RC_RAW[30 * 16] = {
+#include "rc_16_30.inc"
+};
+
+static fp EXT_INIT[4][16], EXT_TERM[4][16], INT_RC[13], DIAG[16];
+static int g_init = 0;
+
+static void p2_init(void) {
+  if (g_init) return;
+  /* my_perm(): drain rows 4..17 (first element each) as internal constants; of the 17
+   * remaining rows, [0..4) are initial and [4..8) (= original 17..21) terminal. */
+  for (int r = 0; r < 4; r++)
+    for (int i = 0; i < 16; i++) {
+      EXT_INIT[r][i] = fp_from_u64(RC_RAW[r * 16 + i]);
+      EXT_TERM[r][i] = fp_from_u64(RC_RAW[(17 + r) * 16 + i]);
+    }
+  for (int r = 0; r < 13; r++) INT_RC[r] = fp_from_u64(RC_RAW[(4 + r) * 16]);
+  fp inv2 = fp_inv(2), inv8 = fp_inv(8), inv16 = fp_inv(16);
+  fp inv256 = fp_inv(256), inv2_24 = fp_inv(1u << 24);
+  fp d[16] = {fp_neg(2), 1, 2, inv2, 3, 4, fp_neg(inv2), fp_neg(3), fp_neg(4),
+              inv256, inv8, inv2_24, fp_neg(inv256), fp_neg(inv8), fp_neg(inv16),
+              fp_neg(inv2_24)};
+  memcpy(DIAG, d, sizeof d);
+  g_init = 1;
+}
+
+static inline fp cube(fp x) { return fp_mul(fp_mul(x, x), x); }
+
+static void mds_light(fp s[16]) {
+  for (int b = 0; b < 16; b += 4) {
+    fp x0 = s[b], x1 = s[b + 1], x2 = s[b + 2], x3 = s[b + 3];
+    /* [2 3 1 1; 1 2 3 1; 1 1 2 3; 3 1 1 2] */
+    fp y0 = fp_add(fp_add(fp_mul(2, x0), fp_mul(3, x1)), fp_add(x2, x3));
+    fp y1 = fp_add(fp_add(x0, fp_mul(2, x1)), fp_add(fp_mul(3, x2), x3));
+    fp y2 = fp_add(fp_add(x0, x1), fp_add(fp_mul(2, x2), fp_mul(3, x3)));
+    fp y3 = fp_add(fp_add(fp_mul(3, x0), x1), fp_add(x2, fp_mul(2, x3)));
+    s[b] = y0; s[b + 1] = y1; s[b + 2] = y2; s[b + 3] = y3;
+  }
+  fp sums[4];
+  for (int k = 0; k < 4; k++) sums[k] = fp_add(fp_add(s[k], s[4 + k]), fp_add(s[8 + k], s[12 + k]));
+  for (int i = 0; i < 16; i++) s[i] = fp_add(s[i], sums[i & 3]);
+}
+
+void or_poseidon2_permute(fp s[16]) {
+  p2_init();
+  mds_light(s);
+  for (int r = 0; r < 4; r++) {
+    for (int i = 0; i < 16; i++) s[i] = cube(fp_add(s[i], EXT_INIT[r][i]));
+    mds_light(s);
+  }
+  for (int r = 0; r < 13; r++) {
+    s[0] = cube(fp_add(s[0], INT_RC[r]));
+    fp sum = 0;
+    for (int i = 0; i < 16; i++) sum = fp_add(sum, s[i]);
+    for (int i = 0; i < 16; i++) s[i] = fp_add(sum, fp_mul(DIAG[i], s[i]));
+  }
+  for (int r = 0; r < 4; r++) {
+    for (int i = 0; i < 16; i++) s[i] = cube(fp_add(s[i], EXT_TERM[r][i]));
+    mds_light(s);
+  }
+}
+
+/* PaddingFreeSponge<Perm,16,8,8>::hash_iter: overwrite-mode absorb in chunks of 8;
+ * permute after each full chunk and after a trailing partial chunk; empty input ->
+ * all-zero digest without a permutation. */
+void or_sponge_begin(or_sponge* sp) { memset(sp, 0, sizeof *sp); }
+void or_sponge_absorb(or_sponge* sp, fp x) {
+  sp->st[sp->pos++] = x;
+  if (sp->pos == 8) {
+    or_poseidon2_permute(sp->st);
+    sp->pos = 0;
+  }
+}
+void or_sponge_finish(or_sponge* sp, fp out[8]) {
+  if (sp->pos != 0) or_poseidon2_permute(sp->st);
+  memcpy(out, sp->st, 8 * sizeof(fp));
+}
+void or_hash(const fp* in, size_t n, fp out[8]) {
+  or_sponge sp;
+  or_sponge_begin(&sp);
+  for (size_t i = 0; i < n; i++) or_sponge_absorb(&sp, in[i]);
+  or_sponge_finish(&sp, out);
+}
+
+/* TruncatedPermutation<Perm,2,8,16>: perm(left || right)[0..8]. */
+void or_compress(const fp l[8], const fp r[8], fp out[8]) {
+  fp s[16];
+  memcpy(s, l, 8 * sizeof(fp));
+  memcpy(s + 8, r, 8 * sizeof(fp));
+  or_poseidon2_permute(s);
+  memcpy(out, s, 8 * sizeof(fp));
+}
+
+/* ------------------------------------------------------------------------------------
+ * MerkleTreeMmcs::commit for matrices whose heights are powers of two [p3-recalled]:
+ *  - matrices sorted (stably) by descending height;
+ *  - layer 0 digest i = sponge(concat row i of every tallest matrix, in order);
+ *  - each next layer j: node = compress(L, R); if matrices of height == layer length
+ *    exist, node = compress(node, sponge(concat row j of those matrices)).
+ * The matrices are bit-reversed LDEs, row-major. */
+static int cmp_height_desc(const void* a, const void* b) {
+  const or_mat* const* x = a;
+  const or_mat* const* y = b;
+  if ((*x)->height != (*y)->height) return (*x)->height > (*y)->height ? -1 : 1;
+  return (*x)->order < (*y)->order ? -1 : ((*x)->order > (*y)->order);
+}
+
+void or_merkle_build(or_merkle* t, or_mat* mats, int nmats) {
+  or_mat** sorted = malloc(sizeof(or_mat*) * nmats);
+  for (int i = 0; i < nmats; i++) { mats[i].order = i; sorted[i] = &mats[i]; }
+  qsort(sorted, nmats, sizeof(or_mat*), cmp_height_desc);
+  size_t h0 = sorted[0]->height;
+  int nl = 0;
+  while ((1ull << nl) < h0) nl++;
+  t->nlayers = nl + 1;
+  t->layers = calloc(t->nlayers, sizeof(fp*));
+  t->mats = mats;
+  t->nmats = nmats;
+  int next = 0;
+  /* layer 0 */
+  t->layers[0] = malloc(sizeof(fp) * 8 * h0);
+  int first_end = next;
+  while (first_end < nmats && sorted[first_end]->height == h0) first_end++;
+#pragma omp parallel for schedule(static)
+  for (long i = 0; i < (long)h0; i++) {
+    or_sponge sp;
+    or_sponge_begin(&sp);
+    for (int m = next; m < first_end; m++) {
+      const or_mat* M = sorted[m];
+      for (size_t c = 0; c < M->width; c++) or_sponge_absorb(&sp, M->values[i * M->width + c]);
+    }
+    or_sponge_finish(&sp, &t->layers[0][8 * i]);
+  }
+  next = first_end;
+  size_t len = h0;
+  for (int L = 1; L < t->nlayers; L++) {
+    size_t nlen = len / 2;
+    int inj_end = next;
+    while (inj_end < nmats && sorted[inj_end]->height == nlen) inj_end++;
+    t->layers[L] = malloc(sizeof(fp) * 8 * nlen);
+    const fp* prev = t->layers[L - 1];
+#pragma omp parallel for schedule(static)
+    for (long j = 0; j < (long)nlen; j++) {
+      fp node[8];
+      or_compress(&prev[16 * j], &prev[16 * j + 8], node);
+      if (inj_end > next) {
+        fp rows[8];
+        or_sponge sp;
+        or_sponge_begin(&sp);
+        for (int m = next; m < inj_end; m++) {
+          const or_mat* M = sorted[m];
+          for (size_t c = 0; c < M->width; c++) or_sponge_absorb(&sp, M->values[j * M->width + c]);
+        }
+        or_sponge_finish(&sp, rows);
+        or_compress(node, rows, node);
+      }
+      memcpy(&t->layers[L][8 * j], node, sizeof node);
+    }
+    next = inj_end;
+    len = nlen;
+  }
+  memcpy(t->root, t->layers[t->nlayers - 1], sizeof t->root);
+  free(sorted);
+}
+
+void or_merkle_free(or_merkle* t) {
+  for (int i = 0; i < t->nlayers; i++) free(t->layers[i]);
+  free(t->layers);
+  t->layers = NULL;
+}
+
+size_t or_merkle_max_height(const or_merkle* t) { return (size_t)1 << (t->nlayers - 1); }
+
+/* ------------------------------------------------------------------------------------
+ * DuplexChallenger<Val, Perm, 16, 8> [p3-recalled]. */
+void or_ch_init(or_challenger* c) { memset(c, 0, sizeof *c); }
+static void duplex(or_challenger* c) {
+  for (int i = 0; i < c->nin; i++) c->st[i] = c->in[i];
+  c->nin = 0;
+  or_poseidon2_permute(c->st);
+  memcpy(c->out, c->st, 8 * sizeof(fp));
+  c->nout = 8;
+}
+void or_ch_observe(or_challenger* c, fp v) {
+  c->nout = 0;
+  c->in[c->nin++] = v;
+  if (c->nin == 8) duplex(c);
+}
+void or_ch_observe_digest(or_challenger* c, const fp d[8]) {
+  for (int i = 0; i < 8; i++) or_ch_observe(c, d[i]);
+}
+void or_ch_observe_ef(or_challenger* c, ef v) {
+  for (int i = 0; i < 4; i++) or_ch_observe(c, v.c[i]);
+}
+fp or_ch_sample(or_challenger* c) {
+  if (c->nin > 0 || c->nout == 0) duplex(c);
+  return c->out[--c->nout];
+}
+ef or_ch_sample_ef(or_challenger* c) {
+  ef r;
+  for (int i = 0; i < 4; i++) r.c[i] = or_ch_sample(c);
+  return r;
+}
+uint32_t or_ch_sample_bits(or_challenger* c, int bits) {
+  fp v = or_ch_sample(c);
+  return v & ((1u << bits) - 1);
+}
+int or_ch_check_witness(or_challenger* c, int bits, fp w) {
+  or_ch_observe(c, w);
+  return or_ch_sample_bits(c, bits) == 0;
+}
+/* Grind: the reference uses rayon find_any (nondeterministic); the normal form is the
+ * SMALLEST valid witness.  Leaves the challenger as check_witness(witness) would. */
+fp or_ch_grind(or_challenger* c, int bits) {
+  fp found = 0;
+  for (fp w = 0; w < OR_P; w++) {
+    or_challenger t = *c;
+    if (or_ch_check_witness(&t, bits, w)) { found = w; break; }
+  }
+  or_ch_check_witness(c, bits, found);
+  return found;
+}
