@@ -1,0 +1,83 @@
+/*
+ * bfz — C ABI of the MI355X core-proof prover for the felicityin/zkvm-brainfuck zkVM.
+ *
+ * This is the drop-in boundary.  Each entry point replaces one reference interface
+ * (paths relative to the reference repository):
+ *
+ *   bfz_execute      ProverClient::execute().run()        crates/sdk/src/lib.rs:57-59,
+ *                    -> BfProver::execute                 crates/prover/src/lib.rs:60-65
+ *   bfz_setup        ProverClient::setup / MachineProver::setup
+ *                                                         crates/sdk/src/lib.rs:133-135,
+ *                                                         crates/stark/src/prover.rs:49,197,
+ *                                                         crates/stark/src/machine.rs:154-224
+ *   bfz_prove        ProverClient::prove().run() / MachineProver::prove
+ *                                                         crates/sdk/src/action.rs:58-61,
+ *                                                         crates/stark/src/prover.rs:112,560-582
+ *   bfz_verify       ProverClient::verify / StarkMachine::verify
+ *                                                         crates/sdk/src/lib.rs:110-116,
+ *                                                         crates/stark/src/machine.rs:258-284
+ *   bfz_commit       MachineProver::commit -> Pcs::commit (coset LDE + MerkleTreeMmcs)
+ *                                                         crates/stark/src/prover.rs:209-236
+ *   bfz_coset_lde    Radix2DitParallel::coset_lde_batch + bit_reverse_rows (inside
+ *                    TwoAdicFriPcs::commit, called at prover.rs:227,334,411)
+ *   bfz_poseidon2_permute  Poseidon2KoalaBear<16> (kb31_poseidon2.rs:35-50)
+ *
+ * Conventions: field elements are uint32_t in MONTGOMERY form (x * 2^32 mod p), i.e.
+ * byte-identical to a Rust `[KoalaBear]` slice; matrices are row-major.  Every function
+ * returns 0 on success and a negative status on failure (bfz_last_error() describes it);
+ * the Rust wrapper panics on a non-zero status, matching the reference (which unwraps).
+ * Calls are serialized internally; one process-wide context drives one GPU.
+ * Proofs are byte strings in the BFZ1 normal form described in DESIGN.md.
+ */
+#ifndef BFZ_H
+#define BFZ_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct bfz_pk bfz_pk;         /* device-resident proving key (DeviceProvingKey) */
+typedef struct bfz_record bfz_record; /* executed record with traces resident in HBM  */
+
+typedef struct {
+  double upload_ms, main_commit_ms, perm_ms, quotient_ms, open_ms, fri_ms, total_ms;
+  double lde_ms, lde_bytes;
+  int lde_calls;
+} bfz_timings;
+
+int bfz_init(int device);
+const char* bfz_last_error(void);
+int bfz_device_name(char* buf, size_t cap);
+void bfz_free(void* p);
+
+int bfz_execute(const char* elf, const uint8_t* stdin_data, size_t nin, uint8_t* out,
+                size_t out_cap, size_t* out_len, uint64_t* cycles);
+
+int bfz_setup(const char* elf, bfz_pk** pk, uint32_t vk_commit[8]);
+void bfz_pk_free(bfz_pk* pk);
+
+int bfz_prove(const bfz_pk* pk, const uint8_t* stdin_data, size_t nin, uint8_t** proof,
+              size_t* proof_len);
+int bfz_verify(const char* elf, const uint32_t vk_commit[8], const uint8_t* proof,
+               size_t proof_len);
+
+/* Split prove: execute + generate traces + upload (untimed), then prove from HBM. */
+int bfz_record_new(const bfz_pk* pk, const uint8_t* stdin_data, size_t nin, bfz_record** rec,
+                   uint64_t* cycles);
+int bfz_record_prove(const bfz_pk* pk, const bfz_record* rec, uint8_t** proof, size_t* proof_len,
+                     bfz_timings* timings);
+void bfz_record_free(bfz_record* rec);
+
+int bfz_set_num_queries(int num_queries); /* FRI_QUERIES (kb31_poseidon2.rs:59-62) */
+
+int bfz_coset_lde(const uint32_t* evals, size_t n, size_t w, uint32_t shift, uint32_t* lde_out);
+int bfz_commit(const uint32_t* const* mats, const size_t* heights, const size_t* widths,
+               size_t nmats, uint32_t root[8]);
+int bfz_poseidon2_permute(uint32_t* states, size_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -29,15 +29,17 @@ def main() -> int:
     if len(vals) != 480:
         print(f"expected 480 constants, got {len(vals)}", file=sys.stderr)
         return 1
-    out = os.path.join(HERE, "rc_16_30.inc")
-    with open(out, "w") as f:
+    outs = [os.path.join(HERE, "rc_16_30.inc"),
+            os.path.join(HERE, "..", "zkvm-brainfuck_amd", "csrc", "rc_16_30.inc")]
+    for out in outs:
+      with open(out, "w") as f:
         f.write("/* Poseidon2 KoalaBear width-16 round constants RC_16_30 (30 x 16, raw u32,\n"
                 " * reduce mod p = from_wrapped_u32).  Data extracted by oracle/gen_constants.py\n"
                 " * from crates/primitives/src/lib.rs:13-555 of the reference. */\n")
         for r in range(30):
             row = vals[16 * r:16 * r + 16]
             f.write("  " + ", ".join(f"{v}u" for v in row) + ",\n")
-    print(f"wrote {out}")
+      print(f"wrote {out}")
     return 0
 
 

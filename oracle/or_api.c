@@ -47,6 +47,14 @@ int or_api_verify(const char* program, const uint8_t* proof, size_t len) {
 
 void or_api_free(void* p) { free(p); }
 
+int or_api_setup_root(const char* program, uint32_t root[8]) {
+  or_program p;
+  if (or_parse_program(program, &p)) return -1;
+  or_setup_root(&p, root);
+  free(p.ins);
+  return 0;
+}
+
 int or_api_trace(const char* program, const uint8_t* in, size_t nin, int chip, int prep,
                  uint32_t** out, size_t* h, size_t* w) {
   or_program p;

@@ -11,6 +11,8 @@ int or_prove_record(const or_program* prog, or_record* rec, uint8_t** out, size_
                     or_timing* tm);
 int or_verify_proof(const or_program* prog, const uint8_t* proof, size_t len);
 void or_set_num_queries(int q);
+void or_setup_root(const or_program* p, uint32_t root[8]);
+int or_api_setup_root(const char* program, uint32_t root[8]);
 
 /* ctypes-facing API (canonical u32 field values everywhere) */
 int or_api_execute(const char* program, const uint8_t* in, size_t nin, uint8_t* out,

@@ -506,6 +506,14 @@ int or_prove_record(const or_program* prog, or_record* rec, uint8_t** out, size_
   return 0;
 }
 
+/* Preprocessed commitment (vk.commit) for a program, canonical form. */
+void or_setup_root(const or_program* p, uint32_t root[8]) {
+  pk_t pk;
+  setup(p, &pk);
+  memcpy(root, pk.prep.tree.root, 32);
+  round_free(&pk.prep, 1);
+}
+
 /* ====================================================================== verifier */
 typedef struct { const uint8_t* p; size_t n, off; int err; } rd;
 static uint32_t ru32(rd* r) {

@@ -1,0 +1,131 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle, bit for bit."""
+import ctypes
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from bfz import _lib, guests, sdk
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))
+P = O.P
+P32 = ctypes.POINTER(ctypes.c_uint32)
+
+
+def mont(a):
+    return ((np.asarray(a, dtype=np.uint64) << np.uint64(32)) % np.uint64(P)).astype(np.uint32)
+
+
+def unmont(a):
+    inv = pow(2, -32, P)
+    return ((np.asarray(a, dtype=np.uint64) * np.uint64(inv)) % np.uint64(P)).astype(np.uint32)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu():
+    _lib.init(0)
+    yield
+
+
+def test_poseidon2_batch_parity():
+    rng = np.random.default_rng(1)
+    st = rng.integers(0, P, size=(4096, 16), dtype=np.uint64).astype(np.uint32)
+    for kat in GOLDEN["poseidon2"]:
+        st[: 1] = np.array(kat["in"], dtype=np.uint32)
+        dev = mont(st).reshape(-1).copy()
+        _lib.check(_lib.lib().bfz_poseidon2_permute(dev.ctypes.data_as(P32), len(st)))
+        got = unmont(dev).reshape(-1, 16)
+        assert got[0].tolist() == kat["out"]
+        exp = O.poseidon2(st.reshape(-1)).reshape(-1, 16)
+        assert np.array_equal(got, exp)
+
+
+@pytest.mark.parametrize("logn,w", [(0, 3), (1, 2), (4, 31), (5, 1), (10, 45), (13, 7), (16, 4),
+                                    (17, 9), (20, 2)])
+def test_coset_lde_parity(logn, w):
+    rng = np.random.default_rng(logn * 100 + w)
+    n = 1 << logn
+    m = rng.integers(0, P, size=(n, w), dtype=np.uint64).astype(np.uint32)
+    out = np.zeros((2 * n, w), dtype=np.uint32)
+    src = mont(m).copy()
+    _lib.check(_lib.lib().bfz_coset_lde(src.ctypes.data_as(P32), n, w, int(mont([3])[0]),
+                                        out.ctypes.data_as(P32)))
+    exp = O.coset_lde(m, 3)
+    assert np.array_equal(unmont(out), exp)
+
+
+def test_commit_root_parity():
+    rng = np.random.default_rng(7)
+    shapes = [(1 << 12, 31), (1 << 12, 41), (1 << 11, 7), (1 << 9, 45), (16, 5), (16, 12)]
+    mats = [rng.integers(0, P, size=s, dtype=np.uint64).astype(np.uint32) for s in shapes]
+    ldes = [O.coset_lde(m, 3) for m in mats]
+    exp = O.merkle_root(ldes)
+    dev = [mont(m).copy() for m in mats]
+    ptrs = (P32 * len(dev))(*[d.ctypes.data_as(P32) for d in dev])
+    hs = (ctypes.c_size_t * len(dev))(*[s[0] for s in shapes])
+    ws = (ctypes.c_size_t * len(dev))(*[s[1] for s in shapes])
+    root = (ctypes.c_uint32 * 8)()
+    _lib.check(_lib.lib().bfz_commit(ptrs, hs, ws, len(dev), root))
+    assert unmont(list(root)).tolist() == exp
+
+
+@pytest.fixture(scope="module")
+def client():
+    return sdk.ProverClient()
+
+
+@pytest.mark.parametrize("name,prog,stdin", guests.REFERENCE_PROGRAMS)
+def test_proof_bytes_match_oracle(client, name, prog, stdin):
+    pk, vk = client.setup(prog)
+    g = [x for x in GOLDEN["proofs"] if x["name"] == name][0]
+    assert unmont(vk.commit).tolist() == g["vk_commit"]
+    pf = client.prove(pk, stdin).run()
+    assert hashlib.sha256(pf.proof).hexdigest() == g["sha256"], "differs from the oracle fixture"
+    assert pf.proof == O.prove(prog, stdin)
+    client.verify(pf, vk)                      # product host verifier
+    assert O.verify(prog, pf.proof)            # oracle verifier
+
+
+def test_fibo17_end_to_end_sdk(client):
+    """crates/sdk/src/lib.rs:186-196 test_e2e_core, through the SDK mirror."""
+    pk, vk = client.setup(guests.FIBO)
+    assert client.execute(guests.FIBO, [17]).run()[0] == 85
+    proof = client.prove(pk, [17]).run()
+    client.verify(proof, vk)
+
+
+def test_fibo255_2pow20_parity(client):
+    """fibonacci trace 2^20 rows (BASELINE config 3): full pipeline, bit-exact vs oracle."""
+    pk, vk = client.setup(guests.FIBO)
+    pf = client.prove(pk, [255]).run()
+    client.verify(pf, vk)
+    assert pf.proof == O.prove(guests.FIBO, [255])
+
+
+@pytest.mark.slow
+def test_fibo_x4_2pow22_properties(client):
+    """Headline size (2^22 Cpu rows): size-independent properties — host verifier and oracle
+    verifier accept, the proof is deterministic, tampering is rejected."""
+    pk, vk = client.setup(guests.FIBO_X4)
+    a = client.prove(pk, [255]).run()
+    client.verify(a, vk)
+    assert O.verify(guests.FIBO_X4, a.proof)
+    b = client.prove(pk, [255]).run()
+    assert a.proof == b.proof
+    bad = bytearray(a.proof)
+    bad[len(bad) // 3] ^= 4
+    with pytest.raises(_lib.BfzError):
+        client.verify(sdk.BfProofWithPublicValues(proof=bytes(bad), stdin=b"\xff"), vk)
+
+
+def test_invalid_trace_is_refused(client):
+    """An execution that violates the AIR cannot be proven (reference panics in FRI's final
+    polynomial check).  A memory pointer that wraps below zero breaks the word range check."""
+    pk, vk = client.setup("<+")
+    with pytest.raises(_lib.BfzError):
+        client.prove(pk, []).run()

@@ -1,0 +1,105 @@
+"""ctypes binding of the C ABI declared in include/bfz.h (the drop-in boundary).
+
+The shared library is built in-tree (zkvm-brainfuck_amd/libbfz.so) by
+`make -C zkvm-brainfuck_amd` or __graft_entry__.build().  There is no fallback: if the
+library is missing, importing anything that proves raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, byref, c_char_p, c_double, c_int, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(HERE), "libbfz.so")
+
+
+class BfzError(RuntimeError):
+    """A negative status returned by the C ABI (message from bfz_last_error)."""
+
+
+class Timings(ctypes.Structure):
+    _fields_ = [
+        ("upload_ms", c_double), ("main_commit_ms", c_double), ("perm_ms", c_double),
+        ("quotient_ms", c_double), ("open_ms", c_double), ("fri_ms", c_double),
+        ("total_ms", c_double), ("lde_ms", c_double), ("lde_bytes", c_double),
+        ("lde_calls", c_int),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+# (name, restype, argtypes) for every symbol declared in include/bfz.h
+SIGNATURES = [
+    ("bfz_init", c_int, [c_int]),
+    ("bfz_last_error", c_char_p, []),
+    ("bfz_device_name", c_int, [c_char_p, c_size_t]),
+    ("bfz_free", None, [c_void_p]),
+    ("bfz_execute", c_int, [c_char_p, POINTER(c_uint8), c_size_t, POINTER(c_uint8), c_size_t,
+                            POINTER(c_size_t), POINTER(c_uint64)]),
+    ("bfz_setup", c_int, [c_char_p, POINTER(c_void_p), POINTER(c_uint32)]),
+    ("bfz_pk_free", None, [c_void_p]),
+    ("bfz_prove", c_int, [c_void_p, POINTER(c_uint8), c_size_t, POINTER(POINTER(c_uint8)),
+                          POINTER(c_size_t)]),
+    ("bfz_verify", c_int, [c_char_p, POINTER(c_uint32), POINTER(c_uint8), c_size_t]),
+    ("bfz_record_new", c_int, [c_void_p, POINTER(c_uint8), c_size_t, POINTER(c_void_p),
+                               POINTER(c_uint64)]),
+    ("bfz_record_prove", c_int, [c_void_p, c_void_p, POINTER(POINTER(c_uint8)), POINTER(c_size_t),
+                                 POINTER(Timings)]),
+    ("bfz_record_free", None, [c_void_p]),
+    ("bfz_set_num_queries", c_int, [c_int]),
+    ("bfz_coset_lde", c_int, [POINTER(c_uint32), c_size_t, c_size_t, c_uint32, POINTER(c_uint32)]),
+    ("bfz_commit", c_int, [POINTER(POINTER(c_uint32)), POINTER(c_size_t), POINTER(c_size_t),
+                           c_size_t, POINTER(c_uint32)]),
+    ("bfz_poseidon2_permute", c_int, [POINTER(c_uint32), c_size_t]),
+]
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise BfzError(f"{LIB_PATH} not built: run `make -C zkvm-brainfuck_amd` "
+                           "(or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(status: int) -> None:
+    if status != 0:
+        msg = lib().bfz_last_error()
+        raise BfzError(f"bfz status {status}: {msg.decode() if msg else ''}")
+
+
+def u8buf(data: bytes):
+    data = bytes(data)
+    return (c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0"), len(data)
+
+
+_initialized = None
+
+
+def init(device: int = 0) -> None:
+    global _initialized
+    if _initialized != device:
+        check(lib().bfz_init(device))
+        _initialized = device
+
+
+def take_bytes(ptr, n: int) -> bytes:
+    try:
+        return ctypes.string_at(ptr, n)
+    finally:
+        lib().bfz_free(ptr)
+
+
+__all__ = ["lib", "check", "init", "u8buf", "take_bytes", "BfzError", "Timings", "LIB_PATH",
+           "SIGNATURES", "byref"]

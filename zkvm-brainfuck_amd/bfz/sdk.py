@@ -1,0 +1,122 @@
+"""Python mirror of the reference SDK (crates/sdk/src/lib.rs, action.rs, proof.rs) over the
+bfz C ABI.  Same names, argument meaning and error behaviour:
+
+    client = ProverClient()                      # ProverClient::new        lib.rs:31-33
+    out = client.execute(elf, stdin).run()       # ProverClient::execute    lib.rs:57-59
+    pk, vk = client.setup(elf)                   # ProverClient::setup      lib.rs:133-135
+    proof = client.prove(pk, stdin).run()        # ProverClient::prove      lib.rs:92-94
+    client.verify(proof, vk)                     # ProverClient::verify     lib.rs:110-116
+
+Errors raise (the reference returns Err / panics in the same places).  Proving runs on the GPU
+through libbfz; verification runs the host verifier compiled into the same library.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+from . import _lib
+from ._lib import BfzError, check, init, lib, take_bytes, u8buf
+
+
+@dataclass
+class BfVerifyingKey:
+    """StarkVerifyingKey: preprocessed commitment (Montgomery u32 x 8) + the program that
+    determines chip_information (crates/prover/src/types.rs:17-20)."""
+    commit: List[int]
+    elf: str
+
+
+@dataclass
+class BfProvingKey:
+    """BfProvingKey (crates/prover/src/types.rs:8-15): device-resident pk + elf + vk."""
+    handle: int
+    elf: str
+    vk: BfVerifyingKey
+
+    def __del__(self):
+        try:
+            if self.handle:
+                lib().bfz_pk_free(ctypes.c_void_p(self.handle))
+                self.handle = 0
+        except Exception:
+            pass
+
+
+@dataclass
+class BfProofWithPublicValues:
+    """crates/sdk/src/proof.rs:10-13 — the proof (BFZ1 normal-form bytes) and stdin."""
+    proof: bytes
+    stdin: bytes
+    public_values: bytes = b""
+    cycles: int = 0
+
+
+class Execute:
+    """action::Execute (crates/sdk/src/action.rs:10-33)."""
+
+    def __init__(self, elf: str, stdin: bytes):
+        self.elf, self.stdin = elf, bytes(stdin)
+
+    def run(self) -> bytes:
+        buf, n = u8buf(self.stdin)
+        cap = 1 << 20
+        out = (ctypes.c_uint8 * cap)()
+        olen = ctypes.c_size_t()
+        cyc = ctypes.c_uint64()
+        check(lib().bfz_execute(self.elf.encode(), buf, n, out, cap, ctypes.byref(olen),
+                                ctypes.byref(cyc)))
+        return bytes(out[: min(olen.value, cap)])
+
+
+class Prove:
+    """action::Prove (crates/sdk/src/action.rs:35-61)."""
+
+    def __init__(self, pk: BfProvingKey, stdin: bytes):
+        self.pk, self.stdin = pk, bytes(stdin)
+
+    def run(self) -> BfProofWithPublicValues:
+        init()
+        buf, n = u8buf(self.stdin)
+        ptr = ctypes.POINTER(ctypes.c_uint8)()
+        plen = ctypes.c_size_t()
+        check(lib().bfz_prove(ctypes.c_void_p(self.pk.handle), buf, n, ctypes.byref(ptr),
+                              ctypes.byref(plen)))
+        return BfProofWithPublicValues(proof=take_bytes(ptr, plen.value), stdin=self.stdin,
+                                       public_values=Execute(self.pk.elf, self.stdin).run())
+
+
+class ProverClient:
+    """crates/sdk/src/lib.rs:20-136, backed by the MI355X prover."""
+
+    def __init__(self, device: int = 0):
+        self.device = device
+
+    @staticmethod
+    def new() -> "ProverClient":
+        return ProverClient()
+
+    def execute(self, elf: str, stdin) -> Execute:
+        return Execute(elf, bytes(stdin))
+
+    def setup(self, elf: str):
+        init(self.device)
+        h = ctypes.c_void_p()
+        commit = (ctypes.c_uint32 * 8)()
+        check(lib().bfz_setup(elf.encode(), ctypes.byref(h), commit))
+        vk = BfVerifyingKey(commit=list(commit), elf=elf)
+        return BfProvingKey(handle=h.value, elf=elf, vk=vk), vk
+
+    def prove(self, pk: BfProvingKey, stdin) -> Prove:
+        return Prove(pk, bytes(stdin))
+
+    def verify(self, proof: BfProofWithPublicValues, vk: BfVerifyingKey) -> None:
+        buf, n = u8buf(proof.proof)
+        commit = (ctypes.c_uint32 * 8)(*vk.commit)
+        check(lib().bfz_verify(vk.elf.encode(), commit, buf, n))
+
+
+def set_num_queries(q: int) -> None:
+    """FRI_QUERIES override (crates/stark/src/kb31_poseidon2.rs:59-62)."""
+    check(lib().bfz_set_num_queries(int(q)))

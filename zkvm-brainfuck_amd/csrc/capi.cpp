@@ -1,0 +1,227 @@
+// extern "C" boundary (include/bfz.h).  Exceptions never cross it: every entry point
+// catches, records the message for bfz_last_error(), and returns a negative status.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+
+#include "../../include/bfz.h"
+#include "fri.h"
+#include "merkle.h"
+#include "ntt.h"
+#include "prover.h"
+#include "verifier.h"
+
+struct bfz_pk {
+  std::unique_ptr<bfz::ProvingKey> pk;
+};
+struct bfz_record {
+  bfz::DeviceTraces dt;
+  uint64_t cycles = 0;
+};
+
+namespace {
+std::mutex g_mu;
+thread_local std::string g_err;
+int g_num_queries = -1;
+
+int fail(const std::exception& e, int code = -1) {
+  g_err = e.what();
+  return code;
+}
+bfz::ProveOptions opts() {
+  bfz::ProveOptions o;
+  o.num_queries = g_num_queries > 0 ? g_num_queries : bfz::num_queries_from_env();
+  return o;
+}
+template <class F>
+int guarded(F&& f) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  try {
+    return f();
+  } catch (const bfz::HipError& e) {
+    return fail(e, -2);
+  } catch (const std::exception& e) {
+    return fail(e, -1);
+  }
+}
+}  // namespace
+
+extern "C" {
+
+int bfz_init(int device) {
+  return guarded([&] {
+    int n = 0;
+    HIP_CHECK(hipGetDeviceCount(&n));
+    if (n <= 0) throw std::runtime_error("no HIP device");
+    HIP_CHECK(hipSetDevice(device));
+    (void)bfz::stream();
+    return 0;
+  });
+}
+
+const char* bfz_last_error(void) { return g_err.c_str(); }
+
+int bfz_device_name(char* buf, size_t cap) {
+  return guarded([&] {
+    hipDeviceProp_t p;
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    HIP_CHECK(hipGetDeviceProperties(&p, dev));
+    std::snprintf(buf, cap, "%s (%s)", p.name, p.gcnArchName);
+    return 0;
+  });
+}
+
+void bfz_free(void* p) { std::free(p); }
+
+int bfz_execute(const char* elf, const uint8_t* in, size_t nin, uint8_t* out, size_t cap,
+                size_t* out_len, uint64_t* cycles) {
+  return guarded([&] {
+    bfz::Program p = bfz::Program::parse(elf);
+    bfz::ExecutionRecord rec;
+    bfz::execute(p, in, nin, rec);
+    const size_t n = std::min(cap, rec.output.size());
+    if (n) std::memcpy(out, rec.output.data(), n);
+    *out_len = rec.output.size();
+    if (cycles) *cycles = rec.global_clk;
+    return 0;
+  });
+}
+
+int bfz_setup(const char* elf, bfz_pk** pk, uint32_t vk_commit[8]) {
+  return guarded([&] {
+    auto k = std::make_unique<bfz_pk>();
+    k->pk = bfz::setup(elf);
+    if (vk_commit) std::memcpy(vk_commit, k->pk->prep.tree.root, 32);
+    *pk = k.release();
+    return 0;
+  });
+}
+
+void bfz_pk_free(bfz_pk* pk) { delete pk; }
+
+static int emit(std::vector<uint8_t>&& v, uint8_t** proof, size_t* len) {
+  uint8_t* p = (uint8_t*)std::malloc(v.size() ? v.size() : 1);
+  if (!p) throw std::runtime_error("out of host memory");
+  std::memcpy(p, v.data(), v.size());
+  *proof = p;
+  *len = v.size();
+  return 0;
+}
+
+int bfz_prove(const bfz_pk* pk, const uint8_t* in, size_t nin, uint8_t** proof, size_t* len) {
+  return guarded([&] { return emit(bfz::prove(*pk->pk, in, nin, opts(), nullptr), proof, len); });
+}
+
+int bfz_verify(const char* elf, const uint32_t vk_commit[8], const uint8_t* proof, size_t len) {
+  return guarded([&] {
+    std::string why;
+    const int nq = g_num_queries > 0 ? g_num_queries : bfz::num_queries_from_env();
+    if (!bfz::verify_proof(elf, vk_commit, proof, len, nq, &why)) {
+      g_err = "verification failed: " + why;
+      return -3;
+    }
+    return 0;
+  });
+}
+
+int bfz_record_new(const bfz_pk* pk, const uint8_t* in, size_t nin, bfz_record** rec,
+                   uint64_t* cycles) {
+  return guarded([&] {
+    auto r = std::make_unique<bfz_record>();
+    bfz::ExecutionRecord er;
+    bfz::execute(pk->pk->program, in, nin, er);
+    bfz::generate_dependencies(er);
+    bfz::upload_traces(er, r->dt, bfz::stream());
+    r->cycles = er.global_clk;
+    if (cycles) *cycles = er.global_clk;
+    *rec = r.release();
+    return 0;
+  });
+}
+
+int bfz_record_prove(const bfz_pk* pk, const bfz_record* rec, uint8_t** proof, size_t* len,
+                     bfz_timings* t) {
+  return guarded([&] {
+    bfz::ProveOptions o = opts();
+    o.timing = t != nullptr;
+    bfz::StageTimes st;
+    auto v = bfz::prove_device(*pk->pk, const_cast<bfz::DeviceTraces&>(rec->dt), o, &st);
+    if (t) {
+      t->upload_ms = st.upload;
+      t->main_commit_ms = st.main_commit;
+      t->perm_ms = st.perm;
+      t->quotient_ms = st.quotient;
+      t->open_ms = st.open;
+      t->fri_ms = st.fri;
+      t->total_ms = st.total;
+      t->lde_ms = st.lde_ms;
+      t->lde_bytes = st.lde_bytes;
+      t->lde_calls = st.lde_calls;
+    }
+    return emit(std::move(v), proof, len);
+  });
+}
+
+void bfz_record_free(bfz_record* rec) { delete rec; }
+
+int bfz_set_num_queries(int q) {
+  g_num_queries = q;
+  return 0;
+}
+
+int bfz_coset_lde(const uint32_t* evals, size_t n, size_t w, uint32_t shift, uint32_t* out) {
+  return guarded([&] {
+    if (n == 0 || (n & (n - 1))) throw std::runtime_error("height must be a power of two");
+    hipStream_t st = bfz::stream();
+    bfz::DBuf<uint32_t> rm(n * w), ev(n * w), lde(2 * n * w), back(2 * n * w);
+    HIP_CHECK(hipMemcpyAsync(rm.p, evals, n * w * 4, hipMemcpyHostToDevice, st));
+    bfz::transpose_bitrev(rm.p, n, (int)w, ev.p, st);
+    bfz::coset_lde(ev.p, n, (int)w, shift, lde.p, st);
+    bfz::transpose_to_rowmajor(lde.p, 2 * n, (int)w, back.p, st);
+    HIP_CHECK(hipMemcpyAsync(out, back.p, 2 * n * w * 4, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    return 0;
+  });
+}
+
+int bfz_commit(const uint32_t* const* mats, const size_t* heights, const size_t* widths,
+               size_t nmats, uint32_t root[8]) {
+  return guarded([&] {
+    hipStream_t st = bfz::stream();
+    bfz::Round r;
+    r.mats.resize(nmats);
+    std::vector<bfz::DBuf<uint32_t>> evs(nmats);
+    for (size_t i = 0; i < nmats; i++) {
+      const size_t n = heights[i], w = widths[i];
+      if (n == 0 || (n & (n - 1))) throw std::runtime_error("height must be a power of two");
+      bfz::DBuf<uint32_t> rm(n * w);
+      evs[i].reset(n * w);
+      HIP_CHECK(hipMemcpyAsync(rm.p, mats[i], n * w * 4, hipMemcpyHostToDevice, st));
+      bfz::transpose_bitrev(rm.p, n, (int)w, evs[i].p, st);
+      HIP_CHECK(hipStreamSynchronize(st));
+      bfz::commit_lde(r.mats[i], evs[i].p, n, (int)w, kb::ONE, st);
+    }
+    r.commit(st);
+    std::memcpy(root, r.tree.root, 32);
+    return 0;
+  });
+}
+
+int bfz_poseidon2_permute(uint32_t* states, size_t n) {
+  return guarded([&] {
+    hipStream_t st = bfz::stream();
+    bfz::DBuf<uint32_t> d(16 * n);
+    HIP_CHECK(hipMemcpyAsync(d.p, states, 16 * n * 4, hipMemcpyHostToDevice, st));
+    bfz::poseidon2_batch(d.p, n, st);
+    HIP_CHECK(hipMemcpyAsync(states, d.p, 16 * n * 4, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    return 0;
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,36 @@
+// Device PCS-open / FRI kernels (see fri.hip).
+#pragma once
+#include <vector>
+
+#include "gpu.h"
+
+namespace bfz {
+
+struct RedCol {            // one committed column at a given LDE height
+  const uint32_t* col;     // device column (bit-reversed rows)
+  kb::EF ca, cb;           // alpha-power coefficients for the two opening points
+  int has_b;
+  int pad[3];
+};
+
+struct GrindState {        // DuplexChallenger state at grind time
+  uint32_t st[16];
+  uint32_t in[8];
+  int nin;
+};
+
+// out[t] = 1 / (x_t - z), x_t = 3 * w_H^bitrev(t), t < 2^logH
+void inv_denoms(const kb::EF& z, int logH, kb::EF* out, hipStream_t st);
+// out_dev[c] = value at z of column c of a committed LDE (height = 2n), via the low coset.
+void open_matrix(const uint32_t* mat, size_t height, int w, const kb::EF* invd,
+                 const kb::EF& scale, kb::EF* out_dev, hipStream_t st);
+// ro[t] += (sum_c ca_c v_c[t] - ya) invd_a[t] + (sum_c cb_c v_c[t] - yb) invd_b[t]
+void reduce_height(const std::vector<RedCol>& cols, size_t H, const kb::EF* invd_a,
+                   const kb::EF* invd_b, const kb::EF& ya, const kb::EF& yb, bool has_b,
+                   kb::EF* ro, hipStream_t st);
+void fri_fold(const kb::EF* in, kb::EF* out, size_t h, const kb::EF& beta, const kb::EF* add,
+              hipStream_t st);
+uint32_t grind(const GrindState& gs, int bits, hipStream_t st);
+void gather_words(const std::vector<uint64_t>& addrs, std::vector<uint32_t>& out, hipStream_t st);
+
+}  // namespace bfz

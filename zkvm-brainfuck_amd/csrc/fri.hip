@@ -1,0 +1,268 @@
+// PCS opening on the device: TwoAdicFriPcs::open + fri::prover::prove [p3-recalled],
+// called from crates/stark/src/prover.rs:460-470.
+//
+//  * inverse denominators 1/(x_t - z) over the largest coset, bit-reversed order
+//    (compute_inverse_denominators); smaller heights use prefixes.
+//  * opened values p(z) by barycentric interpolation over the low coset 3*H_n, which is the
+//    first n rows of the bit-reversed LDE:  p(z) = (z^n - 3^n)/(n 3^n) * sum_t p_t x_t/(z-x_t)
+//  * reduced openings per height:  ro[t] = sum_(mat,point) alpha^off sum_k alpha^k
+//    (p_k(x_t) - y_k) / (x_t - z)
+//  * FRI commit-phase fold: (1/2 + beta/2 g^-rev(i)) lo + (1/2 - beta/2 g^-rev(i)) hi
+//  * proof-of-work grind over the challenger state (smallest witness = normal form)
+#include "fri.h"
+
+#include "poseidon2.h"
+
+namespace bfz {
+
+using namespace kb;
+
+__device__ __forceinline__ uint32_t coset_point(uint32_t t, int logH, const uint32_t* twf) {
+  // x_t = 3 * w_H^bitrev(t); w_H^j = twf[H/2 + j] for j < H/2, -twf[j] otherwise
+  if (logH == 0) return to_mont_c(3);
+  const uint32_t j = dbitrev(t, logH), half = 1u << (logH - 1);
+  const uint32_t w = j < half ? twf[half + j] : mneg(twf[j]);
+  return mmul(to_mont_c(3), w);
+}
+
+constexpr int INV_CHUNK = 8;
+
+__global__ __launch_bounds__(256) void k_inv_denoms(EF z, int logH, const uint32_t* __restrict__ twf,
+                                                    EF* __restrict__ out) {
+  const size_t H = (size_t)1 << logH;
+  const size_t base = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * INV_CHUNK;
+  if (base >= H) return;
+  EF d[INV_CHUNK], pre[INV_CHUNK];
+  const int cnt = (int)min((size_t)INV_CHUNK, H - base);
+  EF run = ef_one();
+#pragma unroll
+  for (int k = 0; k < INV_CHUNK; k++) {
+    if (k < cnt) {
+      d[k] = ef_sub(ef_base(coset_point((uint32_t)(base + k), logH, twf)), z);
+      run = ef_mul(run, d[k]);
+    }
+    pre[k] = run;
+  }
+  EF inv = ef_inv(run);
+#pragma unroll
+  for (int k = INV_CHUNK - 1; k >= 0; k--) {
+    if (k < cnt) {
+      out[base + k] = k ? ef_mul(inv, pre[k - 1]) : inv;
+      inv = ef_mul(inv, d[k]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ openings
+constexpr int OPEN_T = 256, OPEN_R = 4, OPEN_CH = OPEN_T * OPEN_R;
+
+__device__ __forceinline__ EF wave_sum(EF v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int e = 0; e < 4; e++) v.c[e] = madd(v.c[e], __shfl_xor(v.c[e], off, 64));
+  return v;
+}
+
+// partial[chunk * w + c] = sum_{t in chunk} W_t * col_c[t],  W_t = -x_t * invd[t]
+__global__ __launch_bounds__(OPEN_T) void k_open_partial(const uint32_t* __restrict__ mat,
+                                                         size_t height, int w, size_t n, int logH,
+                                                         const EF* __restrict__ invd,
+                                                         const uint32_t* __restrict__ twf,
+                                                         EF* __restrict__ partial) {
+  __shared__ EF sh[OPEN_T / 64][64];
+  const size_t c0 = (size_t)blockIdx.x * OPEN_CH;
+  EF W[OPEN_R];
+  size_t rows[OPEN_R];
+#pragma unroll
+  for (int r = 0; r < OPEN_R; r++) {
+    const size_t t = c0 + (size_t)r * OPEN_T + threadIdx.x;
+    rows[r] = t;
+    if (t < n) {
+      const uint32_t x = coset_point((uint32_t)t, logH, twf);
+      W[r] = ef_neg(ef_mul_base(invd[t], x));
+    } else {
+      W[r] = ef_zero();
+    }
+  }
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int cb = 0; cb < w; cb += 64) {
+    const int cw = min(64, w - cb);
+    for (int c = 0; c < cw; c++) {
+      const uint32_t* col = mat + (size_t)(cb + c) * height;
+      EF acc = ef_zero();
+#pragma unroll
+      for (int r = 0; r < OPEN_R; r++)
+        if (rows[r] < n) acc = ef_add(acc, ef_mul_base(W[r], col[rows[r]]));
+      acc = wave_sum(acc);
+      if (lane == 0) sh[wave][c] = acc;
+    }
+    __syncthreads();
+    if (threadIdx.x < (unsigned)cw) {
+      EF s = sh[0][threadIdx.x];
+#pragma unroll
+      for (int k = 1; k < OPEN_T / 64; k++) s = ef_add(s, sh[k][threadIdx.x]);
+      partial[(size_t)blockIdx.x * w + cb + threadIdx.x] = s;
+    }
+    __syncthreads();
+  }
+}
+
+// out[c] = scale * sum_chunks partial[chunk * w + c]   (one block per column)
+__global__ __launch_bounds__(256) void k_open_final(const EF* __restrict__ partial, int nchunks,
+                                                    int w, EF scale, EF* __restrict__ out) {
+  __shared__ EF sh[4];
+  const int c = blockIdx.x;
+  EF s = ef_zero();
+  for (int k = threadIdx.x; k < nchunks; k += blockDim.x) s = ef_add(s, partial[(size_t)k * w + c]);
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    EF tot = sh[0];
+    for (int k = 1; k < (int)(blockDim.x / 64); k++) tot = ef_add(tot, sh[k]);
+    out[c] = ef_mul(tot, scale);
+  }
+}
+
+// ------------------------------------------------------------------ reduced openings
+__global__ __launch_bounds__(256) void k_reduce(const RedCol* __restrict__ cols, int ncols,
+                                                size_t H, const EF* __restrict__ invd_a,
+                                                const EF* __restrict__ invd_b, EF ya, EF yb,
+                                                int has_b, EF* __restrict__ ro) {
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < H;
+       t += (size_t)gridDim.x * blockDim.x) {
+    EF sa = ef_zero(), sb = ef_zero();
+    for (int c = 0; c < ncols; c++) {
+      const RedCol rc = cols[c];
+      const uint32_t v = rc.col[t];
+      sa = ef_add(sa, ef_mul_base(rc.ca, v));
+      if (rc.has_b) sb = ef_add(sb, ef_mul_base(rc.cb, v));
+    }
+    EF r = ef_mul(ef_sub(sa, ya), invd_a[t]);
+    if (has_b) r = ef_add(r, ef_mul(ef_sub(sb, yb), invd_b[t]));
+    ro[t] = ef_add(ro[t], r);
+  }
+}
+
+// ------------------------------------------------------------------ FRI fold
+__global__ __launch_bounds__(256) void k_fri_fold(const EF* __restrict__ in, EF* __restrict__ out,
+                                                  size_t h, int logh, EF half_beta,
+                                                  const uint32_t* __restrict__ twi,
+                                                  const EF* __restrict__ add) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= h) return;
+  // g_inv^rev(i) with g = w_(2h): twi[h + j] = w_(2h)^-j
+  const uint32_t g = twi[h + dbitrev((uint32_t)i, logh)];
+  const EF p = ef_mul_base(half_beta, g);
+  const uint32_t halfv = to_mont_c((P + 1) / 2);
+  const EF lo = in[2 * i], hi = in[2 * i + 1];
+  EF r = ef_add(ef_mul(ef_add_base(p, halfv), lo), ef_mul(ef_sub(ef_base(halfv), p), hi));
+  if (add) r = ef_add(r, add[i]);
+  out[i] = r;
+}
+
+// ------------------------------------------------------------------ grind
+// Challenger state: sponge state st[16], pending inputs in[0..nin).  observe(w) then
+// sample_bits(bits) == 0  <=>  perm(st with in[0..nin), w written at 0..nin)[7] low bits 0.
+__global__ __launch_bounds__(256) void k_grind(GrindState gs, uint32_t start, uint32_t bits,
+                                               uint32_t* __restrict__ best) {
+  const uint32_t w = start + blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= P) return;
+  uint32_t s[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) s[i] = gs.st[i];
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    if (i < gs.nin) s[i] = gs.in[i];
+  const uint32_t wm = to_mont(w);
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    if (i == gs.nin) s[i] = wm;
+  poseidon2_permute(s);
+  const uint32_t v = from_mont(s[7]);
+  if ((v & ((1u << bits) - 1)) == 0) atomicMin(best, w);
+}
+
+// ------------------------------------------------------------------ gather
+__global__ __launch_bounds__(256) void k_gather_words(const uint64_t* __restrict__ addrs, size_t n,
+                                                      uint32_t* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = *reinterpret_cast<const uint32_t*>(addrs[i]);
+}
+
+// ================================================================== host wrappers
+void inv_denoms(const EF& z, int logH, EF* out, hipStream_t st) {
+  twiddles().ensure(std::max(logH, 1));
+  const size_t H = (size_t)1 << logH;
+  const size_t nthreads = (H + INV_CHUNK - 1) / INV_CHUNK;
+  hipLaunchKernelGGL(k_inv_denoms, dim3(ceil_div(nthreads, 256)), dim3(256), 0, st, z, logH,
+                     (const uint32_t*)twiddles().fwd.p, out);
+  KCHECK();
+}
+
+void open_matrix(const uint32_t* mat, size_t height, int w, const EF* invd, const EF& scale,
+                 EF* out_dev, hipStream_t st) {
+  const size_t n = height / 2;  // low coset = first half of the bit-reversed LDE
+  const int logH = log2i(height);
+  const int nchunks = (int)ceil_div(n, OPEN_CH);
+  DBuf<EF> partial((size_t)nchunks * w);
+  hipLaunchKernelGGL(k_open_partial, dim3(nchunks), dim3(OPEN_T), 0, st, mat, height, w, n, logH,
+                     invd, (const uint32_t*)twiddles().fwd.p, partial.p);
+  KCHECK();
+  hipLaunchKernelGGL(k_open_final, dim3(w), dim3(256), 0, st, (const EF*)partial.p, nchunks, w,
+                     scale, out_dev);
+  KCHECK();
+}
+
+void reduce_height(const std::vector<RedCol>& cols, size_t H, const EF* invd_a, const EF* invd_b,
+                   const EF& ya, const EF& yb, bool has_b, EF* ro, hipStream_t st) {
+  DBuf<RedCol> d(cols.size());
+  HIP_CHECK(hipMemcpyAsync(d.p, cols.data(), cols.size() * sizeof(RedCol), hipMemcpyHostToDevice, st));
+  HIP_CHECK(hipStreamSynchronize(st));  // host vector may go away
+  const unsigned grid = std::min<unsigned>(ceil_div(H, 256), 8192);
+  hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(256), 0, st, (const RedCol*)d.p, (int)cols.size(), H,
+                     invd_a, invd_b, ya, yb, has_b ? 1 : 0, ro);
+  KCHECK();
+}
+
+void fri_fold(const EF* in, EF* out, size_t h, const EF& beta, const EF* add, hipStream_t st) {
+  const int logh = log2i(h);
+  twiddles().ensure(logh + 1);
+  const EF half_beta = ef_mul_base(beta, to_mont_c((P + 1) / 2));
+  hipLaunchKernelGGL(k_fri_fold, dim3(ceil_div(h, 256)), dim3(256), 0, st, in, out, h, logh,
+                     half_beta, (const uint32_t*)twiddles().inv.p, add);
+  KCHECK();
+}
+
+uint32_t grind(const GrindState& gs, int bits, hipStream_t st) {
+  DBuf<uint32_t> best(1);
+  const uint32_t chunk = 1u << 22;
+  for (uint64_t start = 0; start < P; start += chunk) {
+    const uint32_t init = 0xffffffffu;
+    HIP_CHECK(hipMemcpyAsync(best.p, &init, 4, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_grind, dim3(chunk / 256), dim3(256), 0, st, gs, (uint32_t)start,
+                       (uint32_t)bits, best.p);
+    KCHECK();
+    uint32_t h = 0;
+    HIP_CHECK(hipMemcpyAsync(&h, best.p, 4, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    if (h != 0xffffffffu) return h;
+  }
+  throw std::runtime_error("grind: no witness");
+}
+
+void gather_words(const std::vector<uint64_t>& addrs, std::vector<uint32_t>& out, hipStream_t st) {
+  out.assign(addrs.size(), 0);
+  if (addrs.empty()) return;
+  DBuf<uint64_t> a(addrs.size());
+  DBuf<uint32_t> o(addrs.size());
+  HIP_CHECK(hipMemcpyAsync(a.p, addrs.data(), addrs.size() * 8, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_gather_words, dim3(ceil_div(addrs.size(), 256)), dim3(256), 0, st,
+                     (const uint64_t*)a.p, addrs.size(), o.p);
+  KCHECK();
+  HIP_CHECK(hipMemcpyAsync(out.data(), o.p, addrs.size() * 4, hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+}
+
+}  // namespace bfz

@@ -1,0 +1,136 @@
+// Device utilities: error checking, a caching device allocator, launch helpers, and the
+// device-side data layout used by the prover.
+//
+// LAYOUT: every evaluation matrix (trace, LDE, permutation trace, quotient chunk) lives in
+// HBM COLUMN-MAJOR with rows in BIT-REVERSED order (position t <-> natural row bitrev(t)).
+// That is the Merkle-leaf order of TwoAdicFriPcs::commit, so leaf hashing, quotient
+// evaluation, FRI reduction and openings all stream columns with unit stride.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "kb.h"
+
+namespace bfz {
+
+struct HipError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+#define HIP_CHECK(expr)                                                                  \
+  do {                                                                                   \
+    hipError_t _e = (expr);                                                              \
+    if (_e != hipSuccess)                                                                \
+      throw ::bfz::HipError(std::string("HIP error ") + hipGetErrorString(_e) + " at " + \
+                            __FILE__ + ":" + std::to_string(__LINE__) + ": " #expr);     \
+  } while (0)
+
+#define KCHECK() HIP_CHECK(hipGetLastError())
+
+inline unsigned ceil_div(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
+inline int log2i(size_t n) {
+  int l = 0;
+  while (((size_t)1 << l) < n) l++;
+  return l;
+}
+inline uint32_t bitrev32(uint32_t x, int bits) {
+  return bits ? (__builtin_bitreverse32(x) >> (32 - bits)) : 0;
+}
+__device__ __forceinline__ uint32_t dbitrev(uint32_t x, int bits) {
+  return bits ? (__brev(x) >> (32 - bits)) : 0;
+}
+
+// Size-bucketed caching allocator: proofs reuse the same buffer shapes, so after the first
+// proof no hipMalloc/hipFree happens inside the timed region.
+class DevicePool {
+ public:
+  void* alloc(size_t bytes) {
+    bytes = (bytes + 255) & ~(size_t)255;
+    if (bytes == 0) bytes = 256;
+    auto it = free_.find(bytes);
+    if (it != free_.end() && !it->second.empty()) {
+      void* p = it->second.back();
+      it->second.pop_back();
+      return p;
+    }
+    void* p = nullptr;
+    HIP_CHECK(hipMalloc(&p, bytes));
+    size_of_[p] = bytes;
+    return p;
+  }
+  void release(void* p) {
+    if (!p) return;
+    auto it = size_of_.find(p);
+    if (it == size_of_.end()) return;
+    free_[it->second].push_back(p);
+  }
+  void trim() {
+    for (auto& kv : free_)
+      for (void* p : kv.second) {
+        (void)hipFree(p);
+        size_of_.erase(p);
+      }
+    free_.clear();
+  }
+  ~DevicePool() {}
+
+ private:
+  std::map<size_t, std::vector<void*>> free_;
+  std::map<void*, size_t> size_of_;
+};
+
+DevicePool& pool();
+
+template <class T>
+struct DBuf {  // RAII device buffer from the pool
+  T* p = nullptr;
+  size_t n = 0;
+  DBuf() = default;
+  explicit DBuf(size_t count) { reset(count); }
+  DBuf(const DBuf&) = delete;
+  DBuf& operator=(const DBuf&) = delete;
+  DBuf(DBuf&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+  DBuf& operator=(DBuf&& o) noexcept {
+    if (this != &o) { free(); p = o.p; n = o.n; o.p = nullptr; o.n = 0; }
+    return *this;
+  }
+  void reset(size_t count) {
+    free();
+    n = count;
+    p = (T*)pool().alloc(count * sizeof(T));
+  }
+  void free() {
+    if (p) pool().release(p);
+    p = nullptr;
+    n = 0;
+  }
+  ~DBuf() { free(); }
+};
+
+// A column-major bit-reversed-row matrix on the device.
+struct DevMatrix {
+  DBuf<uint32_t> buf;
+  size_t height = 0;  // rows (LDE height for committed matrices)
+  int width = 0;
+  uint32_t* col(int c) const { return buf.p + (size_t)c * height; }
+};
+
+// Twiddle tables: T[h + j] = w_{2h}^j for h = 2^k (k < LOGMAX), j < h   (forward)
+//                 and w_{2h}^-j                                          (inverse)
+struct Twiddles {
+  int logmax = 0;
+  DBuf<uint32_t> fwd, inv;
+  std::vector<uint32_t> host_fwd, host_inv;
+  void ensure(int log_n);
+};
+Twiddles& twiddles();
+
+hipStream_t stream();
+
+}  // namespace bfz

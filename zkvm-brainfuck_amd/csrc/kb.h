@@ -1,0 +1,176 @@
+// KoalaBear field (p = 2^31 - 2^24 + 1) and its quartic extension, for host and device.
+//
+// Storage is MONTGOMERY form (x * 2^32 mod p), byte-identical to Plonky3's MontyField31 —
+// the representation the reference keeps `[KoalaBear]` slices in (crates/stark/src/
+// kb31_poseidon2.rs:20 `Val = KoalaBear`).  EF = BinomialExtensionField<KoalaBear, 4>
+// (kb31_poseidon2.rs:21) with x^4 = W = 3.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#define KB_HD __host__ __device__ __forceinline__
+
+namespace kb {
+
+constexpr uint32_t P = 0x7f000001u;
+
+constexpr uint32_t inv_mod_2_32(uint32_t p) {
+  uint32_t x = p;  // p*p = 1 mod 8
+  for (int i = 0; i < 5; i++) x *= 2u - p * x;
+  return x;
+}
+constexpr uint32_t MU = inv_mod_2_32(P);  // p^-1 mod 2^32
+static_assert(uint32_t(P * MU) == 1u, "MU");
+
+// Montgomery reduction of t < 2^64 with hi(t) < 2p: result in [0, p).
+KB_HD uint32_t mreduce(uint64_t t) {
+  uint32_t lo = (uint32_t)t, hi = (uint32_t)(t >> 32);
+  uint32_t m = lo * MU;
+  uint32_t mh = (uint32_t)(((uint64_t)m * P) >> 32);
+  uint32_t r = hi - mh;
+  if (hi < mh) r += P;
+  if (r >= P) r -= P;
+  return r;
+}
+KB_HD uint32_t mmul(uint32_t a, uint32_t b) {
+  uint64_t t = (uint64_t)a * b;
+  uint32_t lo = (uint32_t)t, hi = (uint32_t)(t >> 32);
+  uint32_t m = lo * MU;
+  uint32_t mh = (uint32_t)(((uint64_t)m * P) >> 32);
+  uint32_t r = hi - mh;
+  return hi < mh ? r + P : r;
+}
+KB_HD uint32_t madd(uint32_t a, uint32_t b) {
+  uint32_t s = a + b;
+  return s >= P ? s - P : s;
+}
+KB_HD uint32_t msub(uint32_t a, uint32_t b) {
+  uint32_t d = a - b;
+  return a < b ? d + P : d;
+}
+KB_HD uint32_t mneg(uint32_t a) { return a ? P - a : 0; }
+KB_HD uint32_t mdbl(uint32_t a) { return madd(a, a); }
+
+constexpr uint32_t to_mont_c(uint32_t x) {
+  return (uint32_t)((((uint64_t)(x % P)) << 32) % P);
+}
+constexpr uint32_t from_mont_c(uint32_t x) {
+  // x * 2^-32 mod p
+  uint64_t r = x;
+  for (int i = 0; i < 32; i++) r = (r & 1) ? (r + P) >> 1 : r >> 1;
+  return (uint32_t)r;
+}
+constexpr uint32_t R2 = (uint32_t)((((uint64_t)1 << 32) % P) * (((uint64_t)1 << 32) % P) % P);
+KB_HD uint32_t to_mont(uint32_t x) { return mmul(x % P, R2); }
+KB_HD uint32_t from_mont(uint32_t x) { return mmul(x, 1u); }
+
+constexpr uint32_t ONE = to_mont_c(1);
+constexpr uint32_t TWO = to_mont_c(2);
+
+KB_HD uint32_t mpow(uint32_t a, uint64_t e) {
+  uint32_t r = ONE;
+  while (e) {
+    if (e & 1) r = mmul(r, a);
+    a = mmul(a, a);
+    e >>= 1;
+  }
+  return r;
+}
+KB_HD uint32_t minv(uint32_t a) { return mpow(a, P - 2); }
+
+// two_adic_generator(bits) = (3^127)^(2^(24-bits))  (Montgomery form)
+inline uint32_t two_adic_gen(int bits) {
+  uint32_t g = mpow(to_mont_c(3), 127);
+  for (int i = bits; i < 24; i++) g = mmul(g, g);
+  return g;
+}
+
+// ---------------------------------------------------------------- quartic extension
+struct EF {
+  uint32_t c[4];
+};
+
+KB_HD EF ef_zero() { return EF{{0, 0, 0, 0}}; }
+KB_HD EF ef_one() { return EF{{ONE, 0, 0, 0}}; }
+KB_HD EF ef_base(uint32_t a) { return EF{{a, 0, 0, 0}}; }
+KB_HD EF ef_add(const EF& a, const EF& b) {
+  return EF{{madd(a.c[0], b.c[0]), madd(a.c[1], b.c[1]), madd(a.c[2], b.c[2]), madd(a.c[3], b.c[3])}};
+}
+KB_HD EF ef_sub(const EF& a, const EF& b) {
+  return EF{{msub(a.c[0], b.c[0]), msub(a.c[1], b.c[1]), msub(a.c[2], b.c[2]), msub(a.c[3], b.c[3])}};
+}
+KB_HD EF ef_neg(const EF& a) { return EF{{mneg(a.c[0]), mneg(a.c[1]), mneg(a.c[2]), mneg(a.c[3])}}; }
+KB_HD EF ef_mul_base(const EF& a, uint32_t b) {
+  return EF{{mmul(a.c[0], b), mmul(a.c[1], b), mmul(a.c[2], b), mmul(a.c[3], b)}};
+}
+KB_HD EF ef_add_base(EF a, uint32_t b) {
+  a.c[0] = madd(a.c[0], b);
+  return a;
+}
+KB_HD uint32_t mul3(uint32_t x) { return madd(madd(x, x), x); }
+KB_HD EF ef_mul(const EF& a, const EF& b) {
+  // lazy reduction: sums of <= 3 products of values < p stay below 2^64 with hi < 2p
+  uint64_t w0 = (uint64_t)a.c[1] * b.c[3] + (uint64_t)a.c[2] * b.c[2] + (uint64_t)a.c[3] * b.c[1];
+  uint64_t w1 = (uint64_t)a.c[2] * b.c[3] + (uint64_t)a.c[3] * b.c[2];
+  uint64_t w2 = (uint64_t)a.c[3] * b.c[3];
+  uint64_t d0 = (uint64_t)a.c[0] * b.c[0];
+  uint64_t d1 = (uint64_t)a.c[0] * b.c[1] + (uint64_t)a.c[1] * b.c[0];
+  uint64_t d2 = (uint64_t)a.c[0] * b.c[2] + (uint64_t)a.c[1] * b.c[1] + (uint64_t)a.c[2] * b.c[0];
+  uint64_t d3a = (uint64_t)a.c[0] * b.c[3] + (uint64_t)a.c[1] * b.c[2];
+  uint64_t d3b = (uint64_t)a.c[2] * b.c[1] + (uint64_t)a.c[3] * b.c[0];
+  EF r;
+  r.c[0] = madd(mreduce(d0), mul3(mreduce(w0)));
+  r.c[1] = madd(mreduce(d1), mul3(mreduce(w1)));
+  r.c[2] = madd(mreduce(d2), mul3(mreduce(w2)));
+  r.c[3] = madd(mreduce(d3a), mreduce(d3b));
+  return r;
+}
+KB_HD bool ef_eq(const EF& a, const EF& b) {
+  return a.c[0] == b.c[0] && a.c[1] == b.c[1] && a.c[2] == b.c[2] && a.c[3] == b.c[3];
+}
+KB_HD bool ef_is_zero(const EF& a) { return !(a.c[0] | a.c[1] | a.c[2] | a.c[3]); }
+
+// Frobenius constants: z = W^((p-1)/4); phi^k multiplies coefficient i by z^(i*k).
+// z^1, z^2, z^3 in Montgomery form (computed at compile time).
+constexpr uint32_t cmul(uint32_t a, uint32_t b) { return (uint32_t)((uint64_t)a * b % P); }
+constexpr uint32_t cpow(uint32_t a, uint64_t e) {
+  uint32_t r = 1;
+  while (e) {
+    if (e & 1) r = cmul(r, a);
+    a = cmul(a, a);
+    e >>= 1;
+  }
+  return r;
+}
+constexpr uint32_t FZ1 = cpow(3, (P - 1) / 4);
+constexpr uint32_t FZ2 = cmul(FZ1, FZ1);
+constexpr uint32_t FZ3 = cmul(FZ2, FZ1);
+constexpr uint32_t FZ1M = to_mont_c(FZ1), FZ2M = to_mont_c(FZ2), FZ3M = to_mont_c(FZ3);
+
+KB_HD EF ef_frob1(const EF& a) {  // z^i
+  return EF{{a.c[0], mmul(a.c[1], FZ1M), mmul(a.c[2], FZ2M), mmul(a.c[3], FZ3M)}};
+}
+KB_HD EF ef_frob2(const EF& a) {  // z^(2i): 1, z^2, z^4 = 1, z^6 = z^2
+  return EF{{a.c[0], mmul(a.c[1], FZ2M), a.c[2], mmul(a.c[3], FZ2M)}};
+}
+KB_HD EF ef_frob3(const EF& a) {  // z^(3i): 1, z^3, z^6 = z^2, z^9 = z
+  return EF{{a.c[0], mmul(a.c[1], FZ3M), mmul(a.c[2], FZ2M), mmul(a.c[3], FZ1M)}};
+}
+KB_HD EF ef_inv(const EF& a) {
+  EF t = ef_mul(ef_mul(ef_frob1(a), ef_frob2(a)), ef_frob3(a));
+  // norm = (a * t).c0
+  uint64_t w0 = (uint64_t)a.c[1] * t.c[3] + (uint64_t)a.c[2] * t.c[2] + (uint64_t)a.c[3] * t.c[1];
+  uint32_t n = madd(mreduce((uint64_t)a.c[0] * t.c[0]), mul3(mreduce(w0)));
+  return ef_mul_base(t, minv(n));
+}
+KB_HD EF ef_pow(EF a, uint64_t e) {
+  EF r = ef_one();
+  while (e) {
+    if (e & 1) r = ef_mul(r, a);
+    a = ef_mul(a, a);
+    e >>= 1;
+  }
+  return r;
+}
+
+}  // namespace kb

@@ -1,0 +1,208 @@
+// LogUp permutation trace on the device: generate_permutation_trace
+// (crates/stark/src/permutation.rs:75-148, row fn populate_permutation_row :27-69).
+//
+// Row r, batch b (interactions 2b, 2b+1 of the chain sends++receives):
+//     perm[r][b] = sum_j  (+-m_j) / (alpha + kind_j + sum_k beta^(k+1) v_jk)
+// last column = inclusive prefix sum over rows of sum_b perm[r][b]; cumulative_sum = last.
+// One thread per storage position (bit-reversed row); per row the batch denominators are
+// inverted together (Montgomery trick: one EF inversion per row).  The running sum is a
+// natural-order scan, so row sums are gathered into natural order, scanned, and scattered
+// back into the bit-reversed last column.
+#include "logup.h"
+
+#include <type_traits>
+
+namespace bfz {
+
+using namespace kb;
+
+constexpr int MAIN_W[NUM_CHIPS] = {31, 1, 7, 45, 12, 2, 41, 5};
+constexpr int PREP_W[NUM_CHIPS] = {0, 6, 0, 0, 0, 2, 0, 0};
+
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+// denominator alpha + kind + sum_k beta^(k+1) v_k and signed multiplicity of interaction J
+template <int CHIP, int J, int MW, int PWD>
+__device__ __forceinline__ void interaction(const uint32_t (&pr)[PWD], const uint32_t (&m)[MW],
+                                            const PermChallenges& ch, EF& den, uint32_t& mult) {
+  constexpr Lookup lk = LookupsOf<CHIP>::v.l[J];
+  EF r = ef_add(ch.alpha, ef_base(to_mont_c(lk.kind)));
+#pragma unroll
+  for (int v = 0; v < lk.nvals; v++)
+    r = ef_add(r, ef_mul_base(ch.beta_pows[v + 1], vcol_eval<BaseOps>(lk.vals[v], pr, m)));
+  den = r;
+  const uint32_t mu = vcol_eval<BaseOps>(lk.mult, pr, m);
+  mult = lk.send ? mu : mneg(mu);
+}
+
+// batch b: numerator / denominator of m_0/d_0 + m_1/d_1 (or m_0/d_0 for a trailing single)
+template <int CHIP, int B, int MW, int PWD>
+__device__ __forceinline__ void batch_frac(const uint32_t (&pr)[PWD], const uint32_t (&m)[MW],
+                                           const PermChallenges& ch, EF& num, EF& den) {
+  constexpr int N = LookupsOf<CHIP>::v.n;
+  EF d0;
+  uint32_t m0;
+  interaction<CHIP, 2 * B>(pr, m, ch, d0, m0);
+  if constexpr (2 * B + 1 < N) {
+    EF d1;
+    uint32_t m1;
+    interaction<CHIP, 2 * B + 1>(pr, m, ch, d1, m1);
+    num = ef_add(ef_mul_base(d1, m0), ef_mul_base(d0, m1));
+    den = ef_mul(d0, d1);
+  } else {
+    num = ef_base(m0);
+    den = d0;
+  }
+}
+
+template <int CHIP>
+__global__ __launch_bounds__(256) void k_perm_rows(const uint32_t* __restrict__ mainc,
+                                                   const uint32_t* __restrict__ prepc, size_t n,
+                                                   PermChallenges ch, uint32_t* __restrict__ perm,
+                                                   EF* __restrict__ rowsum) {
+  constexpr int MW = MAIN_W[CHIP];
+  constexpr int PWD = PREP_W[CHIP] > 0 ? PREP_W[CHIP] : 1;
+  constexpr int NB = (LookupsOf<CHIP>::v.n + 1) / 2;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  uint32_t m[MW], pr[PWD];
+#pragma unroll
+  for (int c = 0; c < MW; c++) m[c] = mainc[(size_t)c * n + t];
+#pragma unroll
+  for (int c = 0; c < PWD; c++) pr[c] = PREP_W[CHIP] > 0 ? prepc[(size_t)c * n + t] : 0;
+  EF sum = ef_zero();
+  // batches are inverted two at a time: 1/(d_a d_b) then cross-multiply
+  static_for<0, (NB + 1) / 2>([&](auto P) {
+    constexpr int BA = 2 * decltype(P)::value, BB = BA + 1;
+    EF na, da;
+    batch_frac<CHIP, BA>(pr, m, ch, na, da);
+    EF va, vb;
+    if constexpr (BB < NB) {
+      EF nb, db;
+      batch_frac<CHIP, BB>(pr, m, ch, nb, db);
+      const EF inv = ef_inv(ef_mul(da, db));
+      va = ef_mul(na, ef_mul(inv, db));
+      vb = ef_mul(nb, ef_mul(inv, da));
+#pragma unroll
+      for (int e = 0; e < 4; e++) perm[(size_t)(4 * BB + e) * n + t] = vb.c[e];
+      sum = ef_add(sum, vb);
+    } else {
+      va = ef_mul(na, ef_inv(da));
+    }
+#pragma unroll
+    for (int e = 0; e < 4; e++) perm[(size_t)(4 * BA + e) * n + t] = va.c[e];
+    sum = ef_add(sum, va);
+  });
+  rowsum[t] = sum;
+}
+
+__global__ __launch_bounds__(256) void k_gather_bitrev_ef(const EF* __restrict__ in,
+                                                          EF* __restrict__ out, size_t n,
+                                                          int logn) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = in[dbitrev((uint32_t)i, logn)];
+}
+
+// perm last EF column (4 base columns starting at col0) <- phi_nat[bitrev(t)]
+__global__ __launch_bounds__(256) void k_write_phi(const EF* __restrict__ phi, size_t n, int logn,
+                                                   uint32_t* __restrict__ perm, int col0) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const EF v = phi[dbitrev((uint32_t)t, logn)];
+#pragma unroll
+  for (int e = 0; e < 4; e++) perm[(size_t)(col0 + e) * n + t] = v.c[e];
+}
+
+// --------------------------------------------------------------------- EF prefix scan
+constexpr int SCAN_T = 256, SCAN_PER = 8, SCAN_BLOCK = SCAN_T * SCAN_PER;
+
+__global__ __launch_bounds__(SCAN_T) void k_scan_block(EF* __restrict__ data, size_t n,
+                                                       EF* __restrict__ block_sums) {
+  __shared__ EF sh[SCAN_T];
+  const size_t base = (size_t)blockIdx.x * SCAN_BLOCK + (size_t)threadIdx.x * SCAN_PER;
+  EF v[SCAN_PER];
+  EF run = ef_zero();
+#pragma unroll
+  for (int k = 0; k < SCAN_PER; k++) {
+    v[k] = base + k < n ? data[base + k] : ef_zero();
+    run = ef_add(run, v[k]);
+    v[k] = run;
+  }
+  sh[threadIdx.x] = run;
+  __syncthreads();
+  for (int off = 1; off < SCAN_T; off <<= 1) {
+    EF o = threadIdx.x >= (unsigned)off ? sh[threadIdx.x - off] : ef_zero();
+    __syncthreads();
+    sh[threadIdx.x] = ef_add(sh[threadIdx.x], o);
+    __syncthreads();
+  }
+  const EF prefix = threadIdx.x ? sh[threadIdx.x - 1] : ef_zero();
+#pragma unroll
+  for (int k = 0; k < SCAN_PER; k++)
+    if (base + k < n) data[base + k] = ef_add(v[k], prefix);
+  if (threadIdx.x == SCAN_T - 1) block_sums[blockIdx.x] = sh[SCAN_T - 1];
+}
+
+__global__ __launch_bounds__(SCAN_T) void k_scan_add(EF* __restrict__ data, size_t n,
+                                                     const EF* __restrict__ block_prefix) {
+  if (blockIdx.x == 0) return;
+  const EF p = block_prefix[blockIdx.x - 1];
+  const size_t base = (size_t)blockIdx.x * SCAN_BLOCK;
+  for (int k = threadIdx.x; k < SCAN_BLOCK; k += SCAN_T)
+    if (base + k < n) data[base + k] = ef_add(data[base + k], p);
+}
+
+void ef_inclusive_scan(EF* data, size_t n, hipStream_t st) {
+  const size_t nb = (n + SCAN_BLOCK - 1) / SCAN_BLOCK;
+  DBuf<EF> sums(nb);
+  hipLaunchKernelGGL(k_scan_block, dim3((unsigned)nb), dim3(SCAN_T), 0, st, data, n, sums.p);
+  KCHECK();
+  if (nb > 1) {
+    ef_inclusive_scan(sums.p, nb, st);
+    hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nb), dim3(SCAN_T), 0, st, data, n,
+                       (const EF*)sums.p);
+    KCHECK();
+  }
+}
+
+template <int CHIP>
+static void launch_rows(const uint32_t* mainc, const uint32_t* prepc, size_t n,
+                        const PermChallenges& ch, uint32_t* perm, EF* rowsum, hipStream_t st) {
+  hipLaunchKernelGGL(k_perm_rows<CHIP>, dim3(ceil_div(n, 256)), dim3(256), 0, st, mainc, prepc, n,
+                     ch, perm, rowsum);
+  KCHECK();
+}
+
+void perm_trace(int chip, const uint32_t* mainc, const uint32_t* prepc, size_t n,
+                const PermChallenges& ch, uint32_t* perm, EF* cumsum_dev, hipStream_t st) {
+  const int logn = log2i(n);
+  DBuf<EF> rows(n), nat(n);
+  switch (chip) {
+    case CHIP_CPU: launch_rows<CHIP_CPU>(mainc, prepc, n, ch, perm, rows.p, st); break;
+    case CHIP_PROGRAM: launch_rows<CHIP_PROGRAM>(mainc, prepc, n, ch, perm, rows.p, st); break;
+    case CHIP_ADDSUB: launch_rows<CHIP_ADDSUB>(mainc, prepc, n, ch, perm, rows.p, st); break;
+    case CHIP_JUMP: launch_rows<CHIP_JUMP>(mainc, prepc, n, ch, perm, rows.p, st); break;
+    case CHIP_MEMORY: launch_rows<CHIP_MEMORY>(mainc, prepc, n, ch, perm, rows.p, st); break;
+    case CHIP_BYTE: launch_rows<CHIP_BYTE>(mainc, prepc, n, ch, perm, rows.p, st); break;
+    case CHIP_MEMINSTRS: launch_rows<CHIP_MEMINSTRS>(mainc, prepc, n, ch, perm, rows.p, st); break;
+    case CHIP_IO: launch_rows<CHIP_IO>(mainc, prepc, n, ch, perm, rows.p, st); break;
+    default: throw std::runtime_error("perm_trace: bad chip");
+  }
+  hipLaunchKernelGGL(k_gather_bitrev_ef, dim3(ceil_div(n, 256)), dim3(256), 0, st,
+                     (const EF*)rows.p, nat.p, n, logn);
+  KCHECK();
+  ef_inclusive_scan(nat.p, n, st);
+  const int col0 = 4 * (perm_width(chip) - 1);
+  hipLaunchKernelGGL(k_write_phi, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const EF*)nat.p, n,
+                     logn, perm, col0);
+  KCHECK();
+  HIP_CHECK(hipMemcpyAsync(cumsum_dev, nat.p + (n - 1), sizeof(EF), hipMemcpyDeviceToDevice, st));
+}
+
+}  // namespace bfz

@@ -1,0 +1,171 @@
+// Poseidon2 Merkle tree kernels (see merkle.h).  MerkleTree::new [p3-recalled]:
+//   leaf i  = sponge(row i of every tallest matrix, concatenated in commit order)
+//   node j  = compress(left, right); if matrices of height == this layer exist,
+//             node = compress(node, sponge(row j of those matrices))
+// One thread per row/node; leaf rows are read column by column so every load of a wave is
+// a contiguous 256-byte segment.
+#include <algorithm>
+
+#include "merkle.h"
+#include "poseidon2.h"
+
+namespace bfz {
+
+using namespace kb;
+
+constexpr int MAXCOLS = 160;
+struct ColList {
+  const uint32_t* p[MAXCOLS];
+  int n;
+};
+
+__device__ __forceinline__ void sponge_cols(uint32_t st[16], const ColList& cl, size_t row) {
+  for (int c0 = 0; c0 < cl.n; c0 += 8) {
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      if (c0 + k < cl.n) st[k] = cl.p[c0 + k][row];
+    poseidon2_permute(st);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_hash_leaves(ColList cl, size_t height,
+                                                     uint32_t* __restrict__ out) {
+  const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= height) return;
+  uint32_t st[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) st[i] = 0;
+  sponge_cols(st, cl, r);
+  uint4* o = reinterpret_cast<uint4*>(out + 8 * r);
+  o[0] = make_uint4(st[0], st[1], st[2], st[3]);
+  o[1] = make_uint4(st[4], st[5], st[6], st[7]);
+}
+
+__global__ __launch_bounds__(256) void k_compress(const uint32_t* __restrict__ prev, size_t nlen,
+                                                  uint32_t* __restrict__ out, ColList inj) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nlen) return;
+  uint32_t st[16];
+  const uint4* in = reinterpret_cast<const uint4*>(prev + 16 * j);
+  uint4 a = in[0], b = in[1], c = in[2], d = in[3];
+  st[0] = a.x; st[1] = a.y; st[2] = a.z; st[3] = a.w;
+  st[4] = b.x; st[5] = b.y; st[6] = b.z; st[7] = b.w;
+  st[8] = c.x; st[9] = c.y; st[10] = c.z; st[11] = c.w;
+  st[12] = d.x; st[13] = d.y; st[14] = d.z; st[15] = d.w;
+  poseidon2_permute(st);
+  if (inj.n > 0) {
+    uint32_t h[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) h[i] = 0;
+    sponge_cols(h, inj, j);
+#pragma unroll
+    for (int i = 0; i < 8; i++) st[8 + i] = h[i];
+    poseidon2_permute(st);
+  }
+  uint4* o = reinterpret_cast<uint4*>(out + 8 * j);
+  o[0] = make_uint4(st[0], st[1], st[2], st[3]);
+  o[1] = make_uint4(st[4], st[5], st[6], st[7]);
+}
+
+__global__ __launch_bounds__(256) void k_permute_batch(uint32_t* __restrict__ s, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t st[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) st[k] = s[16 * i + k];
+  poseidon2_permute(st);
+#pragma unroll
+  for (int k = 0; k < 16; k++) s[16 * i + k] = st[k];
+}
+
+__global__ __launch_bounds__(256) void k_hash_rows8(const uint32_t* __restrict__ rows, size_t n,
+                                                    uint32_t* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t st[16];
+  const uint4* in = reinterpret_cast<const uint4*>(rows + 8 * i);
+  uint4 a = in[0], b = in[1];
+  st[0] = a.x; st[1] = a.y; st[2] = a.z; st[3] = a.w;
+  st[4] = b.x; st[5] = b.y; st[6] = b.z; st[7] = b.w;
+#pragma unroll
+  for (int k = 8; k < 16; k++) st[k] = 0;
+  poseidon2_permute(st);
+  uint4* o = reinterpret_cast<uint4*>(out + 8 * i);
+  o[0] = make_uint4(st[0], st[1], st[2], st[3]);
+  o[1] = make_uint4(st[4], st[5], st[6], st[7]);
+}
+
+static ColList make_cols(const std::vector<const MatRef*>& ms) {
+  ColList cl{};
+  cl.n = 0;
+  for (const MatRef* m : ms)
+    for (int c = 0; c < m->width; c++) {
+      if (cl.n >= MAXCOLS) throw std::runtime_error("merkle: too many columns at one height");
+      cl.p[cl.n++] = m->base + (size_t)c * m->height;
+    }
+  return cl;
+}
+
+void merkle_build(const std::vector<MatRef>& mats, MerkleTree& t, hipStream_t st) {
+  if (mats.empty()) throw std::runtime_error("merkle: no matrices");
+  t.mats = mats;
+  std::vector<const MatRef*> sorted;
+  for (const MatRef& m : mats) sorted.push_back(&m);
+  std::stable_sort(sorted.begin(), sorted.end(),
+                   [](const MatRef* a, const MatRef* b) { return a->height > b->height; });
+  const size_t h0 = sorted[0]->height;
+  const int nl = log2i(h0);
+  t.layers.clear();
+  t.layers.resize(nl + 1);
+  size_t next = 0;
+  std::vector<const MatRef*> grp;
+  while (next < sorted.size() && sorted[next]->height == h0) grp.push_back(sorted[next++]);
+  t.layers[0].reset(8 * h0);
+  hipLaunchKernelGGL(k_hash_leaves, dim3(ceil_div(h0, 256)), dim3(256), 0, st, make_cols(grp), h0,
+                     t.layers[0].p);
+  KCHECK();
+  size_t len = h0;
+  for (int L = 1; L <= nl; L++) {
+    const size_t nlen = len / 2;
+    grp.clear();
+    while (next < sorted.size() && sorted[next]->height == nlen) grp.push_back(sorted[next++]);
+    t.layers[L].reset(8 * nlen);
+    hipLaunchKernelGGL(k_compress, dim3(ceil_div(nlen, 256)), dim3(256), 0, st,
+                       (const uint32_t*)t.layers[L - 1].p, nlen, t.layers[L].p, make_cols(grp));
+    KCHECK();
+    len = nlen;
+  }
+  if (next != sorted.size()) throw std::runtime_error("merkle: non power-of-two heights");
+  HIP_CHECK(hipMemcpyAsync(t.root, t.layers[nl].p, 32, hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+}
+
+void merkle_layers_from_leaves(MerkleTree& t, hipStream_t st) {
+  size_t len = t.mats.empty() ? 0 : t.mats[0].height;
+  const int nl = log2i(len);
+  t.layers.resize(nl + 1);
+  ColList none{};
+  none.n = 0;
+  for (int L = 1; L <= nl; L++) {
+    const size_t nlen = len / 2;
+    t.layers[L].reset(8 * nlen);
+    hipLaunchKernelGGL(k_compress, dim3(ceil_div(nlen, 256)), dim3(256), 0, st,
+                       (const uint32_t*)t.layers[L - 1].p, nlen, t.layers[L].p, none);
+    KCHECK();
+    len = nlen;
+  }
+  HIP_CHECK(hipMemcpyAsync(t.root, t.layers[nl].p, 32, hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+}
+
+void poseidon2_batch(uint32_t* states, size_t n, hipStream_t st) {
+  hipLaunchKernelGGL(k_permute_batch, dim3(ceil_div(n, 256)), dim3(256), 0, st, states, n);
+  KCHECK();
+}
+
+void hash_rows8(const uint32_t* rows, size_t n, uint32_t* digests, hipStream_t st) {
+  hipLaunchKernelGGL(k_hash_rows8, dim3(ceil_div(n, 256)), dim3(256), 0, st, rows, n, digests);
+  KCHECK();
+}
+
+}  // namespace bfz

@@ -1,0 +1,228 @@
+// Coset low-degree extension on the device (the p3 `Radix2DitParallel::coset_lde_batch` +
+// `bit_reverse_rows` step of TwoAdicFriPcs::commit, called from crates/stark/src/
+// prover.rs:227,334,411 and machine.rs:196).
+//
+//   evals (bit-reversed rows, n per column)
+//     --iDFT, DIT (bit-reversed in -> natural out)-->  coefficients c_k
+//     --scale-split--> lo_k = c_k s^k / n,  hi_k = c_k (s w_2n)^k / n
+//     --DFT, DIF on each half (natural in -> bit-reversed out)-->  LDE
+// The first DIF stage of a size-2n transform on a zero-padded input is exactly the
+// scale-split (upper half = lower half times w_2n^k), so [DIF_n(lo); DIF_n(hi)] is the
+// bit-reversed LDE on s*H_2n.  Passes are LDS-tiled radix-2^b with coalesced 2^c-element
+// runs; all columns of a matrix go in one launch (grid.y).
+#include "ntt.h"
+
+namespace bfz {
+
+using namespace kb;
+
+constexpr int TILE_LOG = 12;  // 4096 u32 per tile (16 KiB LDS)
+constexpr int CMAX = 5;       // coalesced runs of 32 elements for strided passes
+
+template <bool DIF>
+__global__ __launch_bounds__(256) void k_ntt_pass(const uint32_t* __restrict__ src,
+                                                  uint32_t* __restrict__ dst, size_t src_stride,
+                                                  size_t dst_stride, int s0, int b, int c,
+                                                  const uint32_t* __restrict__ tw) {
+  __shared__ uint32_t tile[1 << TILE_LOG];
+  const uint32_t* s = src + (size_t)blockIdx.y * src_stride;
+  uint32_t* d = dst + (size_t)blockIdx.y * dst_stride;
+  const int nlo_log = s0 - c;
+  const size_t lo_blk = blockIdx.x & ((1u << nlo_log) - 1);
+  const size_t hi = (size_t)blockIdx.x >> nlo_log;
+  const size_t base = (hi << (s0 + b)) + (lo_blk << c);
+  const int nelem = 1 << (b + c);
+  const int cmask = (1 << c) - 1;
+  for (int e = threadIdx.x; e < nelem; e += blockDim.x) {
+    const int lo = e & cmask, m = e >> c;
+    tile[e] = s[base + ((size_t)m << s0) + lo];
+  }
+  __syncthreads();
+  const int nbf = nelem >> 1;
+  for (int tt = 0; tt < b; tt++) {
+    const int t = DIF ? (b - 1 - tt) : tt;
+    const uint32_t* twt = tw + ((size_t)1 << (s0 + t)) + (lo_blk << c);
+    for (int q = threadIdx.x; q < nbf; q += blockDim.x) {
+      const int lo = q & cmask, qq = q >> c;
+      const int mlow = qq & ((1 << t) - 1);
+      const int m1 = ((qq >> t) << (t + 1)) | mlow;
+      const int i1 = (m1 << c) | lo, i2 = i1 + (1 << (t + c));
+      const uint32_t w = twt[((size_t)mlow << s0) + lo];
+      const uint32_t u = tile[i1], v = tile[i2];
+      if (DIF) {
+        tile[i1] = madd(u, v);
+        tile[i2] = mmul(msub(u, v), w);
+      } else {
+        const uint32_t vw = mmul(v, w);
+        tile[i1] = madd(u, vw);
+        tile[i2] = msub(u, vw);
+      }
+    }
+    __syncthreads();
+  }
+  for (int e = threadIdx.x; e < nelem; e += blockDim.x) {
+    const int lo = e & cmask, m = e >> c;
+    d[base + ((size_t)m << s0) + lo] = tile[e];
+  }
+}
+
+// lo_k = c_k * s^k / n ; hi_k = c_k * t^k / n  with s^k = SL[k & m] * SH[k >> B] (1/n in SH)
+__global__ __launch_bounds__(256) void k_scale_split(const uint32_t* __restrict__ coef,
+                                                     uint32_t* __restrict__ lde, size_t n, int B,
+                                                     const uint32_t* __restrict__ pw) {
+  const uint32_t* c = coef + (size_t)blockIdx.y * n;
+  uint32_t* o = lde + (size_t)blockIdx.y * 2 * n;
+  const size_t mask = ((size_t)1 << B) - 1;
+  const size_t nb = mask + 1;
+  const uint32_t* SL = pw;
+  const uint32_t* SH = pw + nb;
+  const uint32_t* TL = pw + 2 * nb;
+  const uint32_t* TH = pw + 3 * nb;
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n;
+       k += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t v = c[k];
+    const size_t kl = k & mask, kh = k >> B;
+    o[k] = mmul(v, mmul(SL[kl], SH[kh]));
+    o[n + k] = mmul(v, mmul(TL[kl], TH[kh]));
+  }
+}
+
+// out[c][t] = in[bitrev(t)][c]: row-major natural -> column-major bit-reversed.
+__global__ __launch_bounds__(256) void k_transpose_bitrev(const uint32_t* __restrict__ in,
+                                                          uint32_t* __restrict__ out, size_t n,
+                                                          int w, int logn) {
+  __shared__ uint32_t tile[64 * 65];
+  const size_t t0 = (size_t)blockIdx.x * 64;
+  const int total = 64 * w;
+  for (int cb = 0; cb < w; cb += 65) {
+    const int cw = min(65, w - cb);
+    for (int e = threadIdx.x; e < 64 * cw; e += blockDim.x) {
+      const int r = e / cw, cc = e % cw;
+      const size_t t = t0 + r;
+      if (t < n) tile[r * 65 + cc] = in[(size_t)dbitrev((uint32_t)t, logn) * w + cb + cc];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 64 * cw; e += blockDim.x) {
+      const int cc = e / 64, r = e % 64;
+      const size_t t = t0 + r;
+      if (t < n) out[(size_t)(cb + cc) * n + t] = tile[r * 65 + cc];
+    }
+    __syncthreads();
+  }
+  (void)total;
+}
+
+// row-major out[r*w + c] = column-major in[c*H + r]
+__global__ __launch_bounds__(256) void k_transpose_rowmajor(const uint32_t* __restrict__ in,
+                                                            uint32_t* __restrict__ out, size_t H,
+                                                            int w) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= H * (size_t)w) return;
+  const size_t r = e / w, c = e % w;
+  out[e] = in[c * H + r];
+}
+
+// -------------------------------------------------------------------------- host side
+std::vector<std::pair<int, int>> ntt_plan(int L) {
+  std::vector<std::pair<int, int>> p;
+  int s0 = 0;
+  while (s0 < L) {
+    const int c = std::min(s0, CMAX);
+    const int b = std::min(L - s0, TILE_LOG - c);
+    p.push_back({s0, b});
+    s0 += b;
+  }
+  return p;
+}
+
+void ntt_passes(const uint32_t* src, uint32_t* dst, size_t src_stride, size_t dst_stride, int ncols,
+                int L, bool dif, hipStream_t st) {
+  Twiddles& T = twiddles();
+  T.ensure(std::max(L, 1));
+  auto plan = ntt_plan(L);
+  if (dif) std::reverse(plan.begin(), plan.end());
+  bool first = true;
+  for (auto [s0, b] : plan) {
+    const int c = std::min(s0, CMAX);
+    dim3 grid(1u << (L - b - c), ncols);
+    const uint32_t* in = first ? src : dst;
+    const size_t is = first ? src_stride : dst_stride;
+    if (dif)
+      hipLaunchKernelGGL(k_ntt_pass<true>, grid, dim3(256), 0, st, in, dst, is, dst_stride, s0, b,
+                         c, T.fwd.p);
+    else
+      hipLaunchKernelGGL(k_ntt_pass<false>, grid, dim3(256), 0, st, in, dst, is, dst_stride, s0, b,
+                         c, T.inv.p);
+    KCHECK();
+    first = false;
+  }
+  if (plan.empty() && src != dst)
+    HIP_CHECK(hipMemcpy2DAsync(dst, dst_stride * 4, src, src_stride * 4, 4, ncols,
+                               hipMemcpyDeviceToDevice, st));
+}
+
+namespace {
+struct PowKey {
+  uint32_t s;
+  int L;
+  bool operator<(const PowKey& o) const { return s != o.s ? s < o.s : L < o.L; }
+};
+std::map<PowKey, DBuf<uint32_t>>& pow_cache() {
+  static auto* m = new std::map<PowKey, DBuf<uint32_t>>();
+  return *m;
+}
+const uint32_t* scale_tables(uint32_t shift, int L, int B) {
+  auto& cache = pow_cache();
+  auto it = cache.find({shift, L});
+  if (it != cache.end()) return it->second.p;
+  const size_t nb = (size_t)1 << B;
+  std::vector<uint32_t> h(4 * nb);
+  const uint32_t ninv = minv(to_mont((uint32_t)(((uint64_t)1 << L) % P)));
+  const uint32_t t = mmul(shift, two_adic_gen(L + 1));
+  for (int which = 0; which < 2; which++) {
+    const uint32_t base = which ? t : shift;
+    uint32_t* lo = &h[2 * which * nb];
+    uint32_t* hi = &h[(2 * which + 1) * nb];
+    uint32_t a = ONE;
+    for (size_t k = 0; k < nb; k++) { lo[k] = a; a = mmul(a, base); }
+    const uint32_t step = a;  // base^(2^B)
+    uint32_t b = ninv;
+    for (size_t k = 0; k < nb; k++) { hi[k] = b; b = mmul(b, step); }
+  }
+  DBuf<uint32_t> d(4 * nb);
+  HIP_CHECK(hipMemcpy(d.p, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+  const uint32_t* p = d.p;
+  cache.emplace(PowKey{shift, L}, std::move(d));
+  return p;
+}
+}  // namespace
+
+void coset_lde(const uint32_t* evals, size_t n, int w, uint32_t shift, uint32_t* lde,
+               hipStream_t st) {
+  const int L = log2i(n);
+  DBuf<uint32_t> coef(n * (size_t)w);
+  ntt_passes(evals, coef.p, n, n, w, L, /*dif=*/false, st);
+  const int B = (L + 1) / 2;
+  const uint32_t* pw = scale_tables(shift, L, B);
+  dim3 grid(std::min<unsigned>(ceil_div(n, 256), 4096), w);
+  hipLaunchKernelGGL(k_scale_split, grid, dim3(256), 0, st, coef.p, lde, n, B, pw);
+  KCHECK();
+  ntt_passes(lde, lde, n, n, 2 * w, L, /*dif=*/true, st);
+  // coef goes back to the pool here; every consumer is ordered on the same stream.
+}
+
+void transpose_to_rowmajor(const uint32_t* colmajor, size_t H, int w, uint32_t* rowmajor,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(k_transpose_rowmajor, dim3(ceil_div(H * (size_t)w, 256)), dim3(256), 0, st,
+                     colmajor, rowmajor, H, w);
+  KCHECK();
+}
+
+void transpose_bitrev(const uint32_t* rowmajor, size_t n, int w, uint32_t* colmajor,
+                      hipStream_t st) {
+  hipLaunchKernelGGL(k_transpose_bitrev, dim3(ceil_div(n, 64)), dim3(256), 0, st, rowmajor,
+                     colmajor, n, w, log2i(n));
+  KCHECK();
+}
+
+}  // namespace bfz

@@ -1,0 +1,96 @@
+// Poseidon2KoalaBear<16> exactly as configured by the reference's my_perm()
+// (crates/stark/src/kb31_poseidon2.rs:35-50 == crates/primitives/src/lib.rs:1101-1117):
+// 8 external rounds (4 initial from RC rows 0..4, 4 terminal from rows 17..21), 13 internal
+// rounds (first element of rows 4..17), S-box x^3.  Algorithm per the published Plonky3
+// Poseidon2 [p3-recalled]: MDS-light (M4 = [[2,3,1,1],[1,2,3,1],[1,1,2,3],[3,1,1,2]] per
+// 4-lane block + lane-wise block sum) before round 1 and after every external round;
+// internal layer s_i <- sum + d_i * s_i, d = [-2,1,2,1/2,3,4,-1/2,-3,-4,1/2^8,1/8,1/2^24,
+// -1/2^8,-1/8,-1/16,-1/2^24].
+//
+// All constants are folded to Montgomery form at compile time; with the rounds fully
+// unrolled they become instruction literals / SGPR operands on gfx950.
+#pragma once
+#include "kb.h"
+
+namespace kb {
+
+struct P2Tables {
+  uint32_t ext_init[4][16];
+  uint32_t ext_term[4][16];
+  uint32_t internal[13];
+  uint32_t diag[16];
+};
+
+constexpr uint32_t RC_RAW[30 * 16] = {
+#include "rc_16_30.inc"
+};
+
+constexpr uint32_t cinv(uint32_t a) { return cpow(a, P - 2); }
+constexpr uint32_t cneg(uint32_t a) { return a ? P - a : 0; }
+
+constexpr P2Tables make_p2_tables() {
+  P2Tables t{};
+  for (int r = 0; r < 4; r++)
+    for (int i = 0; i < 16; i++) {
+      t.ext_init[r][i] = to_mont_c(RC_RAW[r * 16 + i] % P);
+      t.ext_term[r][i] = to_mont_c(RC_RAW[(17 + r) * 16 + i] % P);
+    }
+  for (int r = 0; r < 13; r++) t.internal[r] = to_mont_c(RC_RAW[(4 + r) * 16] % P);
+  uint32_t d[16] = {cneg(2),        1,          2,         cinv(2),          3,
+                    4,              cneg(cinv(2)), cneg(3), cneg(4),          cinv(256),
+                    cinv(8),        cinv(1u << 24), cneg(cinv(256)), cneg(cinv(8)), cneg(cinv(16)),
+                    cneg(cinv(1u << 24))};
+  for (int i = 0; i < 16; i++) t.diag[i] = to_mont_c(d[i]);
+  return t;
+}
+
+constexpr P2Tables P2 = make_p2_tables();
+
+KB_HD uint32_t cube(uint32_t x) { return mmul(mmul(x, x), x); }
+
+KB_HD void mds_light(uint32_t s[16]) {
+#pragma unroll
+  for (int b = 0; b < 16; b += 4) {
+    uint32_t x0 = s[b], x1 = s[b + 1], x2 = s[b + 2], x3 = s[b + 3];
+    uint32_t t01 = madd(x0, x1), t23 = madd(x2, x3), t0123 = madd(t01, t23);
+    uint32_t t01123 = madd(t0123, x1), t01233 = madd(t0123, x3);
+    s[b + 3] = madd(t01233, mdbl(x0));  // 3x0 + x1 + x2 + 2x3
+    s[b + 1] = madd(t01123, mdbl(x2));  // x0 + 2x1 + 3x2 + x3
+    s[b + 0] = madd(t01123, t01);       // 2x0 + 3x1 + x2 + x3
+    s[b + 2] = madd(t01233, t23);       // x0 + x1 + 2x2 + 3x3
+  }
+  uint32_t sums[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) sums[k] = madd(madd(s[k], s[4 + k]), madd(s[8 + k], s[12 + k]));
+#pragma unroll
+  for (int i = 0; i < 16; i++) s[i] = madd(s[i], sums[i & 3]);
+}
+
+KB_HD void poseidon2_permute(uint32_t s[16]) {
+  mds_light(s);
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) s[i] = cube(madd(s[i], P2.ext_init[r][i]));
+    mds_light(s);
+  }
+#pragma unroll
+  for (int r = 0; r < 13; r++) {
+    s[0] = cube(madd(s[0], P2.internal[r]));
+    uint32_t a0 = madd(madd(s[0], s[1]), madd(s[2], s[3]));
+    uint32_t a1 = madd(madd(s[4], s[5]), madd(s[6], s[7]));
+    uint32_t a2 = madd(madd(s[8], s[9]), madd(s[10], s[11]));
+    uint32_t a3 = madd(madd(s[12], s[13]), madd(s[14], s[15]));
+    uint32_t sum = madd(madd(a0, a1), madd(a2, a3));
+#pragma unroll
+    for (int i = 0; i < 16; i++) s[i] = madd(sum, mmul(P2.diag[i], s[i]));
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) s[i] = cube(madd(s[i], P2.ext_term[r][i]));
+    mds_light(s);
+  }
+}
+
+}  // namespace kb

@@ -1,0 +1,93 @@
+// HIP core prover: the MachineProver<KoalaBearPoseidon2, BfAir> drop-in
+// (crates/stark/src/prover.rs:27-150), device-resident from trace upload to proof.
+#pragma once
+#include <array>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "gpu.h"
+#include "machine.h"
+#include "merkle.h"
+
+namespace bfz {
+
+using kb::EF;
+
+// DuplexChallenger<KoalaBear, Perm, 16, 8> (crates/stark/src/kb31_poseidon2.rs:31,126-128)
+// [p3-recalled]: observe -> input buffer (duplex when 8 pending, clears outputs);
+// sample -> duplex if inputs pending or outputs empty, then pop from the END of the outputs.
+struct Challenger {
+  uint32_t st[16] = {0};
+  uint32_t in[8] = {0};
+  int nin = 0;
+  uint32_t out[8] = {0};
+  int nout = 0;
+  void duplex();
+  void observe(uint32_t v);  // Montgomery form
+  void observe_digest(const uint32_t d[8]);
+  void observe_ef(const EF& e);
+  uint32_t sample();
+  EF sample_ef();
+  uint32_t sample_bits(int bits);
+  bool check_witness(int bits, uint32_t w);
+};
+
+struct CMat {               // a committed matrix: LDE on 3*H_2n (bit-reversed, column-major)
+  DevMatrix lde;
+  size_t n = 0;             // trace-domain size
+  int log_n = 0;
+  uint32_t shift = 0;       // trace-domain shift (Montgomery)
+};
+
+struct Round {
+  std::vector<CMat> mats;
+  MerkleTree tree;
+  void commit(hipStream_t st);
+};
+
+struct ProvingKey {
+  Program program;
+  Round prep;                                // Program / Byte, sorted (Reverse(height), name)
+  std::vector<DBuf<uint32_t>> prep_evals;    // trace evaluations (bit-reversed, column-major)
+  std::array<int, 2> chip_of{};
+  std::array<int, NUM_CHIPS> idx_of_chip{};
+};
+
+struct StageTimes {          // milliseconds, measured with HIP events on the prover stream
+  double upload = 0, main_commit = 0, perm = 0, quotient = 0, open = 0, fri = 0, total = 0;
+  double lde_ms = 0;         // sum over coset_lde calls
+  double lde_bytes = 0;      // algorithmic bytes: 12 * n * w per call
+  int lde_calls = 0;
+};
+
+std::unique_ptr<ProvingKey> setup(const std::string& program_src);
+
+// Coset LDE of trace evaluations (bit-reversed, column-major) into a committed matrix.
+void commit_lde(CMat& cm, const uint32_t* evals, size_t n, int w, uint32_t domain_shift,
+                hipStream_t st);
+
+struct ProveOptions {
+  int num_queries = 84;
+  bool timing = false;
+};
+
+// Full core proof of (program, stdin) in the BFZ1 normal form.
+std::vector<uint8_t> prove(const ProvingKey& pk, const uint8_t* stdin_data, size_t nin,
+                           const ProveOptions& opt, StageTimes* times,
+                           std::vector<uint8_t>* output_stream = nullptr,
+                           uint64_t* cycles = nullptr);
+
+// Prove from pre-generated main traces already resident on the device (bench path).
+struct DeviceTraces {
+  std::vector<int> chips;                     // included chips (any order)
+  std::vector<DBuf<uint32_t>> evals;          // column-major bit-reversed evaluations
+  std::vector<size_t> heights;
+};
+void upload_traces(const ExecutionRecord& rec, DeviceTraces& dt, hipStream_t st);
+std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const ProveOptions& opt,
+                                  StageTimes* times);
+
+int num_queries_from_env();
+
+}  // namespace bfz

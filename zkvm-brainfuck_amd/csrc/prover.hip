@@ -1,0 +1,605 @@
+// HIP core prover (host orchestration).  Mirrors, stage for stage:
+//   MachineProver::prove          crates/stark/src/prover.rs:560-582 (observe_into :595-601)
+//   CpuProver::commit             prover.rs:209-236  (sort by (Reverse(height), name))
+//   CpuProver::open               prover.rs:242-553  (LogUp, quotient, PCS open, proof)
+//   StarkMachine::setup           crates/stark/src/machine.rs:154-224
+// and the p3 TwoAdicFriPcs::{commit, open} / fri::prover [p3-recalled].  All bulk data stays
+// in HBM; only digests, challenges, opened values and the query openings cross to the host.
+#include "prover.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+
+#include "fri.h"
+#include "logup.h"
+#include "ntt.h"
+#include "poseidon2.h"
+#include "quotient.h"
+
+namespace bfz {
+
+using namespace kb;
+
+static constexpr int LOG_BLOWUP = 1;
+static constexpr int POW_BITS = 16;
+
+int num_queries_from_env() {
+  const char* s = std::getenv("FRI_QUERIES");  // kb31_poseidon2.rs:59-62
+  return s ? std::atoi(s) : 84;
+}
+
+// ------------------------------------------------------------------------ challenger
+void Challenger::duplex() {
+  for (int i = 0; i < nin; i++) st[i] = in[i];
+  nin = 0;
+  poseidon2_permute(st);
+  for (int i = 0; i < 8; i++) out[i] = st[i];
+  nout = 8;
+}
+void Challenger::observe(uint32_t v) {
+  nout = 0;
+  in[nin++] = v;
+  if (nin == 8) duplex();
+}
+void Challenger::observe_digest(const uint32_t d[8]) {
+  for (int i = 0; i < 8; i++) observe(d[i]);
+}
+void Challenger::observe_ef(const EF& e) {
+  for (int i = 0; i < 4; i++) observe(e.c[i]);
+}
+uint32_t Challenger::sample() {
+  if (nin > 0 || nout == 0) duplex();
+  return out[--nout];
+}
+EF Challenger::sample_ef() {
+  EF r;
+  for (int i = 0; i < 4; i++) r.c[i] = sample();
+  return r;
+}
+uint32_t Challenger::sample_bits(int bits) { return from_mont(sample()) & ((1u << bits) - 1); }
+bool Challenger::check_witness(int bits, uint32_t w) {
+  observe(to_mont(w));
+  return sample_bits(bits) == 0;
+}
+
+// ------------------------------------------------------------------------ timing
+namespace {
+struct EvTimer {
+  bool on = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
+  std::vector<double*> dst;
+  std::vector<double> bytes;
+  hipEvent_t begin(hipStream_t st) {
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreate(&e));
+    HIP_CHECK(hipEventRecord(e, st));
+    return e;
+  }
+  void end(hipEvent_t b, hipStream_t st, double* into) {
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreate(&e));
+    HIP_CHECK(hipEventRecord(e, st));
+    evs.push_back({b, e});
+    dst.push_back(into);
+  }
+  void collect() {
+    for (size_t i = 0; i < evs.size(); i++) {
+      HIP_CHECK(hipEventSynchronize(evs[i].second));
+      float ms = 0;
+      HIP_CHECK(hipEventElapsedTime(&ms, evs[i].first, evs[i].second));
+      *dst[i] += ms;
+      HIP_CHECK(hipEventDestroy(evs[i].first));
+      HIP_CHECK(hipEventDestroy(evs[i].second));
+    }
+    evs.clear();
+    dst.clear();
+  }
+};
+
+void to_canon_digest(const uint32_t* d, uint32_t* o) {
+  for (int i = 0; i < 8; i++) o[i] = from_mont(d[i]);
+}
+
+struct Writer {
+  std::vector<uint8_t> b;
+  void u32(uint32_t v) {
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(&v);
+    b.insert(b.end(), p, p + 4);
+  }
+  void fp(uint32_t mont) { u32(from_mont(mont)); }
+  void ef(const EF& e) {
+    for (int i = 0; i < 4; i++) fp(e.c[i]);
+  }
+  void digest(const uint32_t* d) {
+    for (int i = 0; i < 8; i++) fp(d[i]);
+  }
+  void bytes(const void* p, size_t n) {
+    const uint8_t* q = (const uint8_t*)p;
+    b.insert(b.end(), q, q + n);
+  }
+};
+}  // namespace
+
+void Round::commit(hipStream_t st) {
+  std::vector<MatRef> refs;
+  for (CMat& m : mats) refs.push_back({m.lde.buf.p, m.lde.height, m.lde.width});
+  merkle_build(refs, tree, st);
+}
+
+static void lde_into(CMat& cm, const uint32_t* evals, size_t n, int w, uint32_t domain_shift,
+                     hipStream_t st, EvTimer* tm, StageTimes* times) {
+  cm.n = n;
+  cm.log_n = log2i(n);
+  cm.shift = domain_shift;
+  cm.lde.height = 2 * n;
+  cm.lde.width = w;
+  cm.lde.buf.reset(2 * n * (size_t)w);
+  const uint32_t lde_shift = mmul(to_mont(3), minv(domain_shift));  // GENERATOR / shift
+  hipEvent_t b = nullptr;
+  if (tm && tm->on) b = tm->begin(st);
+  coset_lde(evals, n, w, lde_shift, cm.lde.buf.p, st);
+  if (tm && tm->on) {
+    tm->end(b, st, &times->lde_ms);
+    times->lde_bytes += 12.0 * (double)n * w;
+    times->lde_calls++;
+  }
+}
+
+void commit_lde(CMat& cm, const uint32_t* evals, size_t n, int w, uint32_t domain_shift,
+                hipStream_t st) {
+  lde_into(cm, evals, n, w, domain_shift, st, nullptr, nullptr);
+}
+
+// ------------------------------------------------------------------------ setup
+std::unique_ptr<ProvingKey> setup(const std::string& src) {
+  auto pk = std::make_unique<ProvingKey>();
+  pk->program = Program::parse(src);
+  hipStream_t st = stream();
+  int chips[2] = {CHIP_PROGRAM, CHIP_BYTE};
+  std::vector<uint32_t> t[2];
+  size_t h[2];
+  for (int i = 0; i < 2; i++) h[i] = prep_trace(chips[i], pk->program, t[i]);
+  int ord[2] = {0, 1};
+  if (h[1] > h[0] || (h[1] == h[0] && std::strcmp(CHIP_INFO[chips[1]].name, CHIP_INFO[chips[0]].name) < 0))
+    std::swap(ord[0], ord[1]);
+  pk->idx_of_chip.fill(-1);
+  pk->prep.mats.resize(2);
+  pk->prep_evals.resize(2);
+  for (int k = 0; k < 2; k++) {
+    const int i = ord[k];
+    const int w = CHIP_INFO[chips[i]].prep_w;
+    pk->chip_of[k] = chips[i];
+    pk->idx_of_chip[chips[i]] = k;
+    DBuf<uint32_t> rm(h[i] * w);
+    HIP_CHECK(hipMemcpyAsync(rm.p, t[i].data(), t[i].size() * 4, hipMemcpyHostToDevice, st));
+    pk->prep_evals[k].reset(h[i] * w);
+    transpose_bitrev(rm.p, h[i], w, pk->prep_evals[k].p, st);
+    HIP_CHECK(hipStreamSynchronize(st));
+    lde_into(pk->prep.mats[k], pk->prep_evals[k].p, h[i], w, ONE, st, nullptr, nullptr);
+  }
+  pk->prep.commit(st);
+  return pk;
+}
+
+void upload_traces(const ExecutionRecord& rec, DeviceTraces& dt, hipStream_t st) {
+  dt.chips.clear();
+  dt.evals.clear();
+  dt.heights.clear();
+  for (int c = 0; c < NUM_CHIPS; c++) {
+    if (!chip_included(c, rec)) continue;
+    std::vector<uint32_t> host;
+    const size_t h = main_trace(c, rec, host);
+    const int w = CHIP_INFO[c].main_w;
+    DBuf<uint32_t> rm(h * w);
+    HIP_CHECK(hipMemcpyAsync(rm.p, host.data(), host.size() * 4, hipMemcpyHostToDevice, st));
+    DBuf<uint32_t> ev(h * w);
+    transpose_bitrev(rm.p, h, w, ev.p, st);
+    HIP_CHECK(hipStreamSynchronize(st));
+    dt.chips.push_back(c);
+    dt.evals.push_back(std::move(ev));
+    dt.heights.push_back(h);
+  }
+}
+
+// ------------------------------------------------------------------------ prove
+std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const ProveOptions& opt,
+                                  StageTimes* times) {
+  hipStream_t st = stream();
+  StageTimes local_times;
+  StageTimes* tms = times ? times : &local_times;
+  EvTimer ev;
+  ev.on = opt.timing && times;
+  std::vector<std::vector<EF>> keep;  // host buffers of async uploads live until the end
+  const auto t_start = std::chrono::steady_clock::now();
+  hipEvent_t e_total = ev.on ? ev.begin(st) : nullptr;
+
+  Challenger ch;
+  ch.observe_digest(pk.prep.tree.root);  // observe_into: commit + 7 zeros
+  for (int i = 0; i < 7; i++) ch.observe(0);
+
+  // ---- commit main (prover.rs:209-236)
+  const int nc = (int)dt.chips.size();
+  std::vector<int> order(nc);
+  for (int i = 0; i < nc; i++) order[i] = i;
+  std::sort(order.begin(), order.end(), [&](int a, int b) {
+    if (dt.heights[a] != dt.heights[b]) return dt.heights[a] > dt.heights[b];
+    return std::strcmp(CHIP_INFO[dt.chips[a]].name, CHIP_INFO[dt.chips[b]].name) < 0;
+  });
+  std::vector<int> chip(nc);
+  std::vector<size_t> hn(nc);
+  for (int k = 0; k < nc; k++) {
+    chip[k] = dt.chips[order[k]];
+    hn[k] = dt.heights[order[k]];
+  }
+  hipEvent_t e0 = ev.on ? ev.begin(st) : nullptr;
+  Round mainr;
+  mainr.mats.resize(nc);
+  for (int k = 0; k < nc; k++)
+    lde_into(mainr.mats[k], dt.evals[order[k]].p, hn[k], CHIP_INFO[chip[k]].main_w, ONE, st, &ev,
+             tms);
+  mainr.commit(st);
+  if (ev.on) ev.end(e0, st, &tms->main_commit);
+
+  // ---- open (prover.rs:242-553), on a clone of the challenger (prover.rs:578)
+  ch.observe_digest(mainr.tree.root);
+  const EF perm_alpha = ch.sample_ef();
+  const EF perm_beta = ch.sample_ef();
+  PermChallenges pc;
+  pc.alpha = perm_alpha;
+  pc.beta_pows[0] = ef_one();
+  for (int j = 1; j < 8; j++) pc.beta_pows[j] = ef_mul(pc.beta_pows[j - 1], perm_beta);
+
+  hipEvent_t e1 = ev.on ? ev.begin(st) : nullptr;
+  Round permr;
+  permr.mats.resize(nc);
+  DBuf<EF> cums_d(nc);
+  for (int k = 0; k < nc; k++) {
+    const int c = chip[k];
+    const int pw = perm_width(c);
+    DBuf<uint32_t> pe(4 * (size_t)pw * hn[k]);
+    const int pi = pk.idx_of_chip[c];
+    const uint32_t* prep = pi >= 0 ? pk.prep_evals[pi].p : nullptr;
+    perm_trace(c, dt.evals[order[k]].p, prep, hn[k], pc, pe.p, cums_d.p + k, st);
+    lde_into(permr.mats[k], pe.p, hn[k], 4 * pw, ONE, st, &ev, tms);
+  }
+  permr.commit(st);
+  std::vector<EF> cums(nc);
+  HIP_CHECK(hipMemcpyAsync(cums.data(), cums_d.p, nc * sizeof(EF), hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+  if (ev.on) ev.end(e1, st, &tms->perm);
+  ch.observe_digest(permr.tree.root);
+  for (int k = 0; k < nc; k++) ch.observe_ef(cums[k]);
+  const EF alpha = ch.sample_ef();
+
+  // ---- quotient (prover.rs:344-412)
+  hipEvent_t e2 = ev.on ? ev.begin(st) : nullptr;
+  Round quotr;
+  quotr.mats.resize(2 * nc);
+  std::vector<DBuf<EF>> apows(nc);
+  for (int k = 0; k < nc; k++) {
+    const int c = chip[k];
+    const size_t n = hn[k];
+    const int logn = log2i(n);
+    const int K = num_constraints(c);
+    keep.emplace_back(K);
+    std::vector<EF>& ap = keep.back();
+    EF p = ef_one();
+    for (int j = K - 1; j >= 0; j--) {
+      ap[j] = p;
+      p = ef_mul(p, alpha);
+    }
+    apows[k].reset(K);
+    HIP_CHECK(hipMemcpyAsync(apows[k].p, ap.data(), K * sizeof(EF), hipMemcpyHostToDevice, st));
+    QuotParams qp;
+    qp.perm_alpha = perm_alpha;
+    for (int j = 0; j < 8; j++) qp.beta_pows[j] = pc.beta_pows[j];
+    qp.cumsum = cums[k];
+    qp.alpha_pows = apows[k].p;
+    const uint32_t three = to_mont(3);
+    const uint32_t sn = mpow(three, n);
+    qp.zh_even = msub(sn, ONE);
+    qp.zh_odd = msub(mneg(sn), ONE);
+    qp.zh_even_inv = minv(qp.zh_even);
+    qp.zh_odd_inv = minv(qp.zh_odd);
+    qp.wn_inv = minv(two_adic_gen(logn));
+    qp.shift = three;
+    const int pi = pk.idx_of_chip[c];
+    const uint32_t* prep_lde = pi >= 0 ? pk.prep.mats[pi].lde.buf.p : nullptr;
+    DBuf<uint32_t> q(8 * n);
+    quotient(c, mainr.mats[k].lde.buf.p, prep_lde, permr.mats[k].lde.buf.p, logn + 1, qp, q.p, st);
+    const uint32_t w2n = two_adic_gen(logn + 1);
+    for (int cc = 0; cc < 2; cc++) {
+      const uint32_t dshift = mmul(three, cc ? w2n : ONE);  // split_domains: shift * g^cc
+      lde_into(quotr.mats[2 * k + cc], q.p + (size_t)4 * cc * n, n, 4, dshift, st, &ev, tms);
+    }
+  }
+  quotr.commit(st);
+  if (ev.on) ev.end(e2, st, &tms->quotient);
+  ch.observe_digest(quotr.tree.root);
+  const EF zeta = ch.sample_ef();
+
+  // ---- PCS open: opened values (prover.rs:417-470)
+  hipEvent_t e3 = ev.on ? ev.begin(st) : nullptr;
+  const Round* rounds[4] = {&pk.prep, &mainr, &permr, &quotr};
+  struct MatPts {
+    int npts;
+    EF pts[2];
+    size_t off[2];  // offsets into the opened-values buffer
+  };
+  std::vector<MatPts> mp[4];
+  int Lmax = 0;
+  size_t nvals = 0;
+  for (int r = 0; r < 4; r++) {
+    for (size_t i = 0; i < rounds[r]->mats.size(); i++) {
+      const CMat& m = rounds[r]->mats[i];
+      bool lo;
+      if (r == 0) lo = CHIP_INFO[pk.chip_of[i]].local_only;
+      else if (r == 1) lo = CHIP_INFO[chip[i]].local_only;
+      else lo = (r == 3);
+      MatPts p;
+      p.npts = lo ? 1 : 2;
+      p.pts[0] = zeta;
+      p.pts[1] = ef_mul_base(zeta, two_adic_gen(m.log_n));
+      for (int j = 0; j < p.npts; j++) {
+        p.off[j] = nvals;
+        nvals += m.lde.width;
+      }
+      mp[r].push_back(p);
+      Lmax = std::max(Lmax, m.log_n + LOG_BLOWUP);
+    }
+  }
+  DBuf<EF> invd_zeta((size_t)1 << Lmax);
+  inv_denoms(zeta, Lmax, invd_zeta.p, st);
+  std::map<int, DBuf<EF>> invd_next;  // by LDE log height
+  for (int r = 0; r < 4; r++)
+    for (size_t i = 0; i < rounds[r]->mats.size(); i++) {
+      const CMat& m = rounds[r]->mats[i];
+      const int lh = m.log_n + LOG_BLOWUP;
+      if (mp[r][i].npts == 2 && !invd_next.count(lh)) {
+        DBuf<EF> d((size_t)1 << lh);
+        inv_denoms(mp[r][i].pts[1], lh, d.p, st);
+        invd_next.emplace(lh, std::move(d));
+      }
+    }
+  DBuf<EF> opened_d(nvals);
+  for (int r = 0; r < 4; r++)
+    for (size_t i = 0; i < rounds[r]->mats.size(); i++) {
+      const CMat& m = rounds[r]->mats[i];
+      const int lh = m.log_n + LOG_BLOWUP;
+      const EF three_n = ef_base(mpow(to_mont(3), m.n));
+      const uint32_t n_f = to_mont((uint32_t)(m.n % P));
+      for (int j = 0; j < mp[r][i].npts; j++) {
+        const EF z = mp[r][i].pts[j];
+        const EF zn = ef_pow(z, m.n);
+        const EF scale = ef_mul(ef_sub(zn, three_n), ef_inv(ef_mul_base(three_n, n_f)));
+        const EF* invd = j == 0 ? invd_zeta.p : invd_next.at(lh).p;
+        open_matrix(m.lde.buf.p, m.lde.height, m.lde.width, invd, scale, opened_d.p + mp[r][i].off[j],
+                    st);
+      }
+    }
+  std::vector<EF> opened(nvals);
+  HIP_CHECK(hipMemcpyAsync(opened.data(), opened_d.p, nvals * sizeof(EF), hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+  for (int r = 0; r < 4; r++)
+    for (size_t i = 0; i < rounds[r]->mats.size(); i++)
+      for (int j = 0; j < mp[r][i].npts; j++)
+        for (int c = 0; c < rounds[r]->mats[i].lde.width; c++)
+          ch.observe_ef(opened[mp[r][i].off[j] + c]);
+  const EF fri_alpha = ch.sample_ef();
+
+  // ---- reduced openings per LDE height
+  std::map<int, DBuf<EF>> ro;
+  for (int lh = Lmax; lh >= 1; lh--) {
+    std::vector<RedCol> cols;
+    EF ya = ef_zero(), yb = ef_zero();
+    size_t num_red = 0;
+    bool has_b = false;
+    for (int r = 0; r < 4; r++)
+      for (size_t i = 0; i < rounds[r]->mats.size(); i++) {
+        const CMat& m = rounds[r]->mats[i];
+        if (m.log_n + LOG_BLOWUP != lh) continue;
+        const int w = m.lde.width;
+        const size_t base = cols.size();
+        for (int c = 0; c < w; c++) {
+          RedCol rc{};
+          rc.col = m.lde.buf.p + (size_t)c * m.lde.height;
+          rc.has_b = 0;
+          cols.push_back(rc);
+        }
+        for (int j = 0; j < mp[r][i].npts; j++) {
+          EF a = ef_pow(fri_alpha, num_red);
+          num_red += w;
+          for (int c = 0; c < w; c++) {
+            const EF y = opened[mp[r][i].off[j] + c];
+            if (j == 0) {
+              cols[base + c].ca = a;
+              ya = ef_add(ya, ef_mul(a, y));
+            } else {
+              cols[base + c].cb = a;
+              cols[base + c].has_b = 1;
+              yb = ef_add(yb, ef_mul(a, y));
+              has_b = true;
+            }
+            a = ef_mul(a, fri_alpha);
+          }
+        }
+      }
+    if (cols.empty()) continue;
+    DBuf<EF> r((size_t)1 << lh);
+    HIP_CHECK(hipMemsetAsync(r.p, 0, ((size_t)1 << lh) * sizeof(EF), st));
+    reduce_height(cols, (size_t)1 << lh, invd_zeta.p, has_b ? invd_next.at(lh).p : nullptr, ya, yb,
+                  has_b, r.p, st);
+    ro.emplace(lh, std::move(r));
+  }
+  if (ev.on) ev.end(e3, st, &tms->open);
+
+  // ---- FRI commit phase (fri::prover::commit_phase)
+  hipEvent_t e4 = ev.on ? ev.begin(st) : nullptr;
+  std::vector<DBuf<EF>> layers;
+  std::vector<MerkleTree> trees;
+  layers.push_back(std::move(ro.at(Lmax)));
+  ro.erase(Lmax);
+  size_t len = (size_t)1 << Lmax;
+  while (len > ((size_t)1 << LOG_BLOWUP)) {
+    const size_t h = len / 2;
+    trees.emplace_back();
+    MerkleTree& t = trees.back();
+    t.mats = {MatRef{(const uint32_t*)layers.back().p, h, 8}};
+    t.layers.clear();
+    t.layers.emplace_back(8 * h);
+    hash_rows8((const uint32_t*)layers.back().p, h, t.layers[0].p, st);
+    merkle_layers_from_leaves(t, st);
+    ch.observe_digest(t.root);
+    const EF beta = ch.sample_ef();
+    DBuf<EF> next(h);
+    const int lgh = log2i(h);
+    const EF* add = ro.count(lgh) ? ro.at(lgh).p : nullptr;
+    fri_fold(layers.back().p, next.p, h, beta, add, st);
+    layers.push_back(std::move(next));
+    len = h;
+  }
+  EF fin[2];
+  HIP_CHECK(hipMemcpyAsync(fin, layers.back().p, 2 * sizeof(EF), hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+  if (!ef_eq(fin[0], fin[1]))
+    throw std::runtime_error("FRI: final polynomial is not constant (trace violates the AIR)");
+  ch.observe_ef(fin[0]);
+  GrindState gs;
+  for (int i = 0; i < 16; i++) gs.st[i] = ch.st[i];
+  for (int i = 0; i < 8; i++) gs.in[i] = ch.in[i];
+  gs.nin = ch.nin;
+  const uint32_t witness = grind(gs, POW_BITS, st);
+  if (!ch.check_witness(POW_BITS, witness)) throw std::runtime_error("grind: bad witness");
+  const int nq = opt.num_queries;
+  std::vector<uint32_t> qidx(nq);
+  for (int q = 0; q < nq; q++) qidx[q] = ch.sample_bits(Lmax);
+
+  // ---- query openings: gather every opened word in proof order
+  std::vector<uint64_t> addrs;
+  auto push_digest = [&](const uint32_t* d) {
+    for (int e = 0; e < 8; e++) addrs.push_back((uint64_t)(uintptr_t)(d + e));
+  };
+  const int ncommit = (int)trees.size();
+  for (int q = 0; q < nq; q++) {
+    const size_t index = qidx[q];
+    for (int r = 0; r < 4; r++) {
+      const Round& R = *rounds[r];
+      const int lrm = (int)R.tree.layers.size() - 1;
+      const size_t ri = index >> (Lmax - lrm);
+      for (const CMat& m : R.mats) {
+        const int lh = log2i(m.lde.height);
+        const size_t row = ri >> (lrm - lh);
+        for (int c = 0; c < m.lde.width; c++)
+          addrs.push_back((uint64_t)(uintptr_t)(m.lde.buf.p + (size_t)c * m.lde.height + row));
+      }
+      for (int L = 0; L < lrm; L++) push_digest(R.tree.layers[L].p + 8 * ((ri >> L) ^ 1));
+    }
+    for (int i = 0; i < ncommit; i++) {
+      const size_t ii = index >> i;
+      const uint32_t* sib = (const uint32_t*)(layers[i].p + (ii ^ 1));
+      for (int e = 0; e < 4; e++) addrs.push_back((uint64_t)(uintptr_t)(sib + e));
+      const size_t pair = ii >> 1;
+      const int lm = (int)trees[i].layers.size() - 1;
+      for (int L = 0; L < lm; L++) push_digest(trees[i].layers[L].p + 8 * ((pair >> L) ^ 1));
+    }
+  }
+  std::vector<uint32_t> words;
+  gather_words(addrs, words, st);
+  if (ev.on) ev.end(e4, st, &tms->fri);
+
+  // ---- serialize (BFZ1 normal form)
+  Writer w;
+  w.u32(0x315a4642u);
+  w.u32((uint32_t)nc);
+  for (int k = 0; k < nc; k++) {
+    const char* nm = CHIP_INFO[chip[k]].name;
+    w.u32((uint32_t)chip[k]);
+    w.u32((uint32_t)std::strlen(nm));
+    w.bytes(nm, std::strlen(nm));
+  }
+  w.digest(mainr.tree.root);
+  w.digest(permr.tree.root);
+  w.digest(quotr.tree.root);
+  auto write_vals = [&](size_t off, int n) {
+    w.u32((uint32_t)n);
+    for (int c = 0; c < n; c++) w.ef(opened[off + c]);
+  };
+  for (int k = 0; k < nc; k++) {
+    w.u32((uint32_t)mainr.mats[k].log_n);
+    const int pi = pk.idx_of_chip[chip[k]];
+    if (pi >= 0) {
+      const int pw = pk.prep.mats[pi].lde.width;
+      write_vals(mp[0][pi].off[0], pw);
+      write_vals(mp[0][pi].off[1], pw);
+    } else {
+      w.u32(0);
+      w.u32(0);
+    }
+    const int mw = mainr.mats[k].lde.width;
+    write_vals(mp[1][k].off[0], mw);
+    if (mp[1][k].npts == 2) {
+      write_vals(mp[1][k].off[1], mw);
+    } else {
+      w.u32((uint32_t)mw);
+      for (int c = 0; c < mw; c++) w.ef(ef_zero());
+    }
+    const int pw = permr.mats[k].lde.width;
+    write_vals(mp[2][k].off[0], pw);
+    write_vals(mp[2][k].off[1], pw);
+    w.u32(2);
+    write_vals(mp[3][2 * k].off[0], 4);
+    write_vals(mp[3][2 * k + 1].off[0], 4);
+    w.ef(cums[k]);
+  }
+  w.u32((uint32_t)ncommit);
+  for (int i = 0; i < ncommit; i++) w.digest(trees[i].root);
+  w.u32((uint32_t)nq);
+  size_t pos = 0;
+  auto take = [&]() { return words[pos++]; };
+  for (int q = 0; q < nq; q++) {
+    w.u32(4);
+    for (int r = 0; r < 4; r++) {
+      const Round& R = *rounds[r];
+      const int lrm = (int)R.tree.layers.size() - 1;
+      w.u32((uint32_t)R.mats.size());
+      for (const CMat& m : R.mats) {
+        w.u32((uint32_t)m.lde.width);
+        for (int c = 0; c < m.lde.width; c++) w.fp(take());
+      }
+      w.u32((uint32_t)lrm);
+      for (int L = 0; L < lrm * 8; L++) w.fp(take());
+    }
+    w.u32((uint32_t)ncommit);
+    for (int i = 0; i < ncommit; i++) {
+      for (int e = 0; e < 4; e++) w.fp(take());
+      const int lm = (int)trees[i].layers.size() - 1;
+      w.u32((uint32_t)lm);
+      for (int L = 0; L < lm * 8; L++) w.fp(take());
+    }
+  }
+  w.ef(fin[0]);
+  w.u32(witness);
+  if (ev.on) {
+    ev.end(e_total, st, &tms->total);
+    ev.collect();
+  }
+  (void)t_start;
+  return std::move(w.b);
+}
+
+std::vector<uint8_t> prove(const ProvingKey& pk, const uint8_t* in, size_t nin,
+                           const ProveOptions& opt, StageTimes* times,
+                           std::vector<uint8_t>* output_stream, uint64_t* cycles) {
+  ExecutionRecord rec;
+  execute(pk.program, in, nin, rec);
+  generate_dependencies(rec);
+  DeviceTraces dt;
+  upload_traces(rec, dt, stream());
+  if (output_stream) *output_stream = rec.output;
+  if (cycles) *cycles = rec.global_clk;
+  return prove_device(pk, dt, opt, times);
+}
+
+}  // namespace bfz

@@ -1,0 +1,26 @@
+// Device quotient evaluation (see quotient.hip).
+#pragma once
+#include "gpu.h"
+#include "machine.h"
+
+namespace bfz {
+
+struct QuotParams {
+  kb::EF perm_alpha;
+  kb::EF beta_pows[8];
+  kb::EF cumsum;
+  const kb::EF* alpha_pows;  // device array: alpha^(K-1-k), k = 0..K-1
+  uint32_t zh_even, zh_odd, zh_even_inv, zh_odd_inv;  // Z_H at even / odd natural index
+  uint32_t wn_inv;  // w_n^-1
+  uint32_t shift;   // GENERATOR = 3
+};
+
+// Number of constraints (AIR + LogUp) emitted by a chip's eval.
+int num_constraints(int chip);
+
+// Writes Q at all 2n points into qout: 8 base columns of n rows (chunk k, coefficient e at
+// column 4k+e), rows in bit-reversed order of the chunk domain.
+void quotient(int chip, const uint32_t* mainc, const uint32_t* prepc, const uint32_t* permc,
+              int logN, const QuotParams& qp, uint32_t* qout, hipStream_t st);
+
+}  // namespace bfz

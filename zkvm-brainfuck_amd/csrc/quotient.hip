@@ -1,0 +1,153 @@
+// Quotient evaluation on the device: quotient_values (crates/stark/src/quotient.rs:18-165)
+// with the ProverConstraintFolder fold (folder.rs:68-89) and Chip::eval (chip.rs:222-228).
+//
+// Point i of the quotient domain 3*H_2n (natural index) sits at storage position
+// t = bitrev(i) of every LDE; its "next" row is i+2 (quotient.rs:41-42, next_step = 2).
+// Selectors [p3-recalled selectors_on_coset]: Z_H(x) = x^n - 1 (= 3^n (-1)^i - 1),
+// is_first = Z_H/(x-1), is_last = Z_H/(x - w_n^-1), is_transition = x - w_n^-1.
+// The Horner fold acc = acc*alpha + c_k is computed as sum_k alpha^(K-1-k) c_k (identical
+// value): base-valued AIR constraints cost 4 base multiplies each instead of an EF multiply.
+// Output: Q(x_i) for storage position t lands in quotient chunk (t >> log n) at row
+// (t mod n) -- the bit-reversed evaluation order of chunk i mod 2 on its domain
+// 3 w_2n^k H_n (split_evals / split_domains), ready for the chunk LDE.
+#include "quotient.h"
+
+#include "air.h"
+
+namespace bfz {
+
+using namespace kb;
+
+constexpr int QMAIN_W[NUM_CHIPS] = {31, 1, 7, 45, 12, 2, 41, 5};
+constexpr int QPREP_W[NUM_CHIPS] = {0, 6, 0, 0, 0, 2, 0, 0};
+constexpr int QPERM_W[NUM_CHIPS] = {9, 2, 4, 2, 3, 2, 2, 2};
+
+struct PowAcc {
+  EF acc;
+  const EF* __restrict__ ap;
+  int k;
+  __device__ __forceinline__ void emit(uint32_t c) {
+    acc = ef_add(acc, ef_mul_base(ap[k], c));
+    k++;
+  }
+  __device__ __forceinline__ void emit_ext(const EF& c) {
+    acc = ef_add(acc, ef_mul(ap[k], c));
+    k++;
+  }
+};
+
+template <int CHIP>
+__global__ __launch_bounds__(256) void k_quotient(const uint32_t* __restrict__ mainc,
+                                                  const uint32_t* __restrict__ prepc,
+                                                  const uint32_t* __restrict__ permc, int logN,
+                                                  QuotParams qp, const uint32_t* __restrict__ twf,
+                                                  uint32_t* __restrict__ qout) {
+  constexpr int MW = QMAIN_W[CHIP];
+  constexpr int PWD = QPREP_W[CHIP] > 0 ? QPREP_W[CHIP] : 1;
+  constexpr int PMW = QPERM_W[CHIP];
+  const size_t N = (size_t)1 << logN, n = N >> 1;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N) return;
+  const uint32_t i = dbitrev((uint32_t)t, logN);
+  const uint32_t inext = (i + 2) & (uint32_t)(N - 1);
+  const size_t tn = dbitrev(inext, logN);
+
+  uint32_t L[MW], Nx[MW], PL[PWD], PN[PWD];
+#pragma unroll
+  for (int c = 0; c < MW; c++) {
+    L[c] = mainc[(size_t)c * N + t];
+    Nx[c] = mainc[(size_t)c * N + tn];
+  }
+#pragma unroll
+  for (int c = 0; c < PWD; c++) {
+    PL[c] = QPREP_W[CHIP] > 0 ? prepc[(size_t)c * N + t] : 0;
+    PN[c] = QPREP_W[CHIP] > 0 ? prepc[(size_t)c * N + tn] : 0;
+  }
+  EF pl[PMW], pn[PMW];
+#pragma unroll
+  for (int e = 0; e < PMW; e++)
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      pl[e].c[k] = permc[(size_t)(4 * e + k) * N + t];
+      pn[e].c[k] = permc[(size_t)(4 * e + k) * N + tn];
+    }
+
+  // x = 3 * w_N^i
+  const uint32_t half = (uint32_t)n;
+  const uint32_t w = i < half ? twf[half + i] : mneg(twf[i]);  // twf[half + (i - half)]
+  const uint32_t x = mmul(qp.shift, w);
+  const uint32_t zh = (i & 1) ? qp.zh_odd : qp.zh_even;
+  const uint32_t zh_inv = (i & 1) ? qp.zh_odd_inv : qp.zh_even_inv;
+  const uint32_t a = msub(x, ONE), b = msub(x, qp.wn_inv);
+  const uint32_t inv_ab = minv(mmul(a, b));
+  const uint32_t zi = mmul(zh, inv_ab);
+  const uint32_t is_first = mmul(zi, b), is_last = mmul(zi, a), is_trans = b;
+
+  PowAcc acc{ef_zero(), qp.alpha_pows, 0};
+  Air<BaseOps, PowAcc> air{L, Nx, PL, PN, is_first, is_last, is_trans, acc};
+  air.template eval_air<CHIP>();
+  air.template eval_perm<CHIP>(pl, pn, qp.perm_alpha, qp.beta_pows, qp.cumsum, ef_base(is_first),
+                               ef_base(is_last), ef_base(is_trans));
+  const EF q = ef_mul_base(acc.acc, zh_inv);
+  const size_t chunk = t >> (logN - 1), pos = t & (n - 1);
+#pragma unroll
+  for (int e = 0; e < 4; e++) qout[(chunk * 4 + e) * n + pos] = q.c[e];
+}
+
+template <int CHIP>
+static void launch_q(const uint32_t* mainc, const uint32_t* prepc, const uint32_t* permc, int logN,
+                     const QuotParams& qp, uint32_t* qout, hipStream_t st) {
+  const size_t N = (size_t)1 << logN;
+  hipLaunchKernelGGL(k_quotient<CHIP>, dim3(ceil_div(N, 256)), dim3(256), 0, st, mainc, prepc,
+                     permc, logN, qp, (const uint32_t*)twiddles().fwd.p, qout);
+  KCHECK();
+}
+
+void quotient(int chip, const uint32_t* mainc, const uint32_t* prepc, const uint32_t* permc,
+              int logN, const QuotParams& qp, uint32_t* qout, hipStream_t st) {
+  twiddles().ensure(logN);
+  switch (chip) {
+    case CHIP_CPU: launch_q<CHIP_CPU>(mainc, prepc, permc, logN, qp, qout, st); break;
+    case CHIP_PROGRAM: launch_q<CHIP_PROGRAM>(mainc, prepc, permc, logN, qp, qout, st); break;
+    case CHIP_ADDSUB: launch_q<CHIP_ADDSUB>(mainc, prepc, permc, logN, qp, qout, st); break;
+    case CHIP_JUMP: launch_q<CHIP_JUMP>(mainc, prepc, permc, logN, qp, qout, st); break;
+    case CHIP_MEMORY: launch_q<CHIP_MEMORY>(mainc, prepc, permc, logN, qp, qout, st); break;
+    case CHIP_BYTE: launch_q<CHIP_BYTE>(mainc, prepc, permc, logN, qp, qout, st); break;
+    case CHIP_MEMINSTRS: launch_q<CHIP_MEMINSTRS>(mainc, prepc, permc, logN, qp, qout, st); break;
+    case CHIP_IO: launch_q<CHIP_IO>(mainc, prepc, permc, logN, qp, qout, st); break;
+    default: throw std::runtime_error("quotient: bad chip");
+  }
+}
+
+}  // namespace bfz
+
+namespace bfz {
+
+template <int CHIP>
+static int count_chip() {
+  EF z[64];
+  for (auto& e : z) e = kb::ef_zero();
+  CountAcc acc;
+  Air<ExtOps, CountAcc> air{z, z, z, z, z[0], z[0], z[0], acc};
+  air.template eval_air<CHIP>();
+  EF bp[8];
+  for (auto& e : bp) e = kb::ef_zero();
+  air.template eval_perm<CHIP>(z, z, z[0], bp, z[0], z[0], z[0], z[0]);
+  return acc.n;
+}
+
+int num_constraints(int chip) {
+  switch (chip) {
+    case CHIP_CPU: return count_chip<CHIP_CPU>();
+    case CHIP_PROGRAM: return count_chip<CHIP_PROGRAM>();
+    case CHIP_ADDSUB: return count_chip<CHIP_ADDSUB>();
+    case CHIP_JUMP: return count_chip<CHIP_JUMP>();
+    case CHIP_MEMORY: return count_chip<CHIP_MEMORY>();
+    case CHIP_BYTE: return count_chip<CHIP_BYTE>();
+    case CHIP_MEMINSTRS: return count_chip<CHIP_MEMINSTRS>();
+    case CHIP_IO: return count_chip<CHIP_IO>();
+  }
+  return 0;
+}
+
+}  // namespace bfz

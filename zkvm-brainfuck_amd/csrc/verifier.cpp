@@ -1,0 +1,461 @@
+// Host verifier (see verifier.h).  Checks, in the reference's order:
+//   BfProver::verify           (crates/prover/src/verify.rs:10-36): Cpu present, log deg <= 22
+//   Verifier::verify_shard     (crates/stark/src/verifier.rs:27-216): byte-multiplicity bound,
+//                              transcript replay, PCS/FRI verification, per-chip OOD check
+//                              folded(zeta) * 1/Z_H(zeta) == recomputed quotient(zeta),
+//                              sum of cumulative sums == 0.
+#include "verifier.h"
+
+#include <algorithm>
+#include <array>
+#include <cstring>
+#include <map>
+#include <stdexcept>
+#include <vector>
+
+#include "air.h"
+#include "machine.h"
+#include "poseidon2.h"
+#include "prover.h"
+
+namespace bfz {
+
+using namespace kb;
+
+namespace {
+
+constexpr int LOG_BLOWUP = 1, POW_BITS = 16, MAX_CPU_LOG_DEGREE = 22;
+
+struct Reader {
+  const uint8_t* p;
+  size_t n, off = 0;
+  uint32_t u32() {
+    if (off + 4 > n) throw std::runtime_error("truncated proof");
+    uint32_t v;
+    std::memcpy(&v, p + off, 4);
+    off += 4;
+    return v;
+  }
+  uint32_t fp() {
+    const uint32_t v = u32();
+    if (v >= P) throw std::runtime_error("non-canonical field element");
+    return to_mont(v);
+  }
+  EF ef() {
+    EF e;
+    for (int i = 0; i < 4; i++) e.c[i] = fp();
+    return e;
+  }
+  void digest(uint32_t* d) {
+    for (int i = 0; i < 8; i++) d[i] = fp();
+  }
+  std::vector<EF> efs(size_t maxn = 4096) {
+    const uint32_t k = u32();
+    if (k > maxn) throw std::runtime_error("bad vector length");
+    std::vector<EF> v(k);
+    for (auto& e : v) e = ef();
+    return v;
+  }
+};
+
+struct HornerAcc {
+  EF acc = ef_zero();
+  EF alpha;
+  void emit(const EF& c) { acc = ef_add(ef_mul(acc, alpha), c); }
+  void emit_ext(const EF& c) { emit(c); }
+};
+
+template <int CHIP>
+EF fold_chip(const std::vector<EF>& pl, const std::vector<EF>& pn, const std::vector<EF>& ml,
+             const std::vector<EF>& mn, const std::vector<EF>& perml, const std::vector<EF>& permn,
+             const EF& pa, const EF* pb_pows, const EF& cumsum, const EF& first, const EF& last,
+             const EF& trans, const EF& alpha) {
+  HornerAcc acc;
+  acc.alpha = alpha;
+  static const EF zero1[1] = {ef_zero()};
+  const EF* PL = pl.empty() ? zero1 : pl.data();
+  const EF* PN = pn.empty() ? zero1 : pn.data();
+  Air<ExtOps, HornerAcc> air{ml.data(), mn.data(), PL, PN, first, last, trans, acc};
+  air.template eval_air<CHIP>();
+  air.template eval_perm<CHIP>(perml.data(), permn.data(), pa, pb_pows, cumsum, first, last, trans);
+  return acc.acc;
+}
+
+EF fold_any(int chip, const std::vector<EF>& pl, const std::vector<EF>& pn, const std::vector<EF>& ml,
+            const std::vector<EF>& mn, const std::vector<EF>& perml, const std::vector<EF>& permn,
+            const EF& pa, const EF* pb, const EF& cs, const EF& f, const EF& l, const EF& t,
+            const EF& al) {
+  switch (chip) {
+    case CHIP_CPU: return fold_chip<CHIP_CPU>(pl, pn, ml, mn, perml, permn, pa, pb, cs, f, l, t, al);
+    case CHIP_PROGRAM: return fold_chip<CHIP_PROGRAM>(pl, pn, ml, mn, perml, permn, pa, pb, cs, f, l, t, al);
+    case CHIP_ADDSUB: return fold_chip<CHIP_ADDSUB>(pl, pn, ml, mn, perml, permn, pa, pb, cs, f, l, t, al);
+    case CHIP_JUMP: return fold_chip<CHIP_JUMP>(pl, pn, ml, mn, perml, permn, pa, pb, cs, f, l, t, al);
+    case CHIP_MEMORY: return fold_chip<CHIP_MEMORY>(pl, pn, ml, mn, perml, permn, pa, pb, cs, f, l, t, al);
+    case CHIP_BYTE: return fold_chip<CHIP_BYTE>(pl, pn, ml, mn, perml, permn, pa, pb, cs, f, l, t, al);
+    case CHIP_MEMINSTRS: return fold_chip<CHIP_MEMINSTRS>(pl, pn, ml, mn, perml, permn, pa, pb, cs, f, l, t, al);
+    case CHIP_IO: return fold_chip<CHIP_IO>(pl, pn, ml, mn, perml, permn, pa, pb, cs, f, l, t, al);
+  }
+  throw std::runtime_error("bad chip");
+}
+
+void sponge(uint32_t st[16], const std::vector<const uint32_t*>& rows, const std::vector<int>& ws) {
+  int pos = 0;
+  for (size_t m = 0; m < rows.size(); m++)
+    for (int c = 0; c < ws[m]; c++) {
+      st[pos++] = rows[m][c];
+      if (pos == 8) {
+        poseidon2_permute(st);
+        pos = 0;
+      }
+    }
+  if (pos) poseidon2_permute(st);
+}
+
+void compress(const uint32_t* l, const uint32_t* r, uint32_t* out) {
+  uint32_t s[16];
+  std::memcpy(s, l, 32);
+  std::memcpy(s + 8, r, 32);
+  poseidon2_permute(s);
+  std::memcpy(out, s, 32);
+}
+
+// MerkleTreeMmcs::verify_batch [p3-recalled]; heights are powers of two.
+bool verify_batch(const uint32_t root[8], const std::vector<size_t>& heights,
+                  const std::vector<int>& widths, size_t index,
+                  const std::vector<std::vector<uint32_t>>& rows,
+                  const std::vector<uint32_t>& path) {
+  std::vector<int> ord(heights.size());
+  for (size_t i = 0; i < ord.size(); i++) ord[i] = (int)i;
+  std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return heights[a] > heights[b]; });
+  size_t cur = heights[ord[0]];
+  size_t k = 0;
+  auto take = [&](std::vector<const uint32_t*>& rp, std::vector<int>& wp) {
+    while (k < ord.size() && heights[ord[k]] == cur) {
+      rp.push_back(rows[ord[k]].data());
+      wp.push_back(widths[ord[k]]);
+      k++;
+    }
+  };
+  std::vector<const uint32_t*> rp;
+  std::vector<int> wp;
+  take(rp, wp);
+  uint32_t h[16] = {0};
+  sponge(h, rp, wp);
+  uint32_t node[8];
+  std::memcpy(node, h, 32);
+  for (size_t L = 0; L < path.size() / 8; L++) {
+    const uint32_t* sib = &path[8 * L];
+    if (index & 1) compress(sib, node, node);
+    else compress(node, sib, node);
+    index >>= 1;
+    cur >>= 1;
+    if (k < ord.size() && heights[ord[k]] == cur) {
+      rp.clear();
+      wp.clear();
+      take(rp, wp);
+      uint32_t hh[16] = {0};
+      sponge(hh, rp, wp);
+      compress(node, hh, node);
+    }
+  }
+  return k == ord.size() && std::memcmp(node, root, 32) == 0;
+}
+
+EF monomial(int e) {
+  EF m = ef_zero();
+  m.c[e] = ONE;
+  return m;
+}
+
+EF zp_at(int log_n, uint32_t shift, const EF& x) {  // (x / s)^(2^log_n) - 1
+  EF u = ef_mul_base(x, minv(shift));
+  for (int i = 0; i < log_n; i++) u = ef_mul(u, u);
+  return ef_sub(u, ef_one());
+}
+
+// number of byte lookups each chip SENDS (Chip::num_sent_byte_lookups)
+int sent_byte_lookups(int chip) { return chip == CHIP_CPU ? 7 : chip == CHIP_ADDSUB ? 3 : 0; }
+
+}  // namespace
+
+bool verify_proof(const std::string& src, const uint32_t vk_commit[8], const uint8_t* proof,
+                  size_t len, int num_queries, std::string* why) {
+  try {
+    Program prog = Program::parse(src);
+    // vk.chip_information: prep matrices sorted by (Reverse(height), name)
+    size_t prog_h = std::max<size_t>(16, [&] {
+      size_t p = 1;
+      while (p < prog.instructions.size()) p <<= 1;
+      return p;
+    }());
+    struct PrepInfo { int chip; int log_n; int w; };
+    std::vector<PrepInfo> prep = {{CHIP_PROGRAM, log2i(prog_h), 6}, {CHIP_BYTE, 16, 2}};
+    if (prep[1].log_n > prep[0].log_n ||
+        (prep[1].log_n == prep[0].log_n && std::strcmp("Byte", "Program") < 0))
+      std::swap(prep[0], prep[1]);
+
+    Reader r{proof, len};
+    if (r.u32() != 0x315a4642u) throw std::runtime_error("bad magic");
+    const uint32_t nc = r.u32();
+    if (nc == 0 || nc > NUM_CHIPS) throw std::runtime_error("bad chip count");
+    std::vector<int> chip(nc);
+    std::vector<bool> seen(NUM_CHIPS, false);
+    for (uint32_t i = 0; i < nc; i++) {
+      chip[i] = (int)r.u32();
+      if (chip[i] < 0 || chip[i] >= NUM_CHIPS || seen[chip[i]]) throw std::runtime_error("bad chip id");
+      seen[chip[i]] = true;
+      const uint32_t l = r.u32();
+      if (l != std::strlen(CHIP_INFO[chip[i]].name) || r.off + l > len ||
+          std::memcmp(proof + r.off, CHIP_INFO[chip[i]].name, l) != 0)
+        throw std::runtime_error("chip name mismatch");
+      r.off += l;
+    }
+    uint32_t main_root[8], perm_root[8], quot_root[8];
+    r.digest(main_root);
+    r.digest(perm_root);
+    r.digest(quot_root);
+    struct ChipOpen {
+      int log_n;
+      std::vector<EF> pl, pn, ml, mn, perml, permn, q[2];
+      EF cumsum;
+    };
+    std::vector<ChipOpen> co(nc);
+    for (uint32_t i = 0; i < nc; i++) {
+      ChipOpen& c = co[i];
+      c.log_n = (int)r.u32();
+      if (c.log_n > 23) throw std::runtime_error("log degree too large");
+      c.pl = r.efs();
+      c.pn = r.efs();
+      c.ml = r.efs();
+      c.mn = r.efs();
+      c.perml = r.efs();
+      c.permn = r.efs();
+      if (r.u32() != 2) throw std::runtime_error("bad quotient chunk count");
+      c.q[0] = r.efs();
+      c.q[1] = r.efs();
+      c.cumsum = r.ef();
+      const int ch = chip[i];
+      const size_t pw = CHIP_INFO[ch].prep_w;
+      if (c.ml.size() != (size_t)CHIP_INFO[ch].main_w || c.mn.size() != c.ml.size() ||
+          c.perml.size() != 4 * (size_t)perm_width(ch) || c.permn.size() != c.perml.size() ||
+          c.pl.size() != pw || c.pn.size() != pw || c.q[0].size() != 4 || c.q[1].size() != 4)
+        throw std::runtime_error("opened-value shape mismatch");
+    }
+    // BfProver::verify: Cpu chip present, log degree bound
+    int cpu_i = -1;
+    for (uint32_t i = 0; i < nc; i++) if (chip[i] == CHIP_CPU) cpu_i = (int)i;
+    if (cpu_i < 0) throw std::runtime_error("missing Cpu chip");
+    if (co[cpu_i].log_n > MAX_CPU_LOG_DEGREE) throw std::runtime_error("Cpu log degree too large");
+    // byte multiplicities must not overflow (verifier.rs:47-62)
+    {
+      unsigned __int128 tot = 0;
+      for (uint32_t i = 0; i < nc; i++) tot += (unsigned __int128)sent_byte_lookups(chip[i]) << co[i].log_n;
+      if (tot > P) throw std::runtime_error("byte multiplicities overflow");
+    }
+    // ---- transcript (verifier.rs:76-101)
+    Challenger ch;
+    ch.observe_digest(vk_commit);
+    for (int i = 0; i < 7; i++) ch.observe(0);
+    ch.observe_digest(main_root);
+    const EF pa = ch.sample_ef(), pb = ch.sample_ef();
+    ch.observe_digest(perm_root);
+    for (uint32_t i = 0; i < nc; i++) {
+      ch.observe_ef(co[i].cumsum);
+      // chips with no interactions must have a zero sum (all chips here have interactions)
+    }
+    const EF alpha = ch.sample_ef();
+    ch.observe_digest(quot_root);
+    const EF zeta = ch.sample_ef();
+
+    // ---- rounds for PCS verify
+    struct VMat { int log_n; uint32_t shift; int w; int np; EF pt[2]; const std::vector<EF>* v[2]; };
+    std::vector<VMat> rounds[4];
+    for (const PrepInfo& pi : prep) {
+      int idx = -1;
+      for (uint32_t j = 0; j < nc; j++) if (chip[j] == pi.chip) idx = (int)j;
+      if (idx < 0) throw std::runtime_error("preprocessed chip missing from proof");
+      VMat m{pi.log_n, ONE, pi.w, CHIP_INFO[pi.chip].local_only ? 1 : 2, {zeta, ef_mul_base(zeta, two_adic_gen(pi.log_n))},
+             {&co[idx].pl, &co[idx].pn}};
+      rounds[0].push_back(m);
+    }
+    for (uint32_t i = 0; i < nc; i++) {
+      const ChipOpen& c = co[i];
+      const EF znext = ef_mul_base(zeta, two_adic_gen(c.log_n));
+      rounds[1].push_back(VMat{c.log_n, ONE, (int)c.ml.size(), CHIP_INFO[chip[i]].local_only ? 1 : 2,
+                               {zeta, znext}, {&c.ml, &c.mn}});
+      rounds[2].push_back(VMat{c.log_n, ONE, (int)c.perml.size(), 2, {zeta, znext}, {&c.perml, &c.permn}});
+      const uint32_t w2n = two_adic_gen(c.log_n + 1);
+      for (int k = 0; k < 2; k++)
+        rounds[3].push_back(VMat{c.log_n, mmul(to_mont(3), k ? w2n : ONE), 4, 1, {zeta, zeta},
+                                 {&c.q[k], &c.q[k]}});
+    }
+    for (int rr = 0; rr < 4; rr++)
+      for (const VMat& m : rounds[rr])
+        for (int p = 0; p < m.np; p++)
+          for (int c = 0; c < m.w; c++) ch.observe_ef((*m.v[p])[c]);
+    const EF fri_alpha = ch.sample_ef();
+    const uint32_t ncommit = r.u32();
+    if (ncommit > 30) throw std::runtime_error("too many FRI rounds");
+    std::vector<std::array<uint32_t, 8>> croots(ncommit);
+    std::vector<EF> betas(ncommit);
+    for (uint32_t i = 0; i < ncommit; i++) {
+      r.digest(croots[i].data());
+      ch.observe_digest(croots[i].data());
+      betas[i] = ch.sample_ef();
+    }
+    const uint32_t nq = r.u32();
+    if ((int)nq != num_queries) throw std::runtime_error("wrong number of queries");
+    const size_t qstart = r.off;
+    // skip to final poly / witness
+    for (uint32_t q = 0; q < nq; q++) {
+      const uint32_t nr = r.u32();
+      for (uint32_t x = 0; x < nr; x++) {
+        const uint32_t nm = r.u32();
+        for (uint32_t i = 0; i < nm; i++) r.off += 4 * (size_t)r.u32();
+        r.off += 32 * (size_t)r.u32();
+      }
+      const uint32_t ns = r.u32();
+      for (uint32_t s = 0; s < ns; s++) {
+        r.off += 16;
+        r.off += 32 * (size_t)r.u32();
+      }
+      if (r.off > len) throw std::runtime_error("truncated proof");
+    }
+    const EF final_poly = r.ef();
+    const uint32_t witness = r.u32();
+    if (r.off != len) throw std::runtime_error("trailing bytes");
+    ch.observe_ef(final_poly);
+    if (witness >= P || !ch.check_witness(POW_BITS, witness)) throw std::runtime_error("bad PoW witness");
+    const int log_max = (int)ncommit + LOG_BLOWUP;
+    r.off = qstart;
+    const uint32_t* roots[4] = {vk_commit, main_root, perm_root, quot_root};
+    const uint32_t half = to_mont_c((P + 1) / 2);
+    (void)half;
+    for (uint32_t q = 0; q < nq; q++) {
+      const size_t index = ch.sample_bits(log_max);
+      if (r.u32() != 4) throw std::runtime_error("bad round count");
+      std::map<int, std::pair<EF, EF>> ro;  // log height -> (alpha_pow, ro)
+      for (int rr = 0; rr < 4; rr++) {
+        const uint32_t nm = r.u32();
+        if (nm != rounds[rr].size()) throw std::runtime_error("bad matrix count");
+        std::vector<std::vector<uint32_t>> rows(nm);
+        std::vector<size_t> heights(nm);
+        std::vector<int> widths(nm);
+        int lbmax = 0;
+        for (uint32_t i = 0; i < nm; i++) {
+          const uint32_t w = r.u32();
+          if ((int)w != rounds[rr][i].w) throw std::runtime_error("bad row width");
+          rows[i].resize(w);
+          for (uint32_t c = 0; c < w; c++) rows[i][c] = r.fp();
+          heights[i] = (size_t)1 << (rounds[rr][i].log_n + LOG_BLOWUP);
+          widths[i] = (int)w;
+          lbmax = std::max(lbmax, rounds[rr][i].log_n + LOG_BLOWUP);
+        }
+        const uint32_t pl = r.u32();
+        if ((int)pl != lbmax) throw std::runtime_error("bad path length");
+        std::vector<uint32_t> path(8 * pl);
+        for (auto& x : path) x = r.fp();
+        const size_t ridx = index >> (log_max - lbmax);
+        if (!verify_batch(roots[rr], heights, widths, ridx, rows, path))
+          throw std::runtime_error("input Merkle opening rejected");
+        for (uint32_t i = 0; i < nm; i++) {
+          const VMat& m = rounds[rr][i];
+          const int lh = m.log_n + LOG_BLOWUP;
+          const uint32_t rev = bitrev32((uint32_t)(index >> (log_max - lh)), lh);
+          const uint32_t x = mmul(to_mont(3), mpow(two_adic_gen(lh), rev));
+          auto it = ro.find(lh);
+          if (it == ro.end()) it = ro.emplace(lh, std::make_pair(ef_one(), ef_zero())).first;
+          for (int p = 0; p < m.np; p++) {
+            const EF inv = ef_inv(ef_sub(ef_base(x), m.pt[p]));
+            for (int c = 0; c < m.w; c++) {
+              const EF quo = ef_mul(ef_sub(ef_base(rows[i][c]), (*m.v[p])[c]), inv);
+              it->second.second = ef_add(it->second.second, ef_mul(it->second.first, quo));
+              it->second.first = ef_mul(it->second.first, fri_alpha);
+            }
+          }
+        }
+      }
+      // verify_query
+      if (r.u32() != ncommit) throw std::runtime_error("bad step count");
+      EF folded = ef_zero();
+      size_t idx = index;
+      for (uint32_t s = 0; s < ncommit; s++) {
+        const int lfh = log_max - 1 - (int)s;
+        auto it = ro.find(lfh + 1);
+        if (it != ro.end()) {
+          folded = ef_add(folded, it->second.second);
+          ro.erase(it);
+        }
+        const EF sib = r.ef();
+        const uint32_t pl = r.u32();
+        if ((int)pl != lfh) throw std::runtime_error("bad FRI path length");
+        std::vector<uint32_t> path(8 * pl);
+        for (auto& x : path) x = r.fp();
+        EF ev[2];
+        ev[idx & 1] = folded;
+        ev[(idx & 1) ^ 1] = sib;
+        std::vector<std::vector<uint32_t>> row(1, std::vector<uint32_t>(8));
+        std::memcpy(row[0].data(), ev[0].c, 16);
+        std::memcpy(row[0].data() + 4, ev[1].c, 16);
+        if (!verify_batch(croots[s].data(), {(size_t)1 << lfh}, {8}, idx >> 1, row, path))
+          throw std::runtime_error("FRI commit-phase opening rejected");
+        idx >>= 1;
+        const uint32_t x0 = mpow(two_adic_gen(lfh + 1), bitrev32((uint32_t)idx, lfh));
+        const uint32_t x1 = mneg(x0);
+        const EF t = ef_mul(ef_sub(betas[s], ef_base(x0)), ef_sub(ev[1], ev[0]));
+        folded = ef_add(ev[0], ef_mul_base(t, minv(msub(x1, x0))));
+      }
+      if (!ro.empty()) throw std::runtime_error("unconsumed reduced openings");
+      if (!ef_eq(folded, final_poly)) throw std::runtime_error("FRI final value mismatch");
+    }
+
+    // ---- OOD constraint checks (verifier.rs:194-213)
+    EF total = ef_zero();
+    for (uint32_t i = 0; i < nc; i++) {
+      const ChipOpen& c = co[i];
+      const int n_log = c.log_n;
+      const uint32_t w2n = two_adic_gen(n_log + 1);
+      const uint32_t sh[2] = {to_mont(3), mmul(to_mont(3), w2n)};
+      EF zps[2];
+      for (int a = 0; a < 2; a++) {
+        const int o = 1 - a;
+        zps[a] = ef_mul(zp_at(n_log, sh[o], zeta), ef_inv(zp_at(n_log, sh[o], ef_base(sh[a]))));
+      }
+      EF quot = ef_zero();
+      for (int a = 0; a < 2; a++)
+        for (int e = 0; e < 4; e++) quot = ef_add(quot, ef_mul(ef_mul(zps[a], monomial(e)), c.q[a][e]));
+      const uint32_t gn_inv = minv(two_adic_gen(n_log));
+      EF zh = zeta;
+      for (int k = 0; k < n_log; k++) zh = ef_mul(zh, zh);
+      zh = ef_sub(zh, ef_one());
+      const EF first = ef_mul(zh, ef_inv(ef_sub(zeta, ef_one())));
+      const EF last = ef_mul(zh, ef_inv(ef_sub(zeta, ef_base(gn_inv))));
+      const EF trans = ef_sub(zeta, ef_base(gn_inv));
+      const int pw = perm_width(chip[i]);
+      std::vector<EF> perml(pw), permn(pw);
+      for (int e = 0; e < pw; e++) {
+        perml[e] = ef_zero();
+        permn[e] = ef_zero();
+        for (int k = 0; k < 4; k++) {
+          perml[e] = ef_add(perml[e], ef_mul(monomial(k), c.perml[4 * e + k]));
+          permn[e] = ef_add(permn[e], ef_mul(monomial(k), c.permn[4 * e + k]));
+        }
+      }
+      EF pb_pows[8];
+      pb_pows[0] = ef_one();
+      for (int j = 1; j < 8; j++) pb_pows[j] = ef_mul(pb_pows[j - 1], pb);
+      const EF folded = fold_any(chip[i], c.pl, c.pn, c.ml, c.mn, perml, permn, pa, pb_pows, c.cumsum,
+                                 first, last, trans, alpha);
+      if (!ef_eq(ef_mul(folded, ef_inv(zh)), quot))
+        throw std::runtime_error(std::string("OOD evaluation mismatch on chip ") + CHIP_INFO[chip[i]].name);
+      total = ef_add(total, c.cumsum);
+    }
+    if (!ef_is_zero(total)) throw std::runtime_error("cumulative sums do not sum to zero");
+    return true;
+  } catch (const std::exception& e) {
+    if (why) *why = e.what();
+    return false;
+  }
+}
+
+}  // namespace bfz
