@@ -55,6 +55,14 @@ void bfz_free(void* p);
 int bfz_execute(const char* elf, const uint8_t* stdin_data, size_t nin, uint8_t* out,
                 size_t out_cap, size_t* out_len, uint64_t* cycles);
 
+/* MachineProver::generate_traces (crates/stark/src/prover.rs:58-81) after
+ * generate_dependencies (machine.rs:228-248): row-major Montgomery trace of one chip
+ * (chip index in BfAir::chips() order, brainfuck/mod.rs:53-81; prep != 0 selects the
+ * preprocessed trace).  *out is malloc'd (bfz_free).  Returns 1 if the chip is not
+ * included in the record. */
+int bfz_trace(const char* elf, const uint8_t* stdin_data, size_t nin, int chip, int prep,
+              uint32_t** out, size_t* height, size_t* width);
+
 int bfz_setup(const char* elf, bfz_pk** pk, uint32_t vk_commit[8]);
 void bfz_pk_free(bfz_pk* pk);
 

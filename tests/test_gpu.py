@@ -123,9 +123,15 @@ def test_fibo_x4_2pow22_properties(client):
         client.verify(sdk.BfProofWithPublicValues(proof=bytes(bad), stdin=b"\xff"), vk)
 
 
-def test_invalid_trace_is_refused(client):
-    """An execution that violates the AIR cannot be proven (reference panics in FRI's final
-    polynomial check).  A memory pointer that wraps below zero breaks the word range check."""
-    pk, vk = client.setup("<+")
-    with pytest.raises(_lib.BfzError):
-        client.prove(pk, []).run()
+def test_invalid_trace_rejected_by_verifiers(client):
+    """An execution that violates the AIR (a memory pointer wrapping below zero breaks the
+    KoalaBear word range check of MemoryInstrs) still yields a proof -- the quotient chunks
+    are low-degree by construction, as in the reference -- but both verifiers reject it at
+    the out-of-domain check (verifier.rs:194-208).  GPU and oracle agree bit for bit."""
+    prog = "<+"
+    pk, vk = client.setup(prog)
+    pf = client.prove(pk, []).run()
+    assert pf.proof == O.prove(prog, [])
+    with pytest.raises(_lib.BfzError, match="OOD evaluation mismatch"):
+        client.verify(pf, vk)
+    assert not O.verify(prog, pf.proof)

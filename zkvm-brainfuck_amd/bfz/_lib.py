@@ -38,6 +38,8 @@ SIGNATURES = [
     ("bfz_free", None, [c_void_p]),
     ("bfz_execute", c_int, [c_char_p, POINTER(c_uint8), c_size_t, POINTER(c_uint8), c_size_t,
                             POINTER(c_size_t), POINTER(c_uint64)]),
+    ("bfz_trace", c_int, [c_char_p, POINTER(c_uint8), c_size_t, c_int, c_int,
+                          POINTER(POINTER(c_uint32)), POINTER(c_size_t), POINTER(c_size_t)]),
     ("bfz_setup", c_int, [c_char_p, POINTER(c_void_p), POINTER(c_uint32)]),
     ("bfz_pk_free", None, [c_void_p]),
     ("bfz_prove", c_int, [c_void_p, POINTER(c_uint8), c_size_t, POINTER(POINTER(c_uint8)),

@@ -92,6 +92,34 @@ int bfz_execute(const char* elf, const uint8_t* in, size_t nin, uint8_t* out, si
   });
 }
 
+int bfz_trace(const char* elf, const uint8_t* in, size_t nin, int chip, int prep, uint32_t** out,
+              size_t* height, size_t* width) {
+  return guarded([&] {
+    if (chip < 0 || chip >= bfz::NUM_CHIPS) throw std::runtime_error("bad chip index");
+    bfz::Program p = bfz::Program::parse(elf);
+    std::vector<uint32_t> t;
+    size_t h = 0;
+    if (prep) {
+      h = bfz::prep_trace(chip, p, t);
+      if (!h) return 1;
+      *width = bfz::CHIP_INFO[chip].prep_w;
+    } else {
+      bfz::ExecutionRecord rec;
+      bfz::execute(p, in, nin, rec);
+      bfz::generate_dependencies(rec);
+      if (!bfz::chip_included(chip, rec)) return 1;
+      h = bfz::main_trace(chip, rec, t);
+      *width = bfz::CHIP_INFO[chip].main_w;
+    }
+    uint32_t* o = (uint32_t*)std::malloc(t.size() * 4 + 4);
+    if (!o) throw std::runtime_error("out of host memory");
+    std::memcpy(o, t.data(), t.size() * 4);
+    *out = o;
+    *height = h;
+    return 0;
+  });
+}
+
 int bfz_setup(const char* elf, bfz_pk** pk, uint32_t vk_commit[8]) {
   return guarded([&] {
     auto k = std::make_unique<bfz_pk>();

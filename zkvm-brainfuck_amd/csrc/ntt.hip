@@ -190,7 +190,9 @@ const uint32_t* scale_tables(uint32_t shift, int L, int B) {
     for (size_t k = 0; k < nb; k++) { hi[k] = b; b = mmul(b, step); }
   }
   DBuf<uint32_t> d(4 * nb);
-  HIP_CHECK(hipMemcpy(d.p, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+  // stream-ordered: a pooled buffer may still be read by kernels queued on stream()
+  HIP_CHECK(hipMemcpyAsync(d.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, stream()));
+  HIP_CHECK(hipStreamSynchronize(stream()));
   const uint32_t* p = d.p;
   cache.emplace(PowKey{shift, L}, std::move(d));
   return p;

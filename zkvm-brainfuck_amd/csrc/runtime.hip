@@ -38,10 +38,12 @@ void Twiddles::ensure(int log_n) {
       b = kb::mmul(b, wi);
     }
   }
+  // stream-ordered: pooled buffers may still be read by kernels queued on stream()
   fwd.reset(N);
   inv.reset(N);
-  HIP_CHECK(hipMemcpy(fwd.p, host_fwd.data(), N * 4, hipMemcpyHostToDevice));
-  HIP_CHECK(hipMemcpy(inv.p, host_inv.data(), N * 4, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpyAsync(fwd.p, host_fwd.data(), N * 4, hipMemcpyHostToDevice, stream()));
+  HIP_CHECK(hipMemcpyAsync(inv.p, host_inv.data(), N * 4, hipMemcpyHostToDevice, stream()));
+  HIP_CHECK(hipStreamSynchronize(stream()));
   logmax = log_n;
 }
 
