@@ -237,7 +237,9 @@ void fri_fold(const EF* in, EF* out, size_t h, const EF& beta, const EF* add, hi
 
 uint32_t grind(const GrindState& gs, int bits, hipStream_t st) {
   DBuf<uint32_t> best(1);
-  const uint32_t chunk = 1u << 22;
+  // 2^(bits+2) candidates per launch: a witness exists in the first chunk with probability
+  // 1 - e^-4, and chunks are scanned in order so the first hit is the smallest witness.
+  const uint32_t chunk = 1u << std::min(22, std::max(16, bits + 2));
   for (uint64_t start = 0; start < P; start += chunk) {
     const uint32_t init = 0xffffffffu;
     HIP_CHECK(hipMemcpyAsync(best.p, &init, 4, hipMemcpyHostToDevice, st));

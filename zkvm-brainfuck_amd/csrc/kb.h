@@ -22,31 +22,47 @@ constexpr uint32_t inv_mod_2_32(uint32_t p) {
 constexpr uint32_t MU = inv_mod_2_32(P);  // p^-1 mod 2^32
 static_assert(uint32_t(P * MU) == 1u, "MU");
 
+// p = 1 + 127*2^24, so p^-1 = 1 - 127*2^24 = 1 + 2^24 - 2^31 (mod 2^32): the Montgomery
+// factor m = lo * p^-1 is two shifts and two adds instead of a 32-bit multiply.
+static_assert(MU == (uint32_t)(1u + (1u << 24) - (1u << 31)), "MU shape");
+KB_HD uint32_t mont_m(uint32_t lo) { return lo + (lo << 24) - (lo << 31); }
+KB_HD uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+
 // Montgomery reduction of t < 2^64 with hi(t) < 2p: result in [0, p).
 KB_HD uint32_t mreduce(uint64_t t) {
   uint32_t lo = (uint32_t)t, hi = (uint32_t)(t >> 32);
-  uint32_t m = lo * MU;
+  uint32_t m = mont_m(lo);
   uint32_t mh = (uint32_t)(((uint64_t)m * P) >> 32);
   uint32_t r = hi - mh;
   if (hi < mh) r += P;
   if (r >= P) r -= P;
   return r;
 }
+// a, b < p: t < p^2 so hi < p/2 and r = hi - mh lies in (-p, p/2); min() folds the sign fix.
 KB_HD uint32_t mmul(uint32_t a, uint32_t b) {
   uint64_t t = (uint64_t)a * b;
   uint32_t lo = (uint32_t)t, hi = (uint32_t)(t >> 32);
-  uint32_t m = lo * MU;
+  uint32_t m = mont_m(lo);
   uint32_t mh = (uint32_t)(((uint64_t)m * P) >> 32);
   uint32_t r = hi - mh;
-  return hi < mh ? r + P : r;
+  return umin(r, r + P);
 }
 KB_HD uint32_t madd(uint32_t a, uint32_t b) {
-  uint32_t s = a + b;
-  return s >= P ? s - P : s;
+  uint32_t s = a + b;  // < 2p < 2^32
+  return umin(s, s - P);
 }
 KB_HD uint32_t msub(uint32_t a, uint32_t b) {
   uint32_t d = a - b;
-  return a < b ? d + P : d;
+  return umin(d, d + P);
+}
+// x * 2^-k (k <= 24) of a value (or its Montgomery form) in [0, p): with m = -x mod 2^k,
+// (x + m p) / 2^k = (x + m) / 2^k + m * 127 * 2^(24-k), both terms exact.
+template <int K>
+KB_HD uint32_t mdiv2k(uint32_t x) {
+  static_assert(K >= 1 && K <= 24, "K");
+  const uint32_t m = (0u - x) & ((1u << K) - 1);
+  const uint32_t y = ((x + m) >> K) + (m << (31 - K)) - (m << (24 - K));
+  return umin(y, y - P);
 }
 KB_HD uint32_t mneg(uint32_t a) { return a ? P - a : 0; }
 KB_HD uint32_t mdbl(uint32_t a) { return madd(a, a); }

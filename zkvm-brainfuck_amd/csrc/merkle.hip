@@ -41,30 +41,99 @@ __global__ __launch_bounds__(256) void k_hash_leaves(ColList cl, size_t height,
   o[1] = make_uint4(st[4], st[5], st[6], st[7]);
 }
 
+// Merkle node j from its two children already in st[0..16]:
+//   compress(children), then with injected columns [c0, c1): compress(node, sponge(row j)).
+// The steps share ONE permutation call site, so the kernel holds a single inlined copy of
+// the (~37 KB) permutation instead of three.
+__device__ __forceinline__ void merkle_node(uint32_t st[16], const ColList& cl, int c0, int c1,
+                                            size_t j) {
+  const int nchunks = (c1 - c0 + 7) >> 3;
+  const int nsteps = nchunks ? nchunks + 2 : 1;
+  uint32_t d[8];
+  for (int step = 0; step < nsteps; step++) {
+    if (step == 1) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) d[i] = st[i];
+#pragma unroll
+      for (int i = 0; i < 16; i++) st[i] = 0;
+    }
+    if (step >= 1 && step <= nchunks) {
+      const int cb = c0 + 8 * (step - 1);
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        if (cb + k < c1) st[k] = cl.p[cb + k][j];
+    }
+    if (nchunks && step == nchunks + 1) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        st[8 + i] = st[i];
+        st[i] = d[i];
+      }
+    }
+    poseidon2_permute(st);
+  }
+}
+
+__device__ __forceinline__ void load16(uint32_t st[16], const uint32_t* p) {
+  const uint4* in = reinterpret_cast<const uint4*>(p);
+  const uint4 a = in[0], b = in[1], c = in[2], d = in[3];
+  st[0] = a.x; st[1] = a.y; st[2] = a.z; st[3] = a.w;
+  st[4] = b.x; st[5] = b.y; st[6] = b.z; st[7] = b.w;
+  st[8] = c.x; st[9] = c.y; st[10] = c.z; st[11] = c.w;
+  st[12] = d.x; st[13] = d.y; st[14] = d.z; st[15] = d.w;
+}
+
+__device__ __forceinline__ void store8(uint32_t* p, const uint32_t st[16]) {
+  uint4* o = reinterpret_cast<uint4*>(p);
+  o[0] = make_uint4(st[0], st[1], st[2], st[3]);
+  o[1] = make_uint4(st[4], st[5], st[6], st[7]);
+}
+
 __global__ __launch_bounds__(256) void k_compress(const uint32_t* __restrict__ prev, size_t nlen,
                                                   uint32_t* __restrict__ out, ColList inj) {
   const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= nlen) return;
   uint32_t st[16];
-  const uint4* in = reinterpret_cast<const uint4*>(prev + 16 * j);
-  uint4 a = in[0], b = in[1], c = in[2], d = in[3];
-  st[0] = a.x; st[1] = a.y; st[2] = a.z; st[3] = a.w;
-  st[4] = b.x; st[5] = b.y; st[6] = b.z; st[7] = b.w;
-  st[8] = c.x; st[9] = c.y; st[10] = c.z; st[11] = c.w;
-  st[12] = d.x; st[13] = d.y; st[14] = d.z; st[15] = d.w;
-  poseidon2_permute(st);
-  if (inj.n > 0) {
-    uint32_t h[16];
-#pragma unroll
-    for (int i = 0; i < 16; i++) h[i] = 0;
-    sponge_cols(h, inj, j);
-#pragma unroll
-    for (int i = 0; i < 8; i++) st[8 + i] = h[i];
-    poseidon2_permute(st);
+  load16(st, prev + 16 * j);
+  merkle_node(st, inj, 0, inj.n, j);
+  store8(out + 8 * j, st);
+}
+
+// All layers of <= TOP_NODES nodes in one workgroup: layer l reads the previous layer from
+// LDS (the first from HBM), writes its digests to HBM (query paths need every layer) and to
+// LDS for the next.  Removes one launch + one permutation latency tail per small layer.
+constexpr int TOP_NODES = 512;
+constexpr int MAXTOP = 24;
+struct TopLayers {
+  uint32_t* out[MAXTOP];
+  int c0[MAXTOP], c1[MAXTOP];
+  int n;
+};
+
+__global__ __launch_bounds__(TOP_NODES) void k_compress_top(const uint32_t* __restrict__ prev,
+                                                            size_t nlen, ColList inj,
+                                                            TopLayers tl) {
+  __shared__ uint4 buf[2][TOP_NODES * 2];
+  for (int l = 0; l < tl.n; l++, nlen >>= 1) {
+    for (size_t j = threadIdx.x; j < nlen; j += blockDim.x) {
+      uint32_t st[16];
+      if (l == 0) {
+        load16(st, prev + 16 * j);
+      } else {
+        const uint4* s4 = buf[(l - 1) & 1] + 4 * j;
+        const uint4 a = s4[0], b = s4[1], c = s4[2], d = s4[3];
+        st[0] = a.x; st[1] = a.y; st[2] = a.z; st[3] = a.w;
+        st[4] = b.x; st[5] = b.y; st[6] = b.z; st[7] = b.w;
+        st[8] = c.x; st[9] = c.y; st[10] = c.z; st[11] = c.w;
+        st[12] = d.x; st[13] = d.y; st[14] = d.z; st[15] = d.w;
+      }
+      merkle_node(st, inj, tl.c0[l], tl.c1[l], j);
+      store8(tl.out[l] + 8 * j, st);
+      buf[l & 1][2 * j] = make_uint4(st[0], st[1], st[2], st[3]);
+      buf[l & 1][2 * j + 1] = make_uint4(st[4], st[5], st[6], st[7]);
+    }
+    __syncthreads();
   }
-  uint4* o = reinterpret_cast<uint4*>(out + 8 * j);
-  o[0] = make_uint4(st[0], st[1], st[2], st[3]);
-  o[1] = make_uint4(st[4], st[5], st[6], st[7]);
 }
 
 __global__ __launch_bounds__(256) void k_permute_batch(uint32_t* __restrict__ s, size_t n) {
@@ -106,6 +175,47 @@ static ColList make_cols(const std::vector<const MatRef*>& ms) {
   return cl;
 }
 
+// Layers 1..nl above layers[0]; sorted[next..] are the matrices still to inject (heights
+// descending).  Big layers get one launch each; the rest go to k_compress_top in one launch.
+static void build_layers(MerkleTree& t, size_t len, const std::vector<const MatRef*>& sorted,
+                         size_t next, hipStream_t st) {
+  const int nl = log2i(len);
+  int L = 1;
+  for (; L <= nl && (len >> 1) > (size_t)TOP_NODES; L++) {
+    const size_t nlen = len >> 1;
+    std::vector<const MatRef*> grp;
+    while (next < sorted.size() && sorted[next]->height == nlen) grp.push_back(sorted[next++]);
+    t.layers[L].reset(8 * nlen);
+    hipLaunchKernelGGL(k_compress, dim3(ceil_div(nlen, 256)), dim3(256), 0, st,
+                       (const uint32_t*)t.layers[L - 1].p, nlen, t.layers[L].p, make_cols(grp));
+    KCHECK();
+    len = nlen;
+  }
+  if (L <= nl) {
+    TopLayers tl{};
+    tl.n = nl - L + 1;
+    if (tl.n > MAXTOP) throw std::runtime_error("merkle: too many top layers");
+    std::vector<const MatRef*> all;
+    size_t nlen = len >> 1;
+    for (int l = 0; l < tl.n; l++, nlen >>= 1) {
+      tl.c0[l] = 0;
+      for (const MatRef* m : all) tl.c0[l] += m->width;
+      while (next < sorted.size() && sorted[next]->height == nlen) all.push_back(sorted[next++]);
+      tl.c1[l] = 0;
+      for (const MatRef* m : all) tl.c1[l] += m->width;
+      t.layers[L + l].reset(8 * nlen);
+      tl.out[l] = t.layers[L + l].p;
+    }
+    const int threads = (int)std::max<size_t>(64, len >> 1);
+    hipLaunchKernelGGL(k_compress_top, dim3(1), dim3(threads), 0, st,
+                       (const uint32_t*)t.layers[L - 1].p, len >> 1, make_cols(all), tl);
+    KCHECK();
+  }
+  if (next != sorted.size()) throw std::runtime_error("merkle: non power-of-two heights");
+  HIP_CHECK(hipMemcpyAsync(t.root, t.layers[nl].p, 32, hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+}
+
 void merkle_build(const std::vector<MatRef>& mats, MerkleTree& t, hipStream_t st) {
   if (mats.empty()) throw std::runtime_error("merkle: no matrices");
   t.mats = mats;
@@ -114,9 +224,8 @@ void merkle_build(const std::vector<MatRef>& mats, MerkleTree& t, hipStream_t st
   std::stable_sort(sorted.begin(), sorted.end(),
                    [](const MatRef* a, const MatRef* b) { return a->height > b->height; });
   const size_t h0 = sorted[0]->height;
-  const int nl = log2i(h0);
   t.layers.clear();
-  t.layers.resize(nl + 1);
+  t.layers.resize(log2i(h0) + 1);
   size_t next = 0;
   std::vector<const MatRef*> grp;
   while (next < sorted.size() && sorted[next]->height == h0) grp.push_back(sorted[next++]);
@@ -124,38 +233,13 @@ void merkle_build(const std::vector<MatRef>& mats, MerkleTree& t, hipStream_t st
   hipLaunchKernelGGL(k_hash_leaves, dim3(ceil_div(h0, 256)), dim3(256), 0, st, make_cols(grp), h0,
                      t.layers[0].p);
   KCHECK();
-  size_t len = h0;
-  for (int L = 1; L <= nl; L++) {
-    const size_t nlen = len / 2;
-    grp.clear();
-    while (next < sorted.size() && sorted[next]->height == nlen) grp.push_back(sorted[next++]);
-    t.layers[L].reset(8 * nlen);
-    hipLaunchKernelGGL(k_compress, dim3(ceil_div(nlen, 256)), dim3(256), 0, st,
-                       (const uint32_t*)t.layers[L - 1].p, nlen, t.layers[L].p, make_cols(grp));
-    KCHECK();
-    len = nlen;
-  }
-  if (next != sorted.size()) throw std::runtime_error("merkle: non power-of-two heights");
-  HIP_CHECK(hipMemcpyAsync(t.root, t.layers[nl].p, 32, hipMemcpyDeviceToHost, st));
-  HIP_CHECK(hipStreamSynchronize(st));
+  build_layers(t, h0, sorted, next, st);
 }
 
 void merkle_layers_from_leaves(MerkleTree& t, hipStream_t st) {
-  size_t len = t.mats.empty() ? 0 : t.mats[0].height;
-  const int nl = log2i(len);
-  t.layers.resize(nl + 1);
-  ColList none{};
-  none.n = 0;
-  for (int L = 1; L <= nl; L++) {
-    const size_t nlen = len / 2;
-    t.layers[L].reset(8 * nlen);
-    hipLaunchKernelGGL(k_compress, dim3(ceil_div(nlen, 256)), dim3(256), 0, st,
-                       (const uint32_t*)t.layers[L - 1].p, nlen, t.layers[L].p, none);
-    KCHECK();
-    len = nlen;
-  }
-  HIP_CHECK(hipMemcpyAsync(t.root, t.layers[nl].p, 32, hipMemcpyDeviceToHost, st));
-  HIP_CHECK(hipStreamSynchronize(st));
+  const size_t len = t.mats.empty() ? 0 : t.mats[0].height;
+  t.layers.resize(log2i(len) + 1);
+  build_layers(t, len, {}, 0, st);
 }
 
 void poseidon2_batch(uint32_t* states, size_t n, hipStream_t st) {

@@ -66,6 +66,144 @@ __global__ __launch_bounds__(256) void k_ntt_pass(const uint32_t* __restrict__ s
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Register-resident radix-16 pass.  A tile is 2^(b+c) elements: 2^b points of a butterfly
+// group (stride 2^s0) x 2^c adjacent groups (coalesced runs).  Every thread holds 16
+// elements; each "window" of 4 index bits is done in registers (4 stages, butterfly
+// twiddle = one table value x a compile-time root of order <= 16), and windows exchange
+// through LDS.  The first window loads straight from HBM and the last stores straight
+// back, so a pass is one read + one write of the data.
+constexpr uint32_t G24 = cpow(3, 127);
+constexpr uint32_t root_pow2(int k) {  // w_(2^k), canonical
+  uint32_t g = G24;
+  for (int i = k; i < 24; i++) g = cmul(g, g);
+  return g;
+}
+struct SmallRoots {
+  uint32_t f[16], i[16];  // [2^k + l] = w_(2^(k+1))^(+-l), k = 0..3 (Montgomery)
+};
+constexpr SmallRoots make_small_roots() {
+  SmallRoots r{};
+  for (int k = 0; k < 4; k++) {
+    const uint32_t w = root_pow2(k + 1), wi = cpow(w, P - 2);
+    uint32_t a = 1, b = 1;
+    for (int l = 0; l < (1 << k); l++) {
+      r.f[(1 << k) + l] = to_mont_c(a);
+      r.i[(1 << k) + l] = to_mont_c(b);
+      a = cmul(a, w);
+      b = cmul(b, wi);
+    }
+  }
+  return r;
+}
+constexpr SmallRoots SMALL = make_small_roots();
+
+constexpr int R16_TILE_LOG = 14;  // 16384 elements per tile, 1024 threads x 16
+
+__device__ __forceinline__ int lds_pad(int idx, int c) { return c < 5 ? idx + (idx >> 4) : idx; }
+
+template <bool DIF>
+__device__ __forceinline__ void r16_window(uint32_t (&x)[16], int g0, int kk_lo, int kk_hi, int s0,
+                                           uint32_t m_low, uint32_t lo_g, const uint32_t* __restrict__ tw) {
+  // performs stages t = g0 + kk for kk in [kk_lo, kk_hi), ascending (DIT) or descending (DIF)
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int kk = DIF ? 3 - q : q;
+    if (kk < kk_lo || kk >= kk_hi) continue;
+    const int t = g0 + kk;
+    const uint32_t wb = tw[(1u << (s0 + t)) + (m_low << s0) + lo_g];
+    uint32_t tws[8];
+#pragma unroll
+    for (int l = 0; l < 8; l++)
+      if (l < (1 << kk)) tws[l] = l == 0 ? wb : mmul(wb, DIF ? SMALL.f[(1 << kk) + l] : SMALL.i[(1 << kk) + l]);
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      if (i & (1 << kk)) continue;
+      const int j = i | (1 << kk);
+      const uint32_t w = tws[i & ((1 << kk) - 1)];
+      const uint32_t u = x[i], v = x[j];
+      if (DIF) {
+        x[i] = madd(u, v);
+        x[j] = mmul(msub(u, v), w);
+      } else {
+        const uint32_t vw = mmul(v, w);
+        x[i] = madd(u, vw);
+        x[j] = msub(u, vw);
+      }
+    }
+  }
+}
+
+template <bool DIF>
+__global__ __launch_bounds__(1024) void k_ntt_r16(const uint32_t* __restrict__ src,
+                                                  uint32_t* __restrict__ dst, size_t src_stride,
+                                                  size_t dst_stride, int s0, int b, int c,
+                                                  const uint32_t* __restrict__ tw) {
+  extern __shared__ uint32_t lds[];
+  const int tid = threadIdx.x;
+  const int nlo_log = s0 - c;
+  const size_t lo_blk = blockIdx.x & ((1u << nlo_log) - 1);
+  const size_t hi = (size_t)blockIdx.x >> nlo_log;
+  const size_t base = (hi << (s0 + b)) + (lo_blk << c);
+  const uint32_t* S = src + (size_t)blockIdx.y * src_stride + base;
+  uint32_t* D = dst + (size_t)blockIdx.y * dst_stride + base;
+  const int lo = tid & ((1 << c) - 1);
+  const uint32_t lo_g = (uint32_t)(lo_blk << c) + lo;
+  const int rest = tid >> c;
+  const int nwin = (b + 3) >> 2;
+  // A contiguous tile (c == 0) is moved between HBM and LDS with thread t touching elements
+  // t, t + T, t + 2T, ... so every wave instruction is one 256-byte segment; the window
+  // pattern (16 adjacent elements per thread in the first DIT window) would otherwise
+  // stride 64 bytes across the lanes of a wave.
+  const bool stage = (c == 0);
+  const int T = (int)blockDim.x;
+  uint32_t x[16];
+  if (stage) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) lds[lds_pad(i * T + tid, 0)] = S[(uint32_t)(i * T + tid)];
+  }
+  int done_lo = 0, done_hi = b;  // DIT: stages < done_lo done; DIF: stages >= done_hi done
+  for (int w = 0; w < nwin; w++) {
+    const int g0 = DIF ? max(b - 4 - 4 * w, 0) : min(4 * w, b - 4);
+    const uint32_t m_low = rest & ((1 << g0) - 1);
+    const uint32_t m_base = m_low | ((uint32_t)(rest >> g0) << (g0 + 4));
+    if (w == 0 && !stage) {
+#pragma unroll
+      for (int i = 0; i < 16; i++) x[i] = S[(uint32_t)((m_base | ((uint32_t)i << g0)) << s0) + lo];
+    } else {
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 16; i++)
+        x[i] = lds[lds_pad((int)(((m_base | ((uint32_t)i << g0)) << c) | lo), c)];
+    }
+    int kk_lo, kk_hi;
+    if (DIF) {
+      kk_lo = 0;
+      kk_hi = min(4, done_hi - g0);
+      done_hi = g0;
+    } else {
+      kk_lo = max(0, done_lo - g0);
+      kk_hi = 4;
+      done_lo = g0 + 4;
+    }
+    r16_window<DIF>(x, g0, kk_lo, kk_hi, s0, m_low, lo_g, tw);
+    if (w == nwin - 1 && !stage) {
+#pragma unroll
+      for (int i = 0; i < 16; i++) D[(uint32_t)((m_base | ((uint32_t)i << g0)) << s0) + lo] = x[i];
+    } else {
+      // each thread rewrites exactly the slots it read for this window: no barrier needed
+#pragma unroll
+      for (int i = 0; i < 16; i++)
+        lds[lds_pad((int)(((m_base | ((uint32_t)i << g0)) << c) | lo), c)] = x[i];
+    }
+  }
+  if (stage) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 16; i++) D[(uint32_t)(i * T + tid)] = lds[lds_pad(i * T + tid, 0)];
+  }
+}
+
 // lo_k = c_k * s^k / n ; hi_k = c_k * t^k / n  with s^k = SL[k & m] * SH[k >> B] (1/n in SH)
 __global__ __launch_bounds__(256) void k_scale_split(const uint32_t* __restrict__ coef,
                                                      uint32_t* __restrict__ lde, size_t n, int B,
@@ -135,10 +273,55 @@ std::vector<std::pair<int, int>> ntt_plan(int L) {
   return p;
 }
 
+struct R16Pass {
+  int s0, b, c;
+};
+// L <= 14: one pass; otherwise two: a fully contiguous first pass of up to 14 stages and a
+// strided second pass with 2^c-element coalesced runs (c <= 6).
+static std::vector<R16Pass> r16_plan(int L) {
+  if (L <= R16_TILE_LOG) return {{0, L, 0}};
+  const int b1 = std::min(R16_TILE_LOG, L - 4), b2 = L - b1;
+  const int c2 = std::min({b1, R16_TILE_LOG - b2, 6});
+  return {{0, b1, 0}, {b1, b2, c2}};
+}
+
+static void r16_attrs() {
+  static bool done = false;
+  if (done) return;
+  const int bytes = ((1 << R16_TILE_LOG) + (1 << (R16_TILE_LOG - 4))) * 4;
+  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_r16<true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_r16<false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  done = true;
+}
+
 void ntt_passes(const uint32_t* src, uint32_t* dst, size_t src_stride, size_t dst_stride, int ncols,
                 int L, bool dif, hipStream_t st) {
   Twiddles& T = twiddles();
   T.ensure(std::max(L, 1));
+  if (L >= 4) {
+    r16_attrs();
+    auto plan = r16_plan(L);
+    if (dif) std::reverse(plan.begin(), plan.end());
+    bool first = true;
+    for (const R16Pass& p : plan) {
+      const int threads = 1 << (p.b + p.c - 4);
+      const size_t lds = ((size_t)1 << (p.b + p.c)) + ((size_t)1 << (p.b + p.c - 4));
+      dim3 grid(1u << (L - p.b - p.c), ncols);
+      const uint32_t* in = first ? src : dst;
+      const size_t is = first ? src_stride : dst_stride;
+      if (dif)
+        hipLaunchKernelGGL(k_ntt_r16<true>, grid, dim3(threads), lds * 4, st, in, dst, is,
+                           dst_stride, p.s0, p.b, p.c, (const uint32_t*)T.fwd.p);
+      else
+        hipLaunchKernelGGL(k_ntt_r16<false>, grid, dim3(threads), lds * 4, st, in, dst, is,
+                           dst_stride, p.s0, p.b, p.c, (const uint32_t*)T.inv.p);
+      KCHECK();
+      first = false;
+    }
+    return;
+  }
   auto plan = ntt_plan(L);
   if (dif) std::reverse(plan.begin(), plan.end());
   bool first = true;

@@ -82,8 +82,24 @@ KB_HD void poseidon2_permute(uint32_t s[16]) {
     uint32_t a2 = madd(madd(s[8], s[9]), madd(s[10], s[11]));
     uint32_t a3 = madd(madd(s[12], s[13]), madd(s[14], s[15]));
     uint32_t sum = madd(madd(a0, a1), madd(a2, a3));
-#pragma unroll
-    for (int i = 0; i < 16; i++) s[i] = madd(sum, mmul(P2.diag[i], s[i]));
+    // s_i <- sum + d_i s_i with d = [-2,1,2,1/2,3,4,-1/2,-3,-4,1/2^8,1/8,1/2^24,-1/2^8,-1/8,
+    // -1/16,-1/2^24]: every d_i is a shift/add (Montgomery form is linear in the value).
+    s[0] = msub(sum, mdbl(s[0]));
+    s[1] = madd(sum, s[1]);
+    s[2] = madd(sum, mdbl(s[2]));
+    s[3] = madd(sum, mdiv2k<1>(s[3]));
+    s[4] = madd(sum, madd(mdbl(s[4]), s[4]));
+    s[5] = madd(sum, mdbl(mdbl(s[5])));
+    s[6] = msub(sum, mdiv2k<1>(s[6]));
+    s[7] = msub(sum, madd(mdbl(s[7]), s[7]));
+    s[8] = msub(sum, mdbl(mdbl(s[8])));
+    s[9] = madd(sum, mdiv2k<8>(s[9]));
+    s[10] = madd(sum, mdiv2k<3>(s[10]));
+    s[11] = madd(sum, mdiv2k<24>(s[11]));
+    s[12] = msub(sum, mdiv2k<8>(s[12]));
+    s[13] = msub(sum, mdiv2k<3>(s[13]));
+    s[14] = msub(sum, mdiv2k<4>(s[14]));
+    s[15] = msub(sum, mdiv2k<24>(s[15]));
   }
 #pragma unroll
   for (int r = 0; r < 4; r++) {
