@@ -43,14 +43,17 @@ typedef struct bfz_record bfz_record; /* executed record with traces resident in
 
 typedef struct {
   double upload_ms, main_commit_ms, perm_ms, quotient_ms, open_ms, fri_ms, total_ms;
-  double lde_ms, lde_bytes;
+  double lde_ms, lde_bytes; /* whole coset LDEs: 12*n*w algorithmic bytes per call */
   int lde_calls;
+  double ntt_kernel_ms, ntt_kernel_bytes; /* NTT pass kernel, per-launch events, 8 B/element */
+  int ntt_kernel_launches;
 } bfz_timings;
 
 int bfz_init(int device);
 const char* bfz_last_error(void);
 int bfz_device_name(char* buf, size_t cap);
 void bfz_free(void* p);
+int bfz_synchronize(void); /* hipDeviceSynchronize on the bound device */
 
 int bfz_execute(const char* elf, const uint8_t* stdin_data, size_t nin, uint8_t* out,
                 size_t out_cap, size_t* out_len, uint64_t* cycles);
@@ -68,6 +71,13 @@ void bfz_pk_free(bfz_pk* pk);
 
 int bfz_prove(const bfz_pk* pk, const uint8_t* stdin_data, size_t nin, uint8_t** proof,
               size_t* proof_len);
+/* MachineProver::prove from host traces (crates/stark/src/prover.rs:560-582 after
+ * generate_dependencies + generate_traces, prover.rs:58-81): chips[i] is the chip index in
+ * BfAir::chips() order, traces[i] its row-major Montgomery main trace (heights[i] x
+ * widths[i], height a power of two).  Preprocessed traces come from the proving key. */
+int bfz_prove_traces(const bfz_pk* pk, const int* chips, const uint32_t* const* traces,
+                     const size_t* heights, const size_t* widths, size_t nchips, uint8_t** proof,
+                     size_t* proof_len);
 int bfz_verify(const char* elf, const uint32_t vk_commit[8], const uint8_t* proof,
                size_t proof_len);
 

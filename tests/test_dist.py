@@ -1,0 +1,51 @@
+"""N>1 path of bench.py on CPU: two gloo ranks run the same timed_steps() the GPU bench uses
+(barriers + max over ranks); every rank proves its own replica, so no data-path collective."""
+import os
+import socket
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank(rank, world, port, q):
+    import time
+
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    calls = []
+    # rank 1 is the slow replica: 40 ms per step vs 5 ms
+    ms = bench.timed_steps(lambda: (calls.append(1), time.sleep(0.04 if rank else 0.005)), 3,
+                           dist)
+    q.put((rank, ms, len(calls)))
+    dist.destroy_process_group()
+
+
+def test_timed_steps_two_gloo_ranks_take_max():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, ms0, n0), (_, ms1, n1) = res
+    assert n0 == n1 == 3            # exactly K steps on every rank
+    assert ms0 == ms1               # every rank reports the same (max) value
+    assert ms0 >= 40.0              # ... which is the slow rank's pace

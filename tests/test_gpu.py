@@ -91,6 +91,32 @@ def test_proof_bytes_match_oracle(client, name, prog, stdin):
     assert O.verify(prog, pf.proof)            # oracle verifier
 
 
+def test_prove_from_host_traces_matches(client):
+    """MachineProver boundary: traces produced on the host (generate_traces) proved through
+    bfz_prove_traces give the same bytes as the record path and the oracle."""
+    pk, vk = client.setup(guests.FIBO)
+    traces = sdk.generate_traces(guests.FIBO, [17])
+    assert [name for _, name, _ in traces][0] == "Cpu"
+    for c, name, t in traces:  # the same traces the oracle generates (canonical form)
+        assert np.array_equal(unmont(t), O.trace(guests.FIBO, [17], c)), name
+    pf = sdk.CoreProver().prove(pk, traces)
+    assert pf == client.prove(pk, [17]).run().proof
+    assert pf == O.prove(guests.FIBO, [17])
+    client.verify(sdk.BfProofWithPublicValues(proof=pf, stdin=bytes([17])), vk)
+
+
+def test_prove_traces_rejects_bad_shapes(client):
+    pk, _ = client.setup(guests.HELLO)
+    traces = sdk.generate_traces(guests.HELLO, [])
+    c, name, t = traces[0]
+    with pytest.raises(_lib.BfzError, match="width mismatch"):
+        sdk.CoreProver().prove(pk, [(c, name, t[:, :-1])] + traces[1:])
+    with pytest.raises(_lib.BfzError, match="power of two"):
+        sdk.CoreProver().prove(pk, [(c, name, t[:-1])] + traces[1:])
+    with pytest.raises(_lib.BfzError, match="repeated"):
+        sdk.CoreProver().prove(pk, traces + traces[:1])
+
+
 def test_fibo17_end_to_end_sdk(client):
     """crates/sdk/src/lib.rs:186-196 test_e2e_core, through the SDK mirror."""
     pk, vk = client.setup(guests.FIBO)

@@ -23,7 +23,8 @@ class Timings(ctypes.Structure):
         ("upload_ms", c_double), ("main_commit_ms", c_double), ("perm_ms", c_double),
         ("quotient_ms", c_double), ("open_ms", c_double), ("fri_ms", c_double),
         ("total_ms", c_double), ("lde_ms", c_double), ("lde_bytes", c_double),
-        ("lde_calls", c_int),
+        ("lde_calls", c_int), ("ntt_kernel_ms", c_double), ("ntt_kernel_bytes", c_double),
+        ("ntt_kernel_launches", c_int),
     ]
 
     def as_dict(self) -> dict:
@@ -36,6 +37,7 @@ SIGNATURES = [
     ("bfz_last_error", c_char_p, []),
     ("bfz_device_name", c_int, [c_char_p, c_size_t]),
     ("bfz_free", None, [c_void_p]),
+    ("bfz_synchronize", c_int, []),
     ("bfz_execute", c_int, [c_char_p, POINTER(c_uint8), c_size_t, POINTER(c_uint8), c_size_t,
                             POINTER(c_size_t), POINTER(c_uint64)]),
     ("bfz_trace", c_int, [c_char_p, POINTER(c_uint8), c_size_t, c_int, c_int,
@@ -44,6 +46,9 @@ SIGNATURES = [
     ("bfz_pk_free", None, [c_void_p]),
     ("bfz_prove", c_int, [c_void_p, POINTER(c_uint8), c_size_t, POINTER(POINTER(c_uint8)),
                           POINTER(c_size_t)]),
+    ("bfz_prove_traces", c_int, [c_void_p, POINTER(c_int), POINTER(POINTER(c_uint32)),
+                                 POINTER(c_size_t), POINTER(c_size_t), c_size_t,
+                                 POINTER(POINTER(c_uint8)), POINTER(c_size_t)]),
     ("bfz_verify", c_int, [c_char_p, POINTER(c_uint32), POINTER(c_uint8), c_size_t]),
     ("bfz_record_new", c_int, [c_void_p, POINTER(c_uint8), c_size_t, POINTER(c_void_p),
                                POINTER(c_uint64)]),

@@ -7,6 +7,11 @@ bfz C ABI.  Same names, argument meaning and error behaviour:
     proof = client.prove(pk, stdin).run()        # ProverClient::prove      lib.rs:92-94
     client.verify(proof, vk)                     # ProverClient::verify     lib.rs:110-116
 
+and of the core MachineProver boundary (crates/stark/src/prover.rs:27-150):
+
+    traces = generate_traces(elf, stdin)         # generate_traces          prover.rs:58-81
+    proof = CoreProver().prove(pk, traces)       # MachineProver::prove     prover.rs:560-582
+
 Errors raise (the reference returns Err / panics in the same places).  Proving runs on the GPU
 through libbfz; verification runs the host verifier compiled into the same library.
 """
@@ -115,6 +120,52 @@ class ProverClient:
         buf, n = u8buf(proof.proof)
         commit = (ctypes.c_uint32 * 8)(*vk.commit)
         check(lib().bfz_verify(vk.elf.encode(), commit, buf, n))
+
+
+# BfAir::chips() order (crates/core/machine/src/brainfuck/mod.rs:53-81) = chip index in the ABI
+CHIPS = ("Cpu", "Program", "AddSub", "Jump", "Memory", "Byte", "MemoryInstrs", "IO")
+
+
+def generate_traces(elf: str, stdin) -> list:
+    """Execute + generate_dependencies + generate_traces: [(chip index, name, trace)] for the
+    chips the record includes, each trace a (height, width) uint32 array in Montgomery form
+    (the byte layout of the reference's RowMajorMatrix<KoalaBear>)."""
+    import numpy as np
+    buf, n = u8buf(bytes(stdin))
+    out = []
+    for c, name in enumerate(CHIPS):
+        p = ctypes.POINTER(ctypes.c_uint32)()
+        h, w = ctypes.c_size_t(), ctypes.c_size_t()
+        rc = lib().bfz_trace(elf.encode(), buf, n, c, 0, ctypes.byref(p), ctypes.byref(h),
+                             ctypes.byref(w))
+        if rc == 1:
+            continue
+        check(rc)
+        arr = np.ctypeslib.as_array(p, shape=(h.value * w.value,)).copy()
+        lib().bfz_free(p)
+        out.append((c, name, arr.reshape(h.value, w.value)))
+    return out
+
+
+class CoreProver:
+    """HIP implementation of MachineProver::prove (crates/stark/src/prover.rs:560-582) from
+    host traces: commit, LogUp, quotient and open run on the device."""
+
+    def prove(self, pk: BfProvingKey, traces) -> bytes:
+        import numpy as np
+        init()
+        mats = [np.ascontiguousarray(t, dtype=np.uint32) for _, _, t in traces]
+        k = len(mats)
+        chips = (ctypes.c_int * k)(*[c for c, _, _ in traces])
+        ptrs = (ctypes.POINTER(ctypes.c_uint32) * k)(
+            *[m.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)) for m in mats])
+        hs = (ctypes.c_size_t * k)(*[m.shape[0] for m in mats])
+        ws = (ctypes.c_size_t * k)(*[m.shape[1] for m in mats])
+        ptr = ctypes.POINTER(ctypes.c_uint8)()
+        plen = ctypes.c_size_t()
+        check(lib().bfz_prove_traces(ctypes.c_void_p(pk.handle), chips, ptrs, hs, ws, k,
+                                     ctypes.byref(ptr), ctypes.byref(plen)))
+        return take_bytes(ptr, plen.value)
 
 
 def set_num_queries(q: int) -> None:

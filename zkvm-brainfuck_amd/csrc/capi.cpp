@@ -145,6 +145,23 @@ int bfz_prove(const bfz_pk* pk, const uint8_t* in, size_t nin, uint8_t** proof, 
   return guarded([&] { return emit(bfz::prove(*pk->pk, in, nin, opts(), nullptr), proof, len); });
 }
 
+int bfz_synchronize(void) {
+  return guarded([&] {
+    HIP_CHECK(hipDeviceSynchronize());
+    return 0;
+  });
+}
+
+int bfz_prove_traces(const bfz_pk* pk, const int* chips, const uint32_t* const* traces,
+                     const size_t* heights, const size_t* widths, size_t nchips, uint8_t** proof,
+                     size_t* len) {
+  return guarded([&] {
+    bfz::DeviceTraces dt;
+    bfz::upload_host_traces(chips, traces, heights, widths, nchips, dt, bfz::stream());
+    return emit(bfz::prove_device(*pk->pk, dt, opts(), nullptr), proof, len);
+  });
+}
+
 int bfz_verify(const char* elf, const uint32_t vk_commit[8], const uint8_t* proof, size_t len) {
   return guarded([&] {
     std::string why;
@@ -190,6 +207,9 @@ int bfz_record_prove(const bfz_pk* pk, const bfz_record* rec, uint8_t** proof, s
       t->lde_ms = st.lde_ms;
       t->lde_bytes = st.lde_bytes;
       t->lde_calls = st.lde_calls;
+      t->ntt_kernel_ms = st.ntt_kernel_ms;
+      t->ntt_kernel_bytes = st.ntt_kernel_bytes;
+      t->ntt_kernel_launches = st.ntt_kernel_launches;
     }
     return emit(std::move(v), proof, len);
   });

@@ -133,4 +133,49 @@ Twiddles& twiddles();
 
 hipStream_t stream();
 
+// Per-launch HIP-event timing of one kernel family (the roofline kernel of bench.py):
+// when `on`, callers bracket each launch with begin()/end(bytes); collect() resolves the
+// events after the stream has drained.  Event creation is host work, so it is only switched
+// on for the one instrumented proof.
+struct KernelProbe {
+  bool on = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  std::vector<double> ev_bytes;
+  double ms = 0, bytes = 0;
+  int launches = 0;
+  hipEvent_t begin(hipStream_t st) {
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreate(&e));
+    HIP_CHECK(hipEventRecord(e, st));
+    return e;
+  }
+  void end(hipEvent_t b, hipStream_t st, double nbytes) {
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreate(&e));
+    HIP_CHECK(hipEventRecord(e, st));
+    ev.push_back({b, e});
+    ev_bytes.push_back(nbytes);
+  }
+  void collect() {
+    for (size_t i = 0; i < ev.size(); i++) {
+      HIP_CHECK(hipEventSynchronize(ev[i].second));
+      float t = 0;
+      HIP_CHECK(hipEventElapsedTime(&t, ev[i].first, ev[i].second));
+      ms += t;
+      bytes += ev_bytes[i];
+      launches++;
+      HIP_CHECK(hipEventDestroy(ev[i].first));
+      HIP_CHECK(hipEventDestroy(ev[i].second));
+    }
+    ev.clear();
+    ev_bytes.clear();
+  }
+  void reset() {
+    collect();
+    ms = bytes = 0;
+    launches = 0;
+  }
+};
+KernelProbe& ntt_probe();  // k_ntt_r16 passes: 8 B per element (one read + one write)
+
 }  // namespace bfz

@@ -55,15 +55,6 @@ KB_HD uint32_t msub(uint32_t a, uint32_t b) {
   uint32_t d = a - b;
   return umin(d, d + P);
 }
-// x * 2^-k (k <= 24) of a value (or its Montgomery form) in [0, p): with m = -x mod 2^k,
-// (x + m p) / 2^k = (x + m) / 2^k + m * 127 * 2^(24-k), both terms exact.
-template <int K>
-KB_HD uint32_t mdiv2k(uint32_t x) {
-  static_assert(K >= 1 && K <= 24, "K");
-  const uint32_t m = (0u - x) & ((1u << K) - 1);
-  const uint32_t y = ((x + m) >> K) + (m << (31 - K)) - (m << (24 - K));
-  return umin(y, y - P);
-}
 KB_HD uint32_t mneg(uint32_t a) { return a ? P - a : 0; }
 KB_HD uint32_t mdbl(uint32_t a) { return madd(a, a); }
 

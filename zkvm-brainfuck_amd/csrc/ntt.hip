@@ -311,6 +311,8 @@ void ntt_passes(const uint32_t* src, uint32_t* dst, size_t src_stride, size_t ds
       dim3 grid(1u << (L - p.b - p.c), ncols);
       const uint32_t* in = first ? src : dst;
       const size_t is = first ? src_stride : dst_stride;
+      KernelProbe& probe = ntt_probe();
+      hipEvent_t ev0 = probe.on ? probe.begin(st) : nullptr;
       if (dif)
         hipLaunchKernelGGL(k_ntt_r16<true>, grid, dim3(threads), lds * 4, st, in, dst, is,
                            dst_stride, p.s0, p.b, p.c, (const uint32_t*)T.fwd.p);
@@ -318,6 +320,7 @@ void ntt_passes(const uint32_t* src, uint32_t* dst, size_t src_stride, size_t ds
         hipLaunchKernelGGL(k_ntt_r16<false>, grid, dim3(threads), lds * 4, st, in, dst, is,
                            dst_stride, p.s0, p.b, p.c, (const uint32_t*)T.inv.p);
       KCHECK();
+      if (probe.on) probe.end(ev0, st, 8.0 * (double)((size_t)1 << L) * ncols);
       first = false;
     }
     return;

@@ -19,6 +19,7 @@ struct P2Tables {
   uint32_t ext_term[4][16];
   uint32_t internal[13];
   uint32_t diag[16];
+  uint32_t dabs[16];  // |d_i| (Montgomery)
 };
 
 constexpr uint32_t RC_RAW[30 * 16] = {
@@ -40,7 +41,12 @@ constexpr P2Tables make_p2_tables() {
                     4,              cneg(cinv(2)), cneg(3), cneg(4),          cinv(256),
                     cinv(8),        cinv(1u << 24), cneg(cinv(256)), cneg(cinv(8)), cneg(cinv(16)),
                     cneg(cinv(1u << 24))};
-  for (int i = 0; i < 16; i++) t.diag[i] = to_mont_c(d[i]);
+  uint32_t da[16] = {2, 1, 2, cinv(2), 3, 4, cinv(2), 3, 4, cinv(256), cinv(8), cinv(1u << 24),
+                     cinv(256), cinv(8), cinv(16), cinv(1u << 24)};
+  for (int i = 0; i < 16; i++) {
+    t.diag[i] = to_mont_c(d[i]);
+    t.dabs[i] = to_mont_c(da[i]);
+  }
   return t;
 }
 
@@ -83,23 +89,25 @@ KB_HD void poseidon2_permute(uint32_t s[16]) {
     uint32_t a3 = madd(madd(s[12], s[13]), madd(s[14], s[15]));
     uint32_t sum = madd(madd(a0, a1), madd(a2, a3));
     // s_i <- sum + d_i s_i with d = [-2,1,2,1/2,3,4,-1/2,-3,-4,1/2^8,1/8,1/2^24,-1/2^8,-1/8,
-    // -1/16,-1/2^24]: every d_i is a shift/add (Montgomery form is linear in the value).
+    // -1/16,-1/2^24].  Small integers use doublings; the fractions are one Montgomery
+    // multiply by |d_i| (cheaper on gfx950 than shifting: v_lshlrev/v_min are half rate,
+    // scripts/ubench_valu.hip), the sign folds into add/sub.
     s[0] = msub(sum, mdbl(s[0]));
     s[1] = madd(sum, s[1]);
     s[2] = madd(sum, mdbl(s[2]));
-    s[3] = madd(sum, mdiv2k<1>(s[3]));
+    s[3] = madd(sum, mmul(s[3], P2.dabs[3]));
     s[4] = madd(sum, madd(mdbl(s[4]), s[4]));
     s[5] = madd(sum, mdbl(mdbl(s[5])));
-    s[6] = msub(sum, mdiv2k<1>(s[6]));
+    s[6] = msub(sum, mmul(s[6], P2.dabs[6]));
     s[7] = msub(sum, madd(mdbl(s[7]), s[7]));
     s[8] = msub(sum, mdbl(mdbl(s[8])));
-    s[9] = madd(sum, mdiv2k<8>(s[9]));
-    s[10] = madd(sum, mdiv2k<3>(s[10]));
-    s[11] = madd(sum, mdiv2k<24>(s[11]));
-    s[12] = msub(sum, mdiv2k<8>(s[12]));
-    s[13] = msub(sum, mdiv2k<3>(s[13]));
-    s[14] = msub(sum, mdiv2k<4>(s[14]));
-    s[15] = msub(sum, mdiv2k<24>(s[15]));
+    s[9] = madd(sum, mmul(s[9], P2.dabs[9]));
+    s[10] = madd(sum, mmul(s[10], P2.dabs[10]));
+    s[11] = madd(sum, mmul(s[11], P2.dabs[11]));
+    s[12] = msub(sum, mmul(s[12], P2.dabs[12]));
+    s[13] = msub(sum, mmul(s[13], P2.dabs[13]));
+    s[14] = msub(sum, mmul(s[14], P2.dabs[14]));
+    s[15] = msub(sum, mmul(s[15], P2.dabs[15]));
   }
 #pragma unroll
   for (int r = 0; r < 4; r++) {

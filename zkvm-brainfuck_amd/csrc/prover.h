@@ -59,6 +59,9 @@ struct StageTimes {          // milliseconds, measured with HIP events on the pr
   double lde_ms = 0;         // sum over coset_lde calls
   double lde_bytes = 0;      // algorithmic bytes: 12 * n * w per call
   int lde_calls = 0;
+  double ntt_kernel_ms = 0;     // k_ntt_r16 launches, one event pair per launch
+  double ntt_kernel_bytes = 0;  // 8 B per element per pass
+  int ntt_kernel_launches = 0;
 };
 
 std::unique_ptr<ProvingKey> setup(const std::string& program_src);
@@ -85,6 +88,10 @@ struct DeviceTraces {
   std::vector<size_t> heights;
 };
 void upload_traces(const ExecutionRecord& rec, DeviceTraces& dt, hipStream_t st);
+// Host main traces as MachineProver::generate_traces returns them (row-major Montgomery,
+// one per included chip); validates chip ids, widths and power-of-two heights.
+void upload_host_traces(const int* chips, const uint32_t* const* mats, const size_t* heights,
+                        const size_t* widths, size_t n, DeviceTraces& dt, hipStream_t st);
 std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const ProveOptions& opt,
                                   StageTimes* times);
 

@@ -203,6 +203,35 @@ void upload_traces(const ExecutionRecord& rec, DeviceTraces& dt, hipStream_t st)
   }
 }
 
+void upload_host_traces(const int* chips, const uint32_t* const* mats, const size_t* heights,
+                        const size_t* widths, size_t n, DeviceTraces& dt, hipStream_t st) {
+  dt.chips.clear();
+  dt.evals.clear();
+  dt.heights.clear();
+  bool seen[NUM_CHIPS] = {};
+  for (size_t i = 0; i < n; i++) {
+    const int c = chips[i];
+    if (c < 0 || c >= NUM_CHIPS || seen[c]) throw std::runtime_error("traces: bad or repeated chip id");
+    seen[c] = true;
+    const size_t h = heights[i];
+    const int w = CHIP_INFO[c].main_w;
+    if ((size_t)w != widths[i])
+      throw std::runtime_error(std::string("traces: width mismatch for ") + CHIP_INFO[c].name);
+    if (h == 0 || (h & (h - 1)) || h > ((size_t)1 << 23))
+      throw std::runtime_error(std::string("traces: height not a power of two <= 2^23 for ") +
+                               CHIP_INFO[c].name);
+    DBuf<uint32_t> rm(h * w);
+    HIP_CHECK(hipMemcpyAsync(rm.p, mats[i], h * w * 4, hipMemcpyHostToDevice, st));
+    DBuf<uint32_t> ev(h * w);
+    transpose_bitrev(rm.p, h, w, ev.p, st);
+    HIP_CHECK(hipStreamSynchronize(st));
+    dt.chips.push_back(c);
+    dt.evals.push_back(std::move(ev));
+    dt.heights.push_back(h);
+  }
+  if (!seen[0]) throw std::runtime_error("traces: the Cpu chip is required");
+}
+
 // ------------------------------------------------------------------------ prove
 std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const ProveOptions& opt,
                                   StageTimes* times) {
@@ -211,6 +240,8 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
   StageTimes* tms = times ? times : &local_times;
   EvTimer ev;
   ev.on = opt.timing && times;
+  ntt_probe().reset();
+  ntt_probe().on = ev.on;
   std::vector<std::vector<EF>> keep;  // host buffers of async uploads live until the end
   const auto t_start = std::chrono::steady_clock::now();
   hipEvent_t e_total = ev.on ? ev.begin(st) : nullptr;
@@ -584,6 +615,12 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
   if (ev.on) {
     ev.end(e_total, st, &tms->total);
     ev.collect();
+    KernelProbe& pr = ntt_probe();
+    pr.collect();
+    pr.on = false;
+    tms->ntt_kernel_ms = pr.ms;
+    tms->ntt_kernel_bytes = pr.bytes;
+    tms->ntt_kernel_launches = pr.launches;
   }
   (void)t_start;
   return std::move(w.b);

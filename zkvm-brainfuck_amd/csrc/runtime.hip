@@ -17,6 +17,11 @@ hipStream_t stream() {
   return s;
 }
 
+KernelProbe& ntt_probe() {
+  static KernelProbe* k = new KernelProbe();
+  return *k;
+}
+
 Twiddles& twiddles() {
   static Twiddles* t = new Twiddles();
   return *t;
