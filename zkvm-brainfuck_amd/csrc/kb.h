@@ -27,6 +27,14 @@ static_assert(uint32_t(P * MU) == 1u, "MU");
 static_assert(MU == (uint32_t)(1u + (1u << 24) - (1u << 31)), "MU shape");
 KB_HD uint32_t mont_m(uint32_t lo) { return lo + (lo << 24) - (lo << 31); }
 KB_HD uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+// Optimization barrier for one VGPR value (no instruction): stops the compiler from fusing a
+// 32-bit "hi - mh" back into a 64-bit borrow chain around it.
+KB_HD uint32_t opaque(uint32_t x) {
+#ifdef __HIP_DEVICE_COMPILE__
+  asm("" : "+v"(x));
+#endif
+  return x;
+}
 
 // Montgomery reduction of t < 2^64 with hi(t) < 2p: result in [0, p).
 KB_HD uint32_t mreduce(uint64_t t) {
@@ -56,7 +64,16 @@ KB_HD uint32_t msub(uint32_t a, uint32_t b) {
   return umin(d, d + P);
 }
 KB_HD uint32_t mneg(uint32_t a) { return a ? P - a : 0; }
-KB_HD uint32_t mdbl(uint32_t a) { return madd(a, a); }
+// 2a: on gfx950 the compiler's a << 1 is a half-rate v_lshlrev; v_add_u32 a, a is full rate.
+KB_HD uint32_t mdbl(uint32_t a) {
+#ifdef __HIP_DEVICE_COMPILE__
+  uint32_t s;
+  asm("v_add_u32 %0, %1, %1" : "=v"(s) : "v"(a));
+#else
+  const uint32_t s = a + a;
+#endif
+  return umin(s, s - P);
+}
 
 constexpr uint32_t to_mont_c(uint32_t x) {
   return (uint32_t)((((uint64_t)(x % P)) << 32) % P);

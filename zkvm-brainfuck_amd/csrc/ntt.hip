@@ -102,7 +102,14 @@ constexpr int R16_TILE_LOG = 14;  // 16384 elements per tile, 1024 threads x 16
 
 __device__ __forceinline__ int lds_pad(int idx, int c) { return c < 5 ? idx + (idx >> 4) : idx; }
 
-template <bool DIF>
+// One 4-stage window on a thread's 16 elements.  Lazy reduction: a Montgomery product only
+// needs its multiplicand < 2^32, so
+//   DIT: an output of stage kk < 3 whose index has bit kk+1 set is the multiplied operand of
+//        the next stage and stays in [0, 2p) (saves the min() of its add/sub);
+//   DIF: u - v + p feeds the twiddle product directly.
+// CONST_TW: the tile's base twiddle is 1 (first DIT / last DIF window of a pass starting at
+// stage 0), so the twiddles are the compile-time small roots and w = 1 products vanish.
+template <bool DIF, bool CONST_TW>
 __device__ __forceinline__ void r16_window(uint32_t (&x)[16], int g0, int kk_lo, int kk_hi, int s0,
                                            uint32_t m_low, uint32_t lo_g, const uint32_t* __restrict__ tw) {
   // performs stages t = g0 + kk for kk in [kk_lo, kk_hi), ascending (DIT) or descending (DIF)
@@ -110,25 +117,36 @@ __device__ __forceinline__ void r16_window(uint32_t (&x)[16], int g0, int kk_lo,
   for (int q = 0; q < 4; q++) {
     const int kk = DIF ? 3 - q : q;
     if (kk < kk_lo || kk >= kk_hi) continue;
-    const int t = g0 + kk;
-    const uint32_t wb = tw[(1u << (s0 + t)) + (m_low << s0) + lo_g];
     uint32_t tws[8];
+    if (CONST_TW) {
 #pragma unroll
-    for (int l = 0; l < 8; l++)
-      if (l < (1 << kk)) tws[l] = l == 0 ? wb : mmul(wb, DIF ? SMALL.f[(1 << kk) + l] : SMALL.i[(1 << kk) + l]);
+      for (int l = 0; l < 8; l++)
+        if (l < (1 << kk)) tws[l] = DIF ? SMALL.f[(1 << kk) + l] : SMALL.i[(1 << kk) + l];
+    } else {
+      const int t = g0 + kk;
+      const uint32_t wb = tw[(1u << (s0 + t)) + (m_low << s0) + lo_g];
+#pragma unroll
+      for (int l = 0; l < 8; l++)
+        if (l < (1 << kk))
+          tws[l] = l == 0 ? wb : mmul(wb, DIF ? SMALL.f[(1 << kk) + l] : SMALL.i[(1 << kk) + l]);
+    }
 #pragma unroll
     for (int i = 0; i < 16; i++) {
       if (i & (1 << kk)) continue;
       const int j = i | (1 << kk);
-      const uint32_t w = tws[i & ((1 << kk) - 1)];
+      const int l = i & ((1 << kk) - 1);
+      const bool unit = CONST_TW && l == 0;  // twiddle known to be 1
+      const uint32_t w = tws[l];
       const uint32_t u = x[i], v = x[j];
       if (DIF) {
         x[i] = madd(u, v);
-        x[j] = mmul(msub(u, v), w);
+        x[j] = unit ? msub(u, v) : mmul(u - v + P, w);
       } else {
-        const uint32_t vw = mmul(v, w);
-        x[i] = madd(u, vw);
-        x[j] = msub(u, vw);
+        const uint32_t vw = unit ? umin(v, v - P) : mmul(v, w);
+        const bool lazy = kk < 3 && ((i >> (kk + 1)) & 1);
+        const uint32_t s_ = u + vw, d = u - vw;
+        x[i] = lazy ? s_ : umin(s_, s_ - P);
+        x[j] = lazy ? d + P : umin(d, d + P);
       }
     }
   }
@@ -186,7 +204,10 @@ __global__ __launch_bounds__(1024) void k_ntt_r16(const uint32_t* __restrict__ s
       kk_hi = 4;
       done_lo = g0 + 4;
     }
-    r16_window<DIF>(x, g0, kk_lo, kk_hi, s0, m_low, lo_g, tw);
+    if (s0 == 0 && g0 == 0)
+      r16_window<DIF, true>(x, g0, kk_lo, kk_hi, s0, m_low, lo_g, tw);
+    else
+      r16_window<DIF, false>(x, g0, kk_lo, kk_hi, s0, m_low, lo_g, tw);
     if (w == nwin - 1 && !stage) {
 #pragma unroll
       for (int i = 0; i < 16; i++) D[(uint32_t)((m_base | ((uint32_t)i << g0)) << s0) + lo] = x[i];

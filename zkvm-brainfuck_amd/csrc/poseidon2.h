@@ -52,7 +52,39 @@ constexpr P2Tables make_p2_tables() {
 
 constexpr P2Tables P2 = make_p2_tables();
 
-KB_HD uint32_t cube(uint32_t x) { return mmul(mmul(x, x), x); }
+// x^3: the square is left unreduced as a signed value in (-p, p/2) and fed to a signed
+// Montgomery product (v_mad_i64_i32 / v_mul_hi_i32), whose result lies in (-p, p):
+// one correction instead of two.
+KB_HD uint32_t cube(uint32_t x) {
+  const uint64_t t = (uint64_t)x * x;
+  const uint32_t m = (uint32_t)t * MU;
+  const int32_t x2 = (int32_t)(opaque((uint32_t)(t >> 32)) - (uint32_t)(((uint64_t)m * P) >> 32));
+  const int64_t u = (int64_t)x2 * (int64_t)(int32_t)x;  // |u| < p^2 (x < p < 2^31)
+  const uint32_t m2 = (uint32_t)u * MU;
+  const int32_t mh = (int32_t)(((int64_t)(int32_t)m2 * (int64_t)P) >> 32);
+  const uint32_t r = (uint32_t)((int32_t)(u >> 32) - mh);  // (-p, p)
+  return umin(r, r + P);
+}
+
+// Sum of 16 reduced values.  Pair sums are < 2p and fit 32 bits; the 8 pairs accumulate
+// exactly in 64 bits with v_mad_u64_u32 (x * 1 + acc: one half-rate op, where a reduced
+// modular add costs add + sub + min), then one reduction: 2^32 = 2^25 - 2 (mod p).
+KB_HD uint32_t sum16(const uint32_t s[16]) {
+#ifdef __HIP_DEVICE_COMPILE__
+  uint32_t one;  // opaque 1 keeps the multiply-add form (an add_co/addc pair costs more)
+  asm("s_mov_b32 %0, 1" : "=s"(one));
+#else
+  const uint32_t one = 1;
+#endif
+  uint64_t acc = (uint64_t)(s[0] + s[1]);
+#pragma unroll
+  for (int k = 1; k < 8; k++) acc = (uint64_t)(s[2 * k] + s[2 * k + 1]) * one + acc;
+  constexpr uint32_t C = (1u << 25) - 2;  // < 16p < 2^35, so hi < 8
+  const uint64_t t = (uint64_t)(uint32_t)(acc >> 32) * C + (uint32_t)acc;  // < 2^32 + 2^28
+  const uint32_t hi2 = (uint32_t)(t >> 32);                                // 0 or 1
+  const uint32_t r = (uint32_t)t + ((0u - hi2) & C);                       // any u32 < 2.02p
+  return umin(r, umin(r - P, r - 2 * P));
+}
 
 KB_HD void mds_light(uint32_t s[16]) {
 #pragma unroll
@@ -83,11 +115,7 @@ KB_HD void poseidon2_permute(uint32_t s[16]) {
 #pragma unroll
   for (int r = 0; r < 13; r++) {
     s[0] = cube(madd(s[0], P2.internal[r]));
-    uint32_t a0 = madd(madd(s[0], s[1]), madd(s[2], s[3]));
-    uint32_t a1 = madd(madd(s[4], s[5]), madd(s[6], s[7]));
-    uint32_t a2 = madd(madd(s[8], s[9]), madd(s[10], s[11]));
-    uint32_t a3 = madd(madd(s[12], s[13]), madd(s[14], s[15]));
-    uint32_t sum = madd(madd(a0, a1), madd(a2, a3));
+    const uint32_t sum = sum16(s);
     // s_i <- sum + d_i s_i with d = [-2,1,2,1/2,3,4,-1/2,-3,-4,1/2^8,1/8,1/2^24,-1/2^8,-1/8,
     // -1/16,-1/2^24].  Small integers use doublings; the fractions are one Montgomery
     // multiply by |d_i| (cheaper on gfx950 than shifting: v_lshlrev/v_min are half rate,
