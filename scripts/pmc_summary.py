@@ -1,7 +1,9 @@
 """Summarize rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes per kernel.
 
-For k_ntt_r16 (the bench roofline kernel) it reports, per launch, the algorithmic bytes
-(8 B per element; a launch covers Grid_Size * 16 elements) next to the counted traffic.
+For the NTT kernels (the bench roofline kernels) it reports, per launch, the algorithmic
+bytes next to the counted traffic: k_ntt_r16 8 B per element (one read + one write),
+k_lde_mid 12 B per input element (read n, write the 2n LDE); a launch covers Grid_Size * 16
+input elements.
 MI355X_MICROARCH.md: FETCH_SIZE under-reports wide coalesced reads by exactly 2x on gfx950;
 both the raw and the x2-corrected fetch figures are written.  Counter units are kB.
 """
@@ -43,9 +45,10 @@ def main(root):
         e = {"launches": n,
              "fetch_kB": round(f["value"] / f["launches"], 1) if f else None,
              "write_kB": round(w["value"] / w["launches"], 1) if w else None}
-        if "k_ntt_r16" in k and f and w:
+        per_elem = 8 if "k_ntt_r16" in k else 12 if "k_lde_mid" in k else 0
+        if per_elem and f and w:  # NTT kernels: a launch covers Grid_Size * 16 input elements
             elems = f["grid"] / f["launches"] * 16
-            e["algorithmic_kB"] = round(8 * elems / 1024, 1)
+            e["algorithmic_kB"] = round(per_elem * elems / 1024, 1)
             e["traffic_kB_fetch_x2_plus_write"] = round(2 * e["fetch_kB"] + e["write_kB"], 1)
             e["traffic_kB_raw"] = round(e["fetch_kB"] + e["write_kB"], 1)
         out["kernels"][k] = e

@@ -8,9 +8,13 @@ namespace bfz {
 
 struct RedCol {            // one committed column at a given LDE height
   const uint32_t* col;     // device column (bit-reversed rows)
-  kb::EF ca, cb;           // alpha-power coefficients for the two opening points
-  int has_b;
-  int pad[3];
+  kb::EF ca;               // alpha-power coefficient at the first opening point
+};
+struct RedMat {            // the columns [first, first + count) of one matrix
+  int first, count;
+  int has_b;               // opened at the second point too: coefficient there = kb * ca
+  int pad;
+  kb::EF kb;               // alpha^width
 };
 
 struct GrindState {        // DuplexChallenger state at grind time
@@ -24,8 +28,9 @@ void inv_denoms(const kb::EF& z, int logH, kb::EF* out, hipStream_t st);
 // out_dev[c] = value at z of column c of a committed LDE (height = 2n), via the low coset.
 void open_matrix(const uint32_t* mat, size_t height, int w, const kb::EF* invd,
                  const kb::EF& scale, kb::EF* out_dev, hipStream_t st);
-// ro[t] += (sum_c ca_c v_c[t] - ya) invd_a[t] + (sum_c cb_c v_c[t] - yb) invd_b[t]
-void reduce_height(const std::vector<RedCol>& cols, size_t H, const kb::EF* invd_a,
+// ro[t] += (sum_c ca_c v_c[t] - ya) invd_a[t] + (sum_m kb_m sum_(c in m) ca_c v_c[t] - yb) invd_b[t]
+void reduce_height(const std::vector<RedCol>& cols, const std::vector<RedMat>& mats, size_t H,
+                   const kb::EF* invd_a,
                    const kb::EF* invd_b, const kb::EF& ya, const kb::EF& yb, bool has_b,
                    kb::EF* ro, hipStream_t st);
 void fri_fold(const kb::EF* in, kb::EF* out, size_t h, const kb::EF& beta, const kb::EF* add,

@@ -53,6 +53,38 @@ __global__ __launch_bounds__(256) void k_inv_denoms(EF z, int logH, const uint32
   }
 }
 
+// Lazy dot products: raw 64-bit products of Montgomery values (each < p^2) accumulate with
+// v_mad_u64_u32, four at a time (4 p^2 < 2^64 and its high word < 2p, mreduce's domain),
+// so a column costs four multiply-adds instead of an EF x base Montgomery product + EF add.
+struct LazyEF {
+  uint64_t acc[4];
+  EF sum;
+  int pending;
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int e = 0; e < 4; e++) acc[e] = 0;
+    sum = ef_zero();
+    pending = 0;
+  }
+  __device__ __forceinline__ void flush() {
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      sum.c[e] = madd(sum.c[e], mreduce(acc[e]));
+      acc[e] = 0;
+    }
+    pending = 0;
+  }
+  __device__ __forceinline__ void add(const EF& coef, uint32_t v) {
+#pragma unroll
+    for (int e = 0; e < 4; e++) acc[e] += (uint64_t)coef.c[e] * v;
+    if (++pending == 4) flush();
+  }
+  __device__ __forceinline__ EF get() {
+    flush();
+    return sum;
+  }
+};
+
 // ------------------------------------------------------------------ openings
 constexpr int OPEN_T = 256, OPEN_R = 4, OPEN_CH = OPEN_T * OPEN_R;
 
@@ -90,11 +122,11 @@ __global__ __launch_bounds__(OPEN_T) void k_open_partial(const uint32_t* __restr
     const int cw = min(64, w - cb);
     for (int c = 0; c < cw; c++) {
       const uint32_t* col = mat + (size_t)(cb + c) * height;
-      EF acc = ef_zero();
+      LazyEF lz;  // OPEN_R = 4 products per component: one reduction per column
+      lz.init();
 #pragma unroll
-      for (int r = 0; r < OPEN_R; r++)
-        if (rows[r] < n) acc = ef_add(acc, ef_mul_base(W[r], col[rows[r]]));
-      acc = wave_sum(acc);
+      for (int r = 0; r < OPEN_R; r++) lz.add(W[r], rows[r] < n ? col[rows[r]] : 0u);
+      EF acc = wave_sum(lz.get());
       if (lane == 0) sh[wave][c] = acc;
     }
     __syncthreads();
@@ -126,18 +158,22 @@ __global__ __launch_bounds__(256) void k_open_final(const EF* __restrict__ parti
 }
 
 // ------------------------------------------------------------------ reduced openings
-__global__ __launch_bounds__(256) void k_reduce(const RedCol* __restrict__ cols, int ncols,
+__global__ __launch_bounds__(256) void k_reduce(const RedCol* __restrict__ cols,
+                                                const RedMat* __restrict__ mats, int nmats,
                                                 size_t H, const EF* __restrict__ invd_a,
                                                 const EF* __restrict__ invd_b, EF ya, EF yb,
                                                 int has_b, EF* __restrict__ ro) {
   for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < H;
        t += (size_t)gridDim.x * blockDim.x) {
     EF sa = ef_zero(), sb = ef_zero();
-    for (int c = 0; c < ncols; c++) {
-      const RedCol rc = cols[c];
-      const uint32_t v = rc.col[t];
-      sa = ef_add(sa, ef_mul_base(rc.ca, v));
-      if (rc.has_b) sb = ef_add(sb, ef_mul_base(rc.cb, v));
+    for (int m = 0; m < nmats; m++) {
+      const RedMat rm = mats[m];
+      LazyEF acc;
+      acc.init();
+      for (int c = rm.first; c < rm.first + rm.count; c++) acc.add(cols[c].ca, cols[c].col[t]);
+      const EF s = acc.get();
+      sa = ef_add(sa, s);
+      if (rm.has_b) sb = ef_add(sb, ef_mul(s, rm.kb));
     }
     EF r = ef_mul(ef_sub(sa, ya), invd_a[t]);
     if (has_b) r = ef_add(r, ef_mul(ef_sub(sb, yb), invd_b[t]));
@@ -215,14 +251,19 @@ void open_matrix(const uint32_t* mat, size_t height, int w, const EF* invd, cons
   KCHECK();
 }
 
-void reduce_height(const std::vector<RedCol>& cols, size_t H, const EF* invd_a, const EF* invd_b,
-                   const EF& ya, const EF& yb, bool has_b, EF* ro, hipStream_t st) {
+void reduce_height(const std::vector<RedCol>& cols, const std::vector<RedMat>& mats, size_t H,
+                   const EF* invd_a, const EF* invd_b, const EF& ya, const EF& yb, bool has_b,
+                   EF* ro, hipStream_t st) {
   DBuf<RedCol> d(cols.size());
+  DBuf<RedMat> dm(mats.size());
   HIP_CHECK(hipMemcpyAsync(d.p, cols.data(), cols.size() * sizeof(RedCol), hipMemcpyHostToDevice, st));
-  HIP_CHECK(hipStreamSynchronize(st));  // host vector may go away
+  HIP_CHECK(hipMemcpyAsync(dm.p, mats.data(), mats.size() * sizeof(RedMat), hipMemcpyHostToDevice,
+                           st));
+  HIP_CHECK(hipStreamSynchronize(st));  // host vectors may go away
   const unsigned grid = std::min<unsigned>(ceil_div(H, 256), 8192);
-  hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(256), 0, st, (const RedCol*)d.p, (int)cols.size(), H,
-                     invd_a, invd_b, ya, yb, has_b ? 1 : 0, ro);
+  hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(256), 0, st, (const RedCol*)d.p,
+                     (const RedMat*)dm.p, (int)mats.size(), H, invd_a, invd_b, ya, yb,
+                     has_b ? 1 : 0, ro);
   KCHECK();
 }
 

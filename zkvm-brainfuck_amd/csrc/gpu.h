@@ -176,6 +176,6 @@ struct KernelProbe {
     launches = 0;
   }
 };
-KernelProbe& ntt_probe();  // k_ntt_r16 passes: 8 B per element (one read + one write)
+KernelProbe& ntt_probe();  // NTT kernels: k_ntt_r16 (8 B/element), k_lde_mid (12 B/input element)
 
 }  // namespace bfz

@@ -225,6 +225,104 @@ __global__ __launch_bounds__(1024) void k_ntt_r16(const uint32_t* __restrict__ s
   }
 }
 
+// Fused middle of a two-pass coset LDE (L > 14).  One tile = 2^b points at stride 2^s0 x 2^c
+// adjacent groups, as the second k_ntt_r16 pass:
+//   iDFT stages [s0, s0+b) (DIT)  ->  coefficients c_k in registers
+//   lo_k = c_k s^k / n, hi_k = c_k t^k / n  (t = s w_2n)
+//   DFT stages [s0+b-1 .. s0] (DIF) of each half  ->  lde[col][0..n) and lde[col][n..2n)
+// The DIT's last window and the DIF's first window hold the same 16 elements per thread, so
+// the coefficients never leave registers.  A thread's coefficient indices step by
+// D = 2^(s0+b-4): its powers are one table lookup times the launch constants (s^D)^i, (t^D)^i.
+struct MidPowers {
+  uint32_t lo[16], hi[16];
+};
+
+__global__ __launch_bounds__(1024) void k_lde_mid(const uint32_t* __restrict__ src,
+                                                  size_t src_stride, uint32_t* __restrict__ lde,
+                                                  size_t n, int s0, int b, int c,
+                                                  const uint32_t* __restrict__ tw_inv,
+                                                  const uint32_t* __restrict__ tw_fwd,
+                                                  const uint32_t* __restrict__ pw, int B,
+                                                  MidPowers mp) {
+  extern __shared__ uint32_t lds[];
+  const int tid = threadIdx.x;
+  const int nlo_log = s0 - c;
+  const size_t lo_blk = blockIdx.x & ((1u << nlo_log) - 1);
+  const size_t hi = (size_t)blockIdx.x >> nlo_log;
+  const size_t base = (hi << (s0 + b)) + (lo_blk << c);
+  const uint32_t* S = src + (size_t)blockIdx.y * src_stride + base;
+  uint32_t* D = lde + (size_t)blockIdx.y * 2 * n + base;
+  const int lo = tid & ((1 << c) - 1);
+  const uint32_t lo_g = (uint32_t)(lo_blk << c) + lo;
+  const int rest = tid >> c;
+  const int nwin = (b + 3) >> 2;
+  uint32_t x[16];
+  int done_lo = 0;
+  for (int w = 0; w < nwin; w++) {  // iDFT
+    const int g0 = min(4 * w, b - 4);
+    const uint32_t m_low = rest & ((1 << g0) - 1);
+    const uint32_t m_base = m_low | ((uint32_t)(rest >> g0) << (g0 + 4));
+    if (w == 0) {
+#pragma unroll
+      for (int i = 0; i < 16; i++) x[i] = S[(uint32_t)((m_base | ((uint32_t)i << g0)) << s0) + lo];
+    } else {
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 16; i++)
+        x[i] = lds[lds_pad((int)(((m_base | ((uint32_t)i << g0)) << c) | lo), c)];
+    }
+    const int kk_lo = max(0, done_lo - g0);
+    done_lo = g0 + 4;
+    r16_window<false, false>(x, g0, kk_lo, 4, s0, m_low, lo_g, tw_inv);
+    if (w < nwin - 1) {
+#pragma unroll
+      for (int i = 0; i < 16; i++)
+        lds[lds_pad((int)(((m_base | ((uint32_t)i << g0)) << c) | lo), c)] = x[i];
+    }
+  }
+  uint32_t coef[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) coef[i] = x[i];
+  {
+    const int g0 = b - 4;
+    const uint32_t m_base = (rest & ((1 << g0) - 1)) | ((uint32_t)(rest >> g0) << (g0 + 4));
+    const size_t k0 = base + ((size_t)m_base << s0) + lo;
+    const size_t mask = ((size_t)1 << B) - 1, nb = mask + 1;
+    const uint32_t S0 = mmul(pw[k0 & mask], pw[nb + (k0 >> B)]);
+    const uint32_t T0 = mmul(pw[2 * nb + (k0 & mask)], pw[3 * nb + (k0 >> B)]);
+    for (int half = 0; half < 2; half++) {
+      const uint32_t P0 = half ? T0 : S0;
+#pragma unroll
+      for (int i = 0; i < 16; i++) x[i] = mmul(coef[i], mmul(P0, half ? mp.hi[i] : mp.lo[i]));
+      if (half && nwin > 1) __syncthreads();  // the lo half's last LDS reads are done
+      uint32_t* Dh = D + (size_t)half * n;
+      int done_hi = b;
+      for (int w = 0; w < nwin; w++) {  // DFT of this half
+        const int gg = max(b - 4 - 4 * w, 0);
+        const uint32_t m_low = rest & ((1 << gg) - 1);
+        const uint32_t mb = m_low | ((uint32_t)(rest >> gg) << (gg + 4));
+        if (w > 0) {
+          __syncthreads();
+#pragma unroll
+          for (int i = 0; i < 16; i++)
+            x[i] = lds[lds_pad((int)(((mb | ((uint32_t)i << gg)) << c) | lo), c)];
+        }
+        const int kk_hi = min(4, done_hi - gg);
+        done_hi = gg;
+        r16_window<true, false>(x, gg, 0, kk_hi, s0, m_low, lo_g, tw_fwd);
+        if (w == nwin - 1) {
+#pragma unroll
+          for (int i = 0; i < 16; i++) Dh[(uint32_t)((mb | ((uint32_t)i << gg)) << s0) + lo] = x[i];
+        } else {
+#pragma unroll
+          for (int i = 0; i < 16; i++)
+            lds[lds_pad((int)(((mb | ((uint32_t)i << gg)) << c) | lo), c)] = x[i];
+        }
+      }
+    }
+  }
+}
+
 // lo_k = c_k * s^k / n ; hi_k = c_k * t^k / n  with s^k = SL[k & m] * SH[k >> B] (1/n in SH)
 __global__ __launch_bounds__(256) void k_scale_split(const uint32_t* __restrict__ coef,
                                                      uint32_t* __restrict__ lde, size_t n, int B,
@@ -314,7 +412,27 @@ static void r16_attrs() {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_r16<false>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lde_mid),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   done = true;
+}
+
+static void r16_launch(const R16Pass& p, const uint32_t* in, size_t is, uint32_t* dst, size_t ds,
+                       int ncols, int L, bool dif, hipStream_t st) {
+  Twiddles& T = twiddles();
+  const int threads = 1 << (p.b + p.c - 4);
+  const size_t lds = ((size_t)1 << (p.b + p.c)) + ((size_t)1 << (p.b + p.c - 4));
+  dim3 grid(1u << (L - p.b - p.c), ncols);
+  KernelProbe& probe = ntt_probe();
+  hipEvent_t ev0 = probe.on ? probe.begin(st) : nullptr;
+  if (dif)
+    hipLaunchKernelGGL(k_ntt_r16<true>, grid, dim3(threads), lds * 4, st, in, dst, is, ds, p.s0,
+                       p.b, p.c, (const uint32_t*)T.fwd.p);
+  else
+    hipLaunchKernelGGL(k_ntt_r16<false>, grid, dim3(threads), lds * 4, st, in, dst, is, ds, p.s0,
+                       p.b, p.c, (const uint32_t*)T.inv.p);
+  KCHECK();
+  if (probe.on) probe.end(ev0, st, 8.0 * (double)((size_t)1 << L) * ncols);
 }
 
 void ntt_passes(const uint32_t* src, uint32_t* dst, size_t src_stride, size_t dst_stride, int ncols,
@@ -327,21 +445,8 @@ void ntt_passes(const uint32_t* src, uint32_t* dst, size_t src_stride, size_t ds
     if (dif) std::reverse(plan.begin(), plan.end());
     bool first = true;
     for (const R16Pass& p : plan) {
-      const int threads = 1 << (p.b + p.c - 4);
-      const size_t lds = ((size_t)1 << (p.b + p.c)) + ((size_t)1 << (p.b + p.c - 4));
-      dim3 grid(1u << (L - p.b - p.c), ncols);
-      const uint32_t* in = first ? src : dst;
-      const size_t is = first ? src_stride : dst_stride;
-      KernelProbe& probe = ntt_probe();
-      hipEvent_t ev0 = probe.on ? probe.begin(st) : nullptr;
-      if (dif)
-        hipLaunchKernelGGL(k_ntt_r16<true>, grid, dim3(threads), lds * 4, st, in, dst, is,
-                           dst_stride, p.s0, p.b, p.c, (const uint32_t*)T.fwd.p);
-      else
-        hipLaunchKernelGGL(k_ntt_r16<false>, grid, dim3(threads), lds * 4, st, in, dst, is,
-                           dst_stride, p.s0, p.b, p.c, (const uint32_t*)T.inv.p);
-      KCHECK();
-      if (probe.on) probe.end(ev0, st, 8.0 * (double)((size_t)1 << L) * ncols);
+      r16_launch(p, first ? src : dst, first ? src_stride : dst_stride, dst, dst_stride, ncols, L,
+                 dif, st);
       first = false;
     }
     return;
@@ -409,6 +514,39 @@ const uint32_t* scale_tables(uint32_t shift, int L, int B) {
 void coset_lde(const uint32_t* evals, size_t n, int w, uint32_t shift, uint32_t* lde,
                hipStream_t st) {
   const int L = log2i(n);
+  if (L > R16_TILE_LOG) {  // iDFT pass 1 -> fused middle -> DFT last pass (3 HBM passes)
+    Twiddles& T = twiddles();
+    T.ensure(L);
+    r16_attrs();
+    const auto plan = r16_plan(L);  // {(0, b1, 0), (b1, b2, c2)}
+    const R16Pass& p1 = plan[0];
+    const R16Pass& p2 = plan[1];
+    DBuf<uint32_t> coef(n * (size_t)w);
+    r16_launch(p1, evals, n, coef.p, n, w, L, false, st);
+    const int B = (L + 1) / 2;
+    const uint32_t* pw = scale_tables(shift, L, B);
+    MidPowers mp;
+    const uint64_t D = (uint64_t)1 << (p2.s0 + p2.b - 4);
+    const uint32_t gs = mpow(shift, D), gt = mpow(mmul(shift, two_adic_gen(L + 1)), D);
+    uint32_t a = ONE, c = ONE;
+    for (int i = 0; i < 16; i++) {
+      mp.lo[i] = a;
+      mp.hi[i] = c;
+      a = mmul(a, gs);
+      c = mmul(c, gt);
+    }
+    const int threads = 1 << (p2.b + p2.c - 4);
+    const size_t ldsz = ((size_t)1 << (p2.b + p2.c)) + ((size_t)1 << (p2.b + p2.c - 4));
+    KernelProbe& probe = ntt_probe();
+    hipEvent_t ev0 = probe.on ? probe.begin(st) : nullptr;
+    hipLaunchKernelGGL(k_lde_mid, dim3(1u << (L - p2.b - p2.c), w), dim3(threads), ldsz * 4, st,
+                       (const uint32_t*)coef.p, n, lde, n, p2.s0, p2.b, p2.c,
+                       (const uint32_t*)T.inv.p, (const uint32_t*)T.fwd.p, pw, B, mp);
+    KCHECK();
+    if (probe.on) probe.end(ev0, st, 12.0 * (double)n * w);  // read n, write 2n
+    r16_launch(p1, lde, n, lde, n, 2 * w, L, true, st);
+    return;
+  }
   DBuf<uint32_t> coef(n * (size_t)w);
   ntt_passes(evals, coef.p, n, n, w, L, /*dif=*/false, st);
   const int B = (L + 1) / 2;

@@ -424,6 +424,7 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
   std::map<int, DBuf<EF>> ro;
   for (int lh = Lmax; lh >= 1; lh--) {
     std::vector<RedCol> cols;
+    std::vector<RedMat> rmats;
     EF ya = ef_zero(), yb = ef_zero();
     size_t num_red = 0;
     bool has_b = false;
@@ -436,9 +437,13 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
         for (int c = 0; c < w; c++) {
           RedCol rc{};
           rc.col = m.lde.buf.p + (size_t)c * m.lde.height;
-          rc.has_b = 0;
           cols.push_back(rc);
         }
+        RedMat rm{};
+        rm.first = (int)base;
+        rm.count = w;
+        // point j's coefficients are alpha^(num_red + k): those of the second point are the
+        // first point's times alpha^w (they follow it directly in the reduction order)
         for (int j = 0; j < mp[r][i].npts; j++) {
           EF a = ef_pow(fri_alpha, num_red);
           num_red += w;
@@ -448,19 +453,22 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
               cols[base + c].ca = a;
               ya = ef_add(ya, ef_mul(a, y));
             } else {
-              cols[base + c].cb = a;
-              cols[base + c].has_b = 1;
               yb = ef_add(yb, ef_mul(a, y));
               has_b = true;
             }
             a = ef_mul(a, fri_alpha);
           }
         }
+        if (mp[r][i].npts == 2) {
+          rm.has_b = 1;
+          rm.kb = ef_pow(fri_alpha, (uint64_t)w);
+        }
+        rmats.push_back(rm);
       }
     if (cols.empty()) continue;
     DBuf<EF> r((size_t)1 << lh);
     HIP_CHECK(hipMemsetAsync(r.p, 0, ((size_t)1 << lh) * sizeof(EF), st));
-    reduce_height(cols, (size_t)1 << lh, invd_zeta.p, has_b ? invd_next.at(lh).p : nullptr, ya, yb,
+    reduce_height(cols, rmats, (size_t)1 << lh, invd_zeta.p, has_b ? invd_next.at(lh).p : nullptr, ya, yb,
                   has_b, r.p, st);
     ro.emplace(lh, std::move(r));
   }
