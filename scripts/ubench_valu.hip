@@ -27,6 +27,10 @@ constexpr int ITERS = 2048;
 KERNEL(k_add, "v_add_u32 %0, %0, %1")
 KERNEL(k_add_e64, "v_add_u32_e64 %0, %0, %1")
 KERNEL(k_sub, "v_sub_u32 %0, %0, %1")
+KERNEL(k_add_lit, "v_add_u32 %0, 0x80ffffff, %0")
+KERNEL(k_add_sgpr, "v_add_u32 %0, s4, %0")
+KERNEL(k_min_lit, "v_min_u32 %0, 0x7f000001, %0")
+KERNEL(k_mul_hi_sgpr, "v_mul_hi_u32 %0, %0, s4")
 KERNEL(k_add_co, "v_add_co_u32 %0, vcc, %0, %1")
 KERNEL(k_addc, "v_addc_co_u32 %0, vcc, %0, %1, vcc")
 KERNEL(k_min, "v_min_u32 %0, %0, %1")
@@ -74,6 +78,10 @@ int main() {
       {"v_add_u32", k_add},
       {"v_add_u32_e64", k_add_e64},
       {"v_sub_u32", k_sub},
+      {"v_add_u32 literal", k_add_lit},
+      {"v_add_u32 sgpr", k_add_sgpr},
+      {"v_min_u32 literal", k_min_lit},
+      {"v_mul_hi sgpr", k_mul_hi_sgpr},
       {"v_add_co_u32", k_add_co},
       {"v_addc_co_u32", k_addc},
       {"v_min_u32", k_min},

@@ -104,45 +104,63 @@ KB_HD void mds_light(uint32_t s[16]) {
   for (int i = 0; i < 16; i++) s[i] = madd(s[i], sums[i & 3]);
 }
 
-KB_HD void poseidon2_permute(uint32_t s[16]) {
-  mds_light(s);
+// N independent permutations advanced round by round, so the scheduler can interleave their
+// dependency chains (the internal rounds are one serial chain per state).
+template <int N>
+KB_HD void poseidon2_permute_n(uint32_t (&s)[N][16]) {
+#pragma unroll
+  for (int k = 0; k < N; k++) mds_light(s[k]);
 #pragma unroll
   for (int r = 0; r < 4; r++) {
 #pragma unroll
-    for (int i = 0; i < 16; i++) s[i] = cube(madd(s[i], P2.ext_init[r][i]));
-    mds_light(s);
+    for (int k = 0; k < N; k++) {
+#pragma unroll
+      for (int i = 0; i < 16; i++) s[k][i] = cube(madd(s[k][i], P2.ext_init[r][i]));
+      mds_light(s[k]);
+    }
   }
 #pragma unroll
   for (int r = 0; r < 13; r++) {
-    s[0] = cube(madd(s[0], P2.internal[r]));
-    const uint32_t sum = sum16(s);
-    // s_i <- sum + d_i s_i with d = [-2,1,2,1/2,3,4,-1/2,-3,-4,1/2^8,1/8,1/2^24,-1/2^8,-1/8,
-    // -1/16,-1/2^24].  Small integers use doublings; the fractions are one Montgomery
-    // multiply by |d_i| (cheaper on gfx950 than shifting: v_lshlrev/v_min are half rate,
-    // scripts/ubench_valu.hip), the sign folds into add/sub.
-    s[0] = msub(sum, mdbl(s[0]));
-    s[1] = madd(sum, s[1]);
-    s[2] = madd(sum, mdbl(s[2]));
-    s[3] = madd(sum, mmul(s[3], P2.dabs[3]));
-    s[4] = madd(sum, madd(mdbl(s[4]), s[4]));
-    s[5] = madd(sum, mdbl(mdbl(s[5])));
-    s[6] = msub(sum, mmul(s[6], P2.dabs[6]));
-    s[7] = msub(sum, madd(mdbl(s[7]), s[7]));
-    s[8] = msub(sum, mdbl(mdbl(s[8])));
-    s[9] = madd(sum, mmul(s[9], P2.dabs[9]));
-    s[10] = madd(sum, mmul(s[10], P2.dabs[10]));
-    s[11] = madd(sum, mmul(s[11], P2.dabs[11]));
-    s[12] = msub(sum, mmul(s[12], P2.dabs[12]));
-    s[13] = msub(sum, mmul(s[13], P2.dabs[13]));
-    s[14] = msub(sum, mmul(s[14], P2.dabs[14]));
-    s[15] = msub(sum, mmul(s[15], P2.dabs[15]));
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+      uint32_t* t = s[k];
+      t[0] = cube(madd(t[0], P2.internal[r]));
+      const uint32_t sum = sum16(t);
+      // s_i <- sum + d_i s_i with d = [-2,1,2,1/2,3,4,-1/2,-3,-4,1/2^8,1/8,1/2^24,-1/2^8,-1/8,
+      // -1/16,-1/2^24].  Small integers use doublings; the fractions are one Montgomery
+      // multiply by |d_i| (cheaper on gfx950 than shifting: v_lshlrev/v_min are half rate,
+      // scripts/ubench_valu.hip), the sign folds into add/sub.
+      t[0] = msub(sum, mdbl(t[0]));
+      t[1] = madd(sum, t[1]);
+      t[2] = madd(sum, mdbl(t[2]));
+      t[3] = madd(sum, mmul(t[3], P2.dabs[3]));
+      t[4] = madd(sum, madd(mdbl(t[4]), t[4]));
+      t[5] = madd(sum, mdbl(mdbl(t[5])));
+      t[6] = msub(sum, mmul(t[6], P2.dabs[6]));
+      t[7] = msub(sum, madd(mdbl(t[7]), t[7]));
+      t[8] = msub(sum, mdbl(mdbl(t[8])));
+      t[9] = madd(sum, mmul(t[9], P2.dabs[9]));
+      t[10] = madd(sum, mmul(t[10], P2.dabs[10]));
+      t[11] = madd(sum, mmul(t[11], P2.dabs[11]));
+      t[12] = msub(sum, mmul(t[12], P2.dabs[12]));
+      t[13] = msub(sum, mmul(t[13], P2.dabs[13]));
+      t[14] = msub(sum, mmul(t[14], P2.dabs[14]));
+      t[15] = msub(sum, mmul(t[15], P2.dabs[15]));
+    }
   }
 #pragma unroll
   for (int r = 0; r < 4; r++) {
 #pragma unroll
-    for (int i = 0; i < 16; i++) s[i] = cube(madd(s[i], P2.ext_term[r][i]));
-    mds_light(s);
+    for (int k = 0; k < N; k++) {
+#pragma unroll
+      for (int i = 0; i < 16; i++) s[k][i] = cube(madd(s[k][i], P2.ext_term[r][i]));
+      mds_light(s[k]);
+    }
   }
+}
+
+KB_HD void poseidon2_permute(uint32_t s[16]) {
+  poseidon2_permute_n<1>(*reinterpret_cast<uint32_t(*)[1][16]>(s));
 }
 
 }  // namespace kb
