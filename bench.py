@@ -4,9 +4,10 @@
 Workload (BASELINE.json metric "core-proof wall-time (ms) + NTT HBM GB/s, fibonacci trace
 2^22 rows"): the FIBO_X4 guest (the reference fibonacci guest run 4x, stdin [255]) executes
 3,767,729 cycles -> Cpu 2^22 x 31, MemoryInstrs 2^21 x 41, AddSub 2^20 x 7, Jump 2^20 x 45 ...
-A "step" is one full core proof (main commit, LogUp, quotient, FRI open, proof assembly)
-from traces already resident in HBM; the executor and trace upload run before the timed
-region.  Every rank proves its own replica (no data-path collective: replicas only), so
+A "step" is one full core proof from the executor's events already resident in HBM:
+device trace generation (generate_dependencies + generate_traces), main commit, LogUp,
+quotient, FRI open and proof assembly.  The executor and the event upload run before the
+timed region.  Every rank proves its own replica (no data-path collective: replicas only), so
 the job is weak-scaled; `value` is the wall time of one step (max over ranks).
 
 Also reported: roofline of the coset-LDE (NTT) kernels, measured live with HIP events on

@@ -42,7 +42,7 @@ typedef struct bfz_pk bfz_pk;         /* device-resident proving key (DeviceProv
 typedef struct bfz_record bfz_record; /* executed record with traces resident in HBM  */
 
 typedef struct {
-  double upload_ms, main_commit_ms, perm_ms, quotient_ms, open_ms, fri_ms, total_ms;
+  double trace_ms, main_commit_ms, perm_ms, quotient_ms, open_ms, fri_ms, total_ms;
   double lde_ms, lde_bytes; /* whole coset LDEs: 12*n*w algorithmic bytes per call */
   int lde_calls;
   double ntt_kernel_ms, ntt_kernel_bytes; /* NTT pass kernel, per-launch events, 8 B/element */
@@ -66,6 +66,11 @@ int bfz_execute(const char* elf, const uint8_t* stdin_data, size_t nin, uint8_t*
 int bfz_trace(const char* elf, const uint8_t* stdin_data, size_t nin, int chip, int prep,
               uint32_t** out, size_t* height, size_t* width);
 
+/* Same trace generated on the device from the uploaded events (the prover's own path),
+ * returned row-major in natural row order for comparison. */
+int bfz_trace_device(const char* elf, const uint8_t* stdin_data, size_t nin, int chip,
+                     uint32_t** out, size_t* height, size_t* width);
+
 int bfz_setup(const char* elf, bfz_pk** pk, uint32_t vk_commit[8]);
 void bfz_pk_free(bfz_pk* pk);
 
@@ -81,7 +86,9 @@ int bfz_prove_traces(const bfz_pk* pk, const int* chips, const uint32_t* const* 
 int bfz_verify(const char* elf, const uint32_t vk_commit[8], const uint8_t* proof,
                size_t proof_len);
 
-/* Split prove: execute + generate traces + upload (untimed), then prove from HBM. */
+/* Split prove: bfz_record_new executes the program and copies its events to HBM (the
+ * proof's inputs); bfz_record_prove generates every chip trace on the device
+ * (generate_dependencies + generate_traces, prover.rs:58-81) and proves. */
 int bfz_record_new(const bfz_pk* pk, const uint8_t* stdin_data, size_t nin, bfz_record** rec,
                    uint64_t* cycles);
 int bfz_record_prove(const bfz_pk* pk, const bfz_record* rec, uint8_t** proof, size_t* proof_len,

@@ -91,6 +91,34 @@ def test_proof_bytes_match_oracle(client, name, prog, stdin):
     assert O.verify(prog, pf.proof)            # oracle verifier
 
 
+def _device_trace(prog, stdin, chip):
+    p = ctypes.POINTER(ctypes.c_uint32)()
+    h, w = ctypes.c_size_t(), ctypes.c_size_t()
+    inb = bytes(stdin)
+    buf = (ctypes.c_uint8 * max(len(inb), 1))(*inb)
+    rc = _lib.lib().bfz_trace_device(prog.encode(), buf, len(inb), chip, ctypes.byref(p),
+                                     ctypes.byref(h), ctypes.byref(w))
+    if rc == 1:
+        return None
+    _lib.check(rc)
+    arr = np.ctypeslib.as_array(p, shape=(h.value * w.value,)).copy().reshape(h.value, w.value)
+    _lib.lib().bfz_free(p)
+    return arr
+
+
+@pytest.mark.parametrize("name,prog,stdin", guests.REFERENCE_PROGRAMS +
+                         [("fibo255", guests.FIBO, [255])])
+def test_device_traces_match_oracle(name, prog, stdin):
+    """generate_dependencies + generate_traces on the device (tracegen.hip) == the oracle's
+    host traces, every chip, including the Byte/Program multiplicity histograms."""
+    for chip in range(8):
+        exp = O.trace(prog, stdin, chip)
+        got = _device_trace(prog, stdin, chip)
+        assert (got is None) == (exp is None), (name, chip)
+        if exp is not None:
+            assert np.array_equal(unmont(got), exp), (name, sdk.CHIPS[chip])
+
+
 def test_prove_from_host_traces_matches(client):
     """MachineProver boundary: traces produced on the host (generate_traces) proved through
     bfz_prove_traces give the same bytes as the record path and the oracle."""

@@ -20,7 +20,7 @@ class BfzError(RuntimeError):
 
 class Timings(ctypes.Structure):
     _fields_ = [
-        ("upload_ms", c_double), ("main_commit_ms", c_double), ("perm_ms", c_double),
+        ("trace_ms", c_double), ("main_commit_ms", c_double), ("perm_ms", c_double),
         ("quotient_ms", c_double), ("open_ms", c_double), ("fri_ms", c_double),
         ("total_ms", c_double), ("lde_ms", c_double), ("lde_bytes", c_double),
         ("lde_calls", c_int), ("ntt_kernel_ms", c_double), ("ntt_kernel_bytes", c_double),
@@ -42,6 +42,8 @@ SIGNATURES = [
                             POINTER(c_size_t), POINTER(c_uint64)]),
     ("bfz_trace", c_int, [c_char_p, POINTER(c_uint8), c_size_t, c_int, c_int,
                           POINTER(POINTER(c_uint32)), POINTER(c_size_t), POINTER(c_size_t)]),
+    ("bfz_trace_device", c_int, [c_char_p, POINTER(c_uint8), c_size_t, c_int,
+                                 POINTER(POINTER(c_uint32)), POINTER(c_size_t), POINTER(c_size_t)]),
     ("bfz_setup", c_int, [c_char_p, POINTER(c_void_p), POINTER(c_uint32)]),
     ("bfz_pk_free", None, [c_void_p]),
     ("bfz_prove", c_int, [c_void_p, POINTER(c_uint8), c_size_t, POINTER(POINTER(c_uint8)),

@@ -13,13 +13,14 @@
 #include "merkle.h"
 #include "ntt.h"
 #include "prover.h"
+#include "tracegen.h"
 #include "verifier.h"
 
 struct bfz_pk {
   std::unique_ptr<bfz::ProvingKey> pk;
 };
 struct bfz_record {
-  bfz::DeviceTraces dt;
+  bfz::DeviceEvents ev;  // executor events resident in HBM
   uint64_t cycles = 0;
 };
 
@@ -120,6 +121,38 @@ int bfz_trace(const char* elf, const uint8_t* in, size_t nin, int chip, int prep
   });
 }
 
+int bfz_trace_device(const char* elf, const uint8_t* in, size_t nin, int chip, uint32_t** out,
+                     size_t* height, size_t* width) {
+  return guarded([&] {
+    if (chip < 0 || chip >= bfz::NUM_CHIPS) throw std::runtime_error("bad chip index");
+    bfz::Program p = bfz::Program::parse(elf);
+    bfz::ExecutionRecord rec;
+    bfz::execute(p, in, nin, rec);
+    if (!bfz::chip_included(chip, rec)) return 1;
+    bfz::DeviceEvents ev;
+    bfz::upload_events(rec, ev, bfz::stream());
+    bfz::DeviceTraces dt;
+    bfz::generate_traces_device(ev, dt, bfz::stream());
+    size_t k = 0;
+    while (dt.chips[k] != chip) k++;
+    const size_t h = dt.heights[k];
+    const int w = bfz::CHIP_INFO[chip].main_w;
+    std::vector<uint32_t> cm(h * w);
+    HIP_CHECK(hipMemcpyAsync(cm.data(), dt.evals[k].p, cm.size() * 4, hipMemcpyDeviceToHost,
+                             bfz::stream()));
+    HIP_CHECK(hipStreamSynchronize(bfz::stream()));
+    uint32_t* o = (uint32_t*)std::malloc(cm.size() * 4 + 4);
+    if (!o) throw std::runtime_error("out of host memory");
+    const int logh = bfz::log2i(h);
+    for (size_t r = 0; r < h; r++)  // column-major bit-reversed -> row-major natural
+      for (int c = 0; c < w; c++) o[r * w + c] = cm[(size_t)c * h + bfz::bitrev32((uint32_t)r, logh)];
+    *out = o;
+    *height = h;
+    *width = w;
+    return 0;
+  });
+}
+
 int bfz_setup(const char* elf, bfz_pk** pk, uint32_t vk_commit[8]) {
   return guarded([&] {
     auto k = std::make_unique<bfz_pk>();
@@ -180,8 +213,7 @@ int bfz_record_new(const bfz_pk* pk, const uint8_t* in, size_t nin, bfz_record**
     auto r = std::make_unique<bfz_record>();
     bfz::ExecutionRecord er;
     bfz::execute(pk->pk->program, in, nin, er);
-    bfz::generate_dependencies(er);
-    bfz::upload_traces(er, r->dt, bfz::stream());
+    bfz::upload_events(er, r->ev, bfz::stream());
     r->cycles = er.global_clk;
     if (cycles) *cycles = er.global_clk;
     *rec = r.release();
@@ -195,9 +227,9 @@ int bfz_record_prove(const bfz_pk* pk, const bfz_record* rec, uint8_t** proof, s
     bfz::ProveOptions o = opts();
     o.timing = t != nullptr;
     bfz::StageTimes st;
-    auto v = bfz::prove_device(*pk->pk, const_cast<bfz::DeviceTraces&>(rec->dt), o, &st);
+    auto v = bfz::prove_events(*pk->pk, rec->ev, o, &st);
     if (t) {
-      t->upload_ms = st.upload;
+      t->trace_ms = st.trace;
       t->main_commit_ms = st.main_commit;
       t->perm_ms = st.perm;
       t->quotient_ms = st.quotient;

@@ -55,7 +55,7 @@ struct ProvingKey {
 };
 
 struct StageTimes {          // milliseconds, measured with HIP events on the prover stream
-  double upload = 0, main_commit = 0, perm = 0, quotient = 0, open = 0, fri = 0, total = 0;
+  double trace = 0, main_commit = 0, perm = 0, quotient = 0, open = 0, fri = 0, total = 0;
   double lde_ms = 0;         // sum over coset_lde calls
   double lde_bytes = 0;      // algorithmic bytes: 12 * n * w per call
   int lde_calls = 0;
@@ -87,7 +87,6 @@ struct DeviceTraces {
   std::vector<DBuf<uint32_t>> evals;          // column-major bit-reversed evaluations
   std::vector<size_t> heights;
 };
-void upload_traces(const ExecutionRecord& rec, DeviceTraces& dt, hipStream_t st);
 // Host main traces as MachineProver::generate_traces returns them (row-major Montgomery,
 // one per included chip); validates chip ids, widths and power-of-two heights.
 void upload_host_traces(const int* chips, const uint32_t* const* mats, const size_t* heights,

@@ -17,6 +17,7 @@
 #include "ntt.h"
 #include "poseidon2.h"
 #include "quotient.h"
+#include "tracegen.h"
 
 namespace bfz {
 
@@ -181,26 +182,6 @@ std::unique_ptr<ProvingKey> setup(const std::string& src) {
   }
   pk->prep.commit(st);
   return pk;
-}
-
-void upload_traces(const ExecutionRecord& rec, DeviceTraces& dt, hipStream_t st) {
-  dt.chips.clear();
-  dt.evals.clear();
-  dt.heights.clear();
-  for (int c = 0; c < NUM_CHIPS; c++) {
-    if (!chip_included(c, rec)) continue;
-    std::vector<uint32_t> host;
-    const size_t h = main_trace(c, rec, host);
-    const int w = CHIP_INFO[c].main_w;
-    DBuf<uint32_t> rm(h * w);
-    HIP_CHECK(hipMemcpyAsync(rm.p, host.data(), host.size() * 4, hipMemcpyHostToDevice, st));
-    DBuf<uint32_t> ev(h * w);
-    transpose_bitrev(rm.p, h, w, ev.p, st);
-    HIP_CHECK(hipStreamSynchronize(st));
-    dt.chips.push_back(c);
-    dt.evals.push_back(std::move(ev));
-    dt.heights.push_back(h);
-  }
 }
 
 void upload_host_traces(const int* chips, const uint32_t* const* mats, const size_t* heights,
@@ -634,17 +615,41 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
   return std::move(w.b);
 }
 
+std::vector<uint8_t> prove_events(const ProvingKey& pk, const DeviceEvents& ev,
+                                  const ProveOptions& opt, StageTimes* times) {
+  hipStream_t st = stream();
+  const bool timing = opt.timing && times;
+  hipEvent_t a = nullptr, b = nullptr;
+  if (timing) {
+    HIP_CHECK(hipEventCreate(&a));
+    HIP_CHECK(hipEventCreate(&b));
+    HIP_CHECK(hipEventRecord(a, st));
+  }
+  DeviceTraces dt;
+  generate_traces_device(ev, dt, st);
+  if (timing) HIP_CHECK(hipEventRecord(b, st));
+  auto proof = prove_device(pk, dt, opt, times);
+  if (timing) {
+    float ms = 0;
+    HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+    times->trace = ms;
+    times->total += ms;
+    HIP_CHECK(hipEventDestroy(a));
+    HIP_CHECK(hipEventDestroy(b));
+  }
+  return proof;
+}
+
 std::vector<uint8_t> prove(const ProvingKey& pk, const uint8_t* in, size_t nin,
                            const ProveOptions& opt, StageTimes* times,
                            std::vector<uint8_t>* output_stream, uint64_t* cycles) {
   ExecutionRecord rec;
   execute(pk.program, in, nin, rec);
-  generate_dependencies(rec);
-  DeviceTraces dt;
-  upload_traces(rec, dt, stream());
+  DeviceEvents ev;
+  upload_events(rec, ev, stream());
   if (output_stream) *output_stream = rec.output;
   if (cycles) *cycles = rec.global_clk;
-  return prove_device(pk, dt, opt, times);
+  return prove_events(pk, ev, opt, times);
 }
 
 }  // namespace bfz

@@ -1,0 +1,36 @@
+// Device trace generation: the executor's events are uploaded once
+// (compact, ~50 B per cycle) and every chip's main trace is filled on the device directly in
+// the prover's layout (column-major, bit-reversed rows), together with the byte-lookup and
+// program multiplicities of StarkMachine::generate_dependencies (machine.rs:228-248).
+#pragma once
+#include "gpu.h"
+#include "machine.h"
+#include "prover.h"
+
+namespace bfz {
+
+struct DeviceEvents {
+  DBuf<CpuEvent> cpu;
+  DBuf<AluEvent> alu;
+  DBuf<JumpEvent> jump;
+  DBuf<MemInstrEvent> meminstr;
+  DBuf<IoEvent> io;
+  DBuf<MemoryEvent> memory;
+  DBuf<Instruction> prog;
+  size_t n[NUM_CHIPS] = {};   // events per chip (Program: instructions, Byte: 0)
+  size_t height[NUM_CHIPS] = {};
+  bool included[NUM_CHIPS] = {};
+  uint64_t global_clk = 0;
+};
+
+// Host -> HBM copy of the record's events (the proof's inputs).
+void upload_events(const ExecutionRecord& rec, DeviceEvents& ev, hipStream_t st);
+
+// generate_dependencies + generate_traces on the device, into dt (replaces its contents).
+void generate_traces_device(const DeviceEvents& ev, DeviceTraces& dt, hipStream_t st);
+
+// Device trace generation + prove_device; with timing, StageTimes::trace covers the former.
+std::vector<uint8_t> prove_events(const ProvingKey& pk, const DeviceEvents& ev,
+                                  const ProveOptions& opt, StageTimes* times);
+
+}  // namespace bfz
