@@ -225,6 +225,60 @@ __global__ __launch_bounds__(1024) void k_ntt_r16(const uint32_t* __restrict__ s
   }
 }
 
+// Contiguous pass (stages 0..B-1 of 2^B-element tiles, s0 = c = 0) with B a compile-time
+// constant: the window loop unrolls, every window's g0 is a constant, and the LDS address of
+// element i is pad(m_base) + (i << g0) + ((i << g0) >> 4) (the bits [g0, g0+4) of m_base are
+// zero, so the padding never carries) -- all offsets fold into ds_read/ds_write immediates.
+template <int G0>
+__device__ __forceinline__ constexpr int tile_off(int i) { return (i << G0) + ((i << G0) >> 4); }
+
+template <bool DIF, int B>
+__global__ __launch_bounds__(1 << (B - 4)) void k_ntt_tile(const uint32_t* __restrict__ src,
+                                                           uint32_t* __restrict__ dst,
+                                                           size_t src_stride, size_t dst_stride,
+                                                           const uint32_t* __restrict__ tw) {
+  static_assert(B >= 8 && B <= R16_TILE_LOG, "tile");
+  constexpr int T = 1 << (B - 4);
+  constexpr int NW = (B + 3) / 4;
+  extern __shared__ uint32_t lds[];
+  const int tid = threadIdx.x;
+  const size_t base = (size_t)blockIdx.x << B;
+  const uint32_t* S = src + (size_t)blockIdx.y * src_stride + base;
+  uint32_t* D = dst + (size_t)blockIdx.y * dst_stride + base;
+  const int tpad = tid + (tid >> 4);
+#pragma unroll
+  for (int i = 0; i < 16; i++) lds[i * (T + T / 16) + tpad] = S[i * T + tid];
+  uint32_t x[16];
+  int done_lo = 0, done_hi = B;
+#pragma unroll
+  for (int w = 0; w < NW; w++) {
+    const int g0 = DIF ? (B - 4 - 4 * w > 0 ? B - 4 - 4 * w : 0) : (4 * w < B - 4 ? 4 * w : B - 4);
+    const uint32_t m_low = tid & ((1 << g0) - 1);
+    const uint32_t m_base = m_low | ((uint32_t)(tid >> g0) << (g0 + 4));
+    const uint32_t pb = m_base + (m_base >> 4);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 16; i++) x[i] = lds[pb + (i << g0) + ((i << g0) >> 4)];
+    int kk_lo = 0, kk_hi = 4;
+    if (DIF) {
+      kk_hi = done_hi - g0 < 4 ? done_hi - g0 : 4;
+      done_hi = g0;
+    } else {
+      kk_lo = done_lo - g0 > 0 ? done_lo - g0 : 0;
+      done_lo = g0 + 4;
+    }
+    if (g0 == 0)
+      r16_window<DIF, true>(x, g0, kk_lo, kk_hi, 0, m_low, 0, tw);
+    else
+      r16_window<DIF, false>(x, g0, kk_lo, kk_hi, 0, m_low, 0, tw);
+#pragma unroll
+    for (int i = 0; i < 16; i++) lds[pb + (i << g0) + ((i << g0) >> 4)] = x[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 16; i++) D[i * T + tid] = lds[i * (T + T / 16) + tpad];
+}
+
 // Fused middle of a two-pass coset LDE (L > 14).  One tile = 2^b points at stride 2^s0 x 2^c
 // adjacent groups, as the second k_ntt_r16 pass:
 //   iDFT stages [s0, s0+b) (DIT)  ->  coefficients c_k in registers
@@ -237,13 +291,22 @@ struct MidPowers {
   uint32_t lo[16], hi[16];
 };
 
-__global__ __launch_bounds__(1024) void k_lde_mid(const uint32_t* __restrict__ src,
-                                                  size_t src_stride, uint32_t* __restrict__ lde,
-                                                  size_t n, int s0, int b, int c,
-                                                  const uint32_t* __restrict__ tw_inv,
-                                                  const uint32_t* __restrict__ tw_fwd,
-                                                  const uint32_t* __restrict__ pw, int B,
-                                                  MidPowers mp) {
+// Plan of an L-stage transform: pass 1 = stages [0, b1) contiguous, pass 2 = [b1, L) with
+// 2^c2-element coalesced runs (see r16_plan); everything is a compile-time function of L.
+template <int L>
+struct MidPlan {
+  static constexpr int b1 = L - 4 < R16_TILE_LOG ? L - 4 : R16_TILE_LOG;
+  static constexpr int b2 = L - b1;
+  static constexpr int c2 = b1 < R16_TILE_LOG - b2 ? (b1 < 6 ? b1 : 6)
+                                                  : (R16_TILE_LOG - b2 < 6 ? R16_TILE_LOG - b2 : 6);
+};
+
+template <int L>
+__global__ __launch_bounds__(1 << (MidPlan<L>::b2 + MidPlan<L>::c2 - 4)) void k_lde_mid(
+    const uint32_t* __restrict__ src, size_t src_stride, uint32_t* __restrict__ lde, size_t n,
+    const uint32_t* __restrict__ tw_inv, const uint32_t* __restrict__ tw_fwd,
+    const uint32_t* __restrict__ pw, int B, MidPowers mp) {
+  constexpr int s0 = MidPlan<L>::b1, b = MidPlan<L>::b2, c = MidPlan<L>::c2;
   extern __shared__ uint32_t lds[];
   const int tid = threadIdx.x;
   const int nlo_log = s0 - c;
@@ -258,6 +321,7 @@ __global__ __launch_bounds__(1024) void k_lde_mid(const uint32_t* __restrict__ s
   const int nwin = (b + 3) >> 2;
   uint32_t x[16];
   int done_lo = 0;
+#pragma unroll
   for (int w = 0; w < nwin; w++) {  // iDFT
     const int g0 = min(4 * w, b - 4);
     const uint32_t m_low = rest & ((1 << g0) - 1);
@@ -297,6 +361,7 @@ __global__ __launch_bounds__(1024) void k_lde_mid(const uint32_t* __restrict__ s
       if (half && nwin > 1) __syncthreads();  // the lo half's last LDS reads are done
       uint32_t* Dh = D + (size_t)half * n;
       int done_hi = b;
+#pragma unroll
       for (int w = 0; w < nwin; w++) {  // DFT of this half
         const int gg = max(b - 4 - 4 * w, 0);
         const uint32_t m_low = rest & ((1 << gg) - 1);
@@ -412,9 +477,41 @@ static void r16_attrs() {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_r16<false>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lde_mid),
+  const void* mids[] = {(const void*)&k_lde_mid<15>, (const void*)&k_lde_mid<16>,
+                        (const void*)&k_lde_mid<17>, (const void*)&k_lde_mid<18>,
+                        (const void*)&k_lde_mid<19>, (const void*)&k_lde_mid<20>,
+                        (const void*)&k_lde_mid<21>, (const void*)&k_lde_mid<22>,
+                        (const void*)&k_lde_mid<23>};
+  for (const void* f : mids)
+    HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<true, 14>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<false, 14>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   done = true;
+}
+
+template <bool DIF, int B>
+static void tile_launch(dim3 grid, const uint32_t* in, size_t is, uint32_t* dst, size_t ds,
+                        const uint32_t* tw, hipStream_t st) {
+  const size_t lds = ((size_t)1 << B) + ((size_t)1 << (B - 4));
+  hipLaunchKernelGGL((k_ntt_tile<DIF, B>), grid, dim3(1 << (B - 4)), lds * 4, st, in, dst, is, ds,
+                     tw);
+}
+
+template <bool DIF>
+static bool tile_dispatch(int b, dim3 grid, const uint32_t* in, size_t is, uint32_t* dst,
+                          size_t ds, const uint32_t* tw, hipStream_t st) {
+  switch (b) {
+    case 8: tile_launch<DIF, 8>(grid, in, is, dst, ds, tw, st); return true;
+    case 9: tile_launch<DIF, 9>(grid, in, is, dst, ds, tw, st); return true;
+    case 10: tile_launch<DIF, 10>(grid, in, is, dst, ds, tw, st); return true;
+    case 11: tile_launch<DIF, 11>(grid, in, is, dst, ds, tw, st); return true;
+    case 12: tile_launch<DIF, 12>(grid, in, is, dst, ds, tw, st); return true;
+    case 13: tile_launch<DIF, 13>(grid, in, is, dst, ds, tw, st); return true;
+    case 14: tile_launch<DIF, 14>(grid, in, is, dst, ds, tw, st); return true;
+  }
+  return false;
 }
 
 static void r16_launch(const R16Pass& p, const uint32_t* in, size_t is, uint32_t* dst, size_t ds,
@@ -425,7 +522,11 @@ static void r16_launch(const R16Pass& p, const uint32_t* in, size_t is, uint32_t
   dim3 grid(1u << (L - p.b - p.c), ncols);
   KernelProbe& probe = ntt_probe();
   hipEvent_t ev0 = probe.on ? probe.begin(st) : nullptr;
-  if (dif)
+  if (p.s0 == 0 && p.c == 0 &&
+      (dif ? tile_dispatch<true>(p.b, grid, in, is, dst, ds, (const uint32_t*)T.fwd.p, st)
+           : tile_dispatch<false>(p.b, grid, in, is, dst, ds, (const uint32_t*)T.inv.p, st))) {
+    // specialised contiguous pass
+  } else if (dif)
     hipLaunchKernelGGL(k_ntt_r16<true>, grid, dim3(threads), lds * 4, st, in, dst, is, ds, p.s0,
                        p.b, p.c, (const uint32_t*)T.fwd.p);
   else
@@ -539,9 +640,19 @@ void coset_lde(const uint32_t* evals, size_t n, int w, uint32_t shift, uint32_t*
     const size_t ldsz = ((size_t)1 << (p2.b + p2.c)) + ((size_t)1 << (p2.b + p2.c - 4));
     KernelProbe& probe = ntt_probe();
     hipEvent_t ev0 = probe.on ? probe.begin(st) : nullptr;
-    hipLaunchKernelGGL(k_lde_mid, dim3(1u << (L - p2.b - p2.c), w), dim3(threads), ldsz * 4, st,
-                       (const uint32_t*)coef.p, n, lde, n, p2.s0, p2.b, p2.c,
-                       (const uint32_t*)T.inv.p, (const uint32_t*)T.fwd.p, pw, B, mp);
+    const dim3 grid(1u << (L - p2.b - p2.c), w);
+#define BFZ_MID(LL)                                                                              \
+  case LL:                                                                                       \
+    static_assert(MidPlan<LL>::b2 >= 4, "plan");                                                 \
+    hipLaunchKernelGGL(k_lde_mid<LL>, grid, dim3(threads), ldsz * 4, st, (const uint32_t*)coef.p, \
+                       n, lde, n, (const uint32_t*)T.inv.p, (const uint32_t*)T.fwd.p, pw, B, mp); \
+    break;
+    switch (L) {
+      BFZ_MID(15) BFZ_MID(16) BFZ_MID(17) BFZ_MID(18) BFZ_MID(19) BFZ_MID(20) BFZ_MID(21)
+      BFZ_MID(22) BFZ_MID(23)
+      default: throw std::runtime_error("coset_lde: log height above 23");
+    }
+#undef BFZ_MID
     KCHECK();
     if (probe.on) probe.end(ev0, st, 12.0 * (double)n * w);  // read n, write 2n
     r16_launch(p1, lde, n, lde, n, 2 * w, L, true, st);
