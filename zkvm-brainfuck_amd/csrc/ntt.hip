@@ -109,7 +109,10 @@ __device__ __forceinline__ int lds_pad(int idx, int c) { return c < 5 ? idx + (i
 //   DIF: u - v + p feeds the twiddle product directly.
 // CONST_TW: the tile's base twiddle is 1 (first DIT / last DIF window of a pass starting at
 // stage 0), so the twiddles are the compile-time small roots and w = 1 products vanish.
-template <bool DIF, bool CONST_TW>
+// TW_LOAD: read every twiddle of the stage from the table (tile kernels: s0 = lo_g = 0, the
+// table slice below 2^14 is L2-resident) instead of multiplying one loaded base by the small
+// roots -- a load replaces a Montgomery product.
+template <bool DIF, bool CONST_TW, bool TW_LOAD = false>
 __device__ __forceinline__ void r16_window(uint32_t (&x)[16], int g0, int kk_lo, int kk_hi, int s0,
                                            uint32_t m_low, uint32_t lo_g, const uint32_t* __restrict__ tw) {
   // performs stages t = g0 + kk for kk in [kk_lo, kk_hi), ascending (DIT) or descending (DIF)
@@ -122,6 +125,11 @@ __device__ __forceinline__ void r16_window(uint32_t (&x)[16], int g0, int kk_lo,
 #pragma unroll
       for (int l = 0; l < 8; l++)
         if (l < (1 << kk)) tws[l] = DIF ? SMALL.f[(1 << kk) + l] : SMALL.i[(1 << kk) + l];
+    } else if (TW_LOAD) {
+      const uint32_t* tt = tw + (1u << (g0 + kk)) + m_low;
+#pragma unroll
+      for (int l = 0; l < 8; l++)
+        if (l < (1 << kk)) tws[l] = tt[l << g0];
     } else {
       const int t = g0 + kk;
       const uint32_t wb = tw[(1u << (s0 + t)) + (m_low << s0) + lo_g];
@@ -270,7 +278,7 @@ __global__ __launch_bounds__(1 << (B - 4)) void k_ntt_tile(const uint32_t* __res
     if (g0 == 0)
       r16_window<DIF, true>(x, g0, kk_lo, kk_hi, 0, m_low, 0, tw);
     else
-      r16_window<DIF, false>(x, g0, kk_lo, kk_hi, 0, m_low, 0, tw);
+      r16_window<DIF, false, true>(x, g0, kk_lo, kk_hi, 0, m_low, 0, tw);
 #pragma unroll
     for (int i = 0; i < 16; i++) lds[pb + (i << g0) + ((i << g0) >> 4)] = x[i];
   }
