@@ -101,6 +101,8 @@ int bfz_coset_lde(const uint32_t* evals, size_t n, size_t w, uint32_t shift, uin
 int bfz_commit(const uint32_t* const* mats, const size_t* heights, const size_t* widths,
                size_t nmats, uint32_t root[8]);
 int bfz_poseidon2_permute(uint32_t* states, size_t n);
+/* The latency-optimised form used for small Merkle layers (16 lanes per state, DPP). */
+int bfz_poseidon2_permute_small(uint32_t* states, size_t n);
 
 #ifdef __cplusplus
 }

@@ -45,6 +45,18 @@ def test_poseidon2_batch_parity():
         assert np.array_equal(got, exp)
 
 
+def test_poseidon2_lane_mode_parity():
+    """16-lanes-per-state permutation (DPP cross-lane MDS) == oracle."""
+    rng = np.random.default_rng(3)
+    st = rng.integers(0, P, size=(100, 16), dtype=np.uint64).astype(np.uint32)
+    st[0] = GOLDEN["poseidon2"][0]["in"]
+    dev = mont(st).reshape(-1).copy()
+    _lib.check(_lib.lib().bfz_poseidon2_permute_small(dev.ctypes.data_as(P32), len(st)))
+    got = unmont(dev).reshape(-1, 16)
+    assert got[0].tolist() == GOLDEN["poseidon2"][0]["out"]
+    assert np.array_equal(got, O.poseidon2(st.reshape(-1)).reshape(-1, 16))
+
+
 @pytest.mark.parametrize("logn,w", [(0, 3), (1, 2), (4, 31), (5, 1), (10, 45), (13, 7), (16, 4),
                                     (17, 9), (20, 2)])
 def test_coset_lde_parity(logn, w):

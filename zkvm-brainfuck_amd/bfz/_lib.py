@@ -62,6 +62,7 @@ SIGNATURES = [
     ("bfz_commit", c_int, [POINTER(POINTER(c_uint32)), POINTER(c_size_t), POINTER(c_size_t),
                            c_size_t, POINTER(c_uint32)]),
     ("bfz_poseidon2_permute", c_int, [POINTER(c_uint32), c_size_t]),
+    ("bfz_poseidon2_permute_small", c_int, [POINTER(c_uint32), c_size_t]),
 ]
 
 _lib = None

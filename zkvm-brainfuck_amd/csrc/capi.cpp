@@ -304,4 +304,16 @@ int bfz_poseidon2_permute(uint32_t* states, size_t n) {
   });
 }
 
+int bfz_poseidon2_permute_small(uint32_t* states, size_t n) {
+  return guarded([&] {
+    hipStream_t st = bfz::stream();
+    bfz::DBuf<uint32_t> d(16 * n);
+    HIP_CHECK(hipMemcpyAsync(d.p, states, 16 * n * 4, hipMemcpyHostToDevice, st));
+    bfz::poseidon2_batch_small(d.p, n, st);
+    HIP_CHECK(hipMemcpyAsync(states, d.p, 16 * n * 4, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    return 0;
+  });
+}
+
 }  // extern "C"

@@ -26,6 +26,9 @@ void merkle_build(const std::vector<MatRef>& mats, MerkleTree& tree, hipStream_t
 // Batched Poseidon2 permutations of n 16-element states in place (device pointer).
 void poseidon2_batch(uint32_t* states, size_t n, hipStream_t st);
 
+// Same, latency-optimised (16 lanes per state; for few states).
+void poseidon2_batch_small(uint32_t* states, size_t n, hipStream_t st);
+
 // Hash of 8-element rows (FRI commit-phase leaves: pairs of EF values), one permutation each.
 void hash_rows8(const uint32_t* rows, size_t n, uint32_t* digests, hipStream_t st);
 

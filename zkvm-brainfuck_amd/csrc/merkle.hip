@@ -99,10 +99,32 @@ __global__ __launch_bounds__(256) void k_compress(const uint32_t* __restrict__ p
   store8(out + 8 * j, st);
 }
 
+// Merkle node j in lane mode (see poseidon2_permute_lane): lane l of the node's 16-lane row
+// holds word l of the state; the digest ends up in lanes 0..7.
+__device__ __forceinline__ uint32_t merkle_node_lane(uint32_t v, const ColList& cl, int c0, int c1,
+                                                     size_t j, int lane) {
+  v = poseidon2_permute_lane(v, lane);
+  const int nchunks = (c1 - c0 + 7) >> 3;
+  if (nchunks) {
+    const uint32_t d = v;
+    uint32_t h = 0;
+    for (int k = 0; k < nchunks; k++) {  // PaddingFreeSponge, overwrite mode
+      const int col = c0 + 8 * k + lane;
+      if (lane < 8 && col < c1) h = cl.p[col][j];
+      h = poseidon2_permute_lane(h, lane);
+    }
+    const uint32_t hs = dpp<DPP_ROR8>(h);  // lanes 8..15 <- h[0..7]
+    v = poseidon2_permute_lane(lane < 8 ? d : hs, lane);
+  }
+  return v;
+}
+
 // All layers of <= TOP_NODES nodes in one workgroup: layer l reads the previous layer from
 // LDS (the first from HBM), writes its digests to HBM (query paths need every layer) and to
-// LDS for the next.  Removes one launch + one permutation latency tail per small layer.
+// LDS for the next.  Layers of <= LANE_NODES nodes switch to lane mode (16 lanes per node):
+// there the permutation latency, not throughput, is the cost.
 constexpr int TOP_NODES = 512;
+constexpr int LANE_NODES = 256;   // up to 4 batches of 64 nodes per 1024-thread block
 constexpr int MAXTOP = 24;
 struct TopLayers {
   uint32_t* out[MAXTOP];
@@ -110,30 +132,73 @@ struct TopLayers {
   int n;
 };
 
-__global__ __launch_bounds__(TOP_NODES) void k_compress_top(const uint32_t* __restrict__ prev,
-                                                            size_t nlen, ColList inj,
-                                                            TopLayers tl) {
+__global__ __launch_bounds__(1024) void k_compress_top(const uint32_t* __restrict__ prev,
+                                                       size_t nlen, ColList inj, TopLayers tl) {
   __shared__ uint4 buf[2][TOP_NODES * 2];
   for (int l = 0; l < tl.n; l++, nlen >>= 1) {
-    for (size_t j = threadIdx.x; j < nlen; j += blockDim.x) {
-      uint32_t st[16];
-      if (l == 0) {
-        load16(st, prev + 16 * j);
-      } else {
-        const uint4* s4 = buf[(l - 1) & 1] + 4 * j;
-        const uint4 a = s4[0], b = s4[1], c = s4[2], d = s4[3];
-        st[0] = a.x; st[1] = a.y; st[2] = a.z; st[3] = a.w;
-        st[4] = b.x; st[5] = b.y; st[6] = b.z; st[7] = b.w;
-        st[8] = c.x; st[9] = c.y; st[10] = c.z; st[11] = c.w;
-        st[12] = d.x; st[13] = d.y; st[14] = d.z; st[15] = d.w;
+    const uint32_t* src32 = l == 0 ? prev : reinterpret_cast<const uint32_t*>(buf[(l - 1) & 1]);
+    uint32_t* dst32 = reinterpret_cast<uint32_t*>(buf[l & 1]);
+    if (nlen <= (size_t)LANE_NODES) {
+      const int lane = threadIdx.x & 15;
+      for (size_t j = threadIdx.x >> 4; j < nlen; j += blockDim.x >> 4) {
+        // whole 16-lane rows are active together (DPP needs all of them)
+        const uint32_t v = merkle_node_lane(src32[16 * j + lane], inj, tl.c0[l], tl.c1[l], j, lane);
+        if (lane < 8) {
+          tl.out[l][8 * j + lane] = v;
+          dst32[8 * j + lane] = v;
+        }
       }
-      merkle_node(st, inj, tl.c0[l], tl.c1[l], j);
-      store8(tl.out[l] + 8 * j, st);
-      buf[l & 1][2 * j] = make_uint4(st[0], st[1], st[2], st[3]);
-      buf[l & 1][2 * j + 1] = make_uint4(st[4], st[5], st[6], st[7]);
+    } else {
+      for (size_t j = threadIdx.x; j < nlen; j += blockDim.x) {
+        uint32_t st[16];
+        if (l == 0) {
+          load16(st, prev + 16 * j);
+        } else {
+          const uint4* s4 = buf[(l - 1) & 1] + 4 * j;
+          const uint4 a = s4[0], b = s4[1], c = s4[2], d = s4[3];
+          st[0] = a.x; st[1] = a.y; st[2] = a.z; st[3] = a.w;
+          st[4] = b.x; st[5] = b.y; st[6] = b.z; st[7] = b.w;
+          st[8] = c.x; st[9] = c.y; st[10] = c.z; st[11] = c.w;
+          st[12] = d.x; st[13] = d.y; st[14] = d.z; st[15] = d.w;
+        }
+        merkle_node(st, inj, tl.c0[l], tl.c1[l], j);
+        store8(tl.out[l] + 8 * j, st);
+        buf[l & 1][2 * j] = make_uint4(st[0], st[1], st[2], st[3]);
+        buf[l & 1][2 * j + 1] = make_uint4(st[4], st[5], st[6], st[7]);
+      }
     }
     __syncthreads();
   }
+}
+
+// Medium layers (TOP_NODES < nodes <= LANE_LAYER_MAX) in lane mode: a single-lane launch of
+// this size is one permutation latency long (~12 us) while 16 lanes per node finish sooner.
+constexpr size_t LANE_LAYER_MAX = (size_t)1 << 14;
+__global__ __launch_bounds__(256) void k_compress_lanes(const uint32_t* __restrict__ prev,
+                                                        size_t nlen, uint32_t* __restrict__ out,
+                                                        ColList inj) {
+  const size_t j = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+  const int lane = threadIdx.x & 15;
+  if (j >= nlen) return;
+  const uint32_t v = merkle_node_lane(prev[16 * j + lane], inj, 0, inj.n, j, lane);
+  if (lane < 8) out[8 * j + lane] = v;
+}
+
+__global__ __launch_bounds__(256) void k_hash_rows8_lanes(const uint32_t* __restrict__ rows,
+                                                          size_t n, uint32_t* __restrict__ out) {
+  const size_t i = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+  const int lane = threadIdx.x & 15;
+  if (i >= n) return;
+  const uint32_t v = poseidon2_permute_lane(lane < 8 ? rows[8 * i + lane] : 0u, lane);
+  if (lane < 8) out[8 * i + lane] = v;
+}
+
+// Lane-mode batch permutation (bfz_poseidon2_permute_small): 16 lanes per state.
+__global__ __launch_bounds__(256) void k_permute_lanes(uint32_t* __restrict__ s, size_t n) {
+  const size_t i = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+  const int lane = threadIdx.x & 15;
+  if (i >= n) return;
+  s[16 * i + lane] = poseidon2_permute_lane(s[16 * i + lane], lane);
 }
 
 __global__ __launch_bounds__(256) void k_permute_batch(uint32_t* __restrict__ s, size_t n) {
@@ -186,8 +251,12 @@ static void build_layers(MerkleTree& t, size_t len, const std::vector<const MatR
     std::vector<const MatRef*> grp;
     while (next < sorted.size() && sorted[next]->height == nlen) grp.push_back(sorted[next++]);
     t.layers[L].reset(8 * nlen);
-    hipLaunchKernelGGL(k_compress, dim3(ceil_div(nlen, 256)), dim3(256), 0, st,
-                       (const uint32_t*)t.layers[L - 1].p, nlen, t.layers[L].p, make_cols(grp));
+    if (nlen <= LANE_LAYER_MAX)
+      hipLaunchKernelGGL(k_compress_lanes, dim3(ceil_div(16 * nlen, 256)), dim3(256), 0, st,
+                         (const uint32_t*)t.layers[L - 1].p, nlen, t.layers[L].p, make_cols(grp));
+    else
+      hipLaunchKernelGGL(k_compress, dim3(ceil_div(nlen, 256)), dim3(256), 0, st,
+                         (const uint32_t*)t.layers[L - 1].p, nlen, t.layers[L].p, make_cols(grp));
     KCHECK();
     len = nlen;
   }
@@ -206,8 +275,7 @@ static void build_layers(MerkleTree& t, size_t len, const std::vector<const MatR
       t.layers[L + l].reset(8 * nlen);
       tl.out[l] = t.layers[L + l].p;
     }
-    const int threads = (int)std::max<size_t>(64, len >> 1);
-    hipLaunchKernelGGL(k_compress_top, dim3(1), dim3(threads), 0, st,
+    hipLaunchKernelGGL(k_compress_top, dim3(1), dim3(1024), 0, st,
                        (const uint32_t*)t.layers[L - 1].p, len >> 1, make_cols(all), tl);
     KCHECK();
   }
@@ -247,8 +315,17 @@ void poseidon2_batch(uint32_t* states, size_t n, hipStream_t st) {
   KCHECK();
 }
 
+void poseidon2_batch_small(uint32_t* states, size_t n, hipStream_t st) {
+  hipLaunchKernelGGL(k_permute_lanes, dim3(ceil_div(16 * n, 256)), dim3(256), 0, st, states, n);
+  KCHECK();
+}
+
 void hash_rows8(const uint32_t* rows, size_t n, uint32_t* digests, hipStream_t st) {
-  hipLaunchKernelGGL(k_hash_rows8, dim3(ceil_div(n, 256)), dim3(256), 0, st, rows, n, digests);
+  if (n <= LANE_LAYER_MAX)
+    hipLaunchKernelGGL(k_hash_rows8_lanes, dim3(ceil_div(16 * n, 256)), dim3(256), 0, st, rows, n,
+                       digests);
+  else
+    hipLaunchKernelGGL(k_hash_rows8, dim3(ceil_div(n, 256)), dim3(256), 0, st, rows, n, digests);
   KCHECK();
 }
 

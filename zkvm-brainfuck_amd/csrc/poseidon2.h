@@ -163,4 +163,53 @@ KB_HD void poseidon2_permute(uint32_t s[16]) {
   poseidon2_permute_n<1>(*reinterpret_cast<uint32_t(*)[1][16]>(s));
 }
 
+// ---------------------------------------------------------------------------------------
+// Latency-optimised permutation: one state element per lane, a state per 16-lane DPP row
+// (lane = threadIdx.x & 15).  Cross-lane steps use DPP: quad_perm rotations for the M4 blocks,
+// row_ror for the block sums and the internal-round total.  About 1/6 of the single-lane
+// latency; used where only a few permutations are in flight (top layers of Merkle trees).
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+}
+constexpr int DPP_QROT1 = 0x39, DPP_QROT2 = 0x4E, DPP_QROT3 = 0x93;  // quad_perm x_{j+1,2,3}
+constexpr int DPP_ROR1 = 0x121, DPP_ROR2 = 0x122, DPP_ROR4 = 0x124, DPP_ROR8 = 0x128;
+
+__device__ __forceinline__ uint32_t mds_light_lane(uint32_t x) {
+  const uint32_t a1 = dpp<DPP_QROT1>(x), a2 = dpp<DPP_QROT2>(x), a3 = dpp<DPP_QROT3>(x);
+  const uint32_t s4 = madd(madd(x, a1), madd(a2, a3));
+  const uint32_t y = madd(madd(s4, x), mdbl(a1));  // 2x_j + 3x_{j+1} + x_{j+2} + x_{j+3}
+  const uint32_t t = madd(y, dpp<DPP_ROR8>(y));
+  return madd(y, madd(t, dpp<DPP_ROR4>(t)));      // + sum of the 4 blocks at this position
+}
+
+__device__ __forceinline__ uint32_t sum_lanes16(uint32_t v) {
+  v = madd(v, dpp<DPP_ROR1>(v));
+  v = madd(v, dpp<DPP_ROR2>(v));
+  v = madd(v, dpp<DPP_ROR4>(v));
+  return madd(v, dpp<DPP_ROR8>(v));
+}
+
+__device__ __forceinline__ uint32_t poseidon2_permute_lane(uint32_t v, int lane) {
+  uint32_t rce[8];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    rce[r] = P2.ext_init[r][lane];
+    rce[4 + r] = P2.ext_term[r][lane];
+  }
+  const uint32_t dg = P2.diag[lane];
+  v = mds_light_lane(v);
+#pragma unroll
+  for (int r = 0; r < 4; r++) v = mds_light_lane(cube(madd(v, rce[r])));
+#pragma unroll
+  for (int r = 0; r < 13; r++) {
+    const uint32_t c = cube(madd(v, P2.internal[r]));
+    v = lane == 0 ? c : v;
+    v = madd(sum_lanes16(v), mmul(v, dg));
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r++) v = mds_light_lane(cube(madd(v, rce[4 + r])));
+  return v;
+}
+
 }  // namespace kb
