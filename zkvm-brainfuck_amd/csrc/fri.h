@@ -26,8 +26,9 @@ struct GrindState {        // DuplexChallenger state at grind time
 // out[t] = 1 / (x_t - z), x_t = 3 * w_H^bitrev(t), t < 2^logH
 void inv_denoms(const kb::EF& z, int logH, kb::EF* out, hipStream_t st);
 // out_dev[c] = value at z of column c of a committed LDE (height = 2n), via the low coset.
-void open_matrix(const uint32_t* mat, size_t height, int w, const kb::EF* invd,
-                 const kb::EF& scale, kb::EF* out_dev, hipStream_t st);
+void open_matrix(const uint32_t* mat, size_t height, int w, const kb::EF* invd_a,
+                 const kb::EF& scale_a, kb::EF* out_a, const kb::EF* invd_b,
+                 const kb::EF& scale_b, kb::EF* out_b, hipStream_t st);
 // ro[t] += (sum_c ca_c v_c[t] - ya) invd_a[t] + (sum_m kb_m sum_(c in m) ca_c v_c[t] - yb) invd_b[t]
 void reduce_height(const std::vector<RedCol>& cols, const std::vector<RedMat>& mats, size_t H,
                    const kb::EF* invd_a,

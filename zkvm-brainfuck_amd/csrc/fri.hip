@@ -54,39 +54,39 @@ __global__ __launch_bounds__(256) void k_inv_denoms(EF z, int logH, const uint32
 }
 
 // Lazy dot products: raw 64-bit products of Montgomery values (each < p^2) accumulate with
-// v_mad_u64_u32, four at a time (4 p^2 < 2^64 and its high word < 2p, mreduce's domain),
-// so a column costs four multiply-adds instead of an EF x base Montgomery product + EF add.
+// v_mad_u64_u32; every 4 products the accumulator is folded, acc = hi * (2^32 mod p) + lo
+// (< 2^57, one more v_mad_u64_u32), which leaves room for 4 more (4 p^2 + 2^57 < 2^64).  One
+// Montgomery reduction at the end (fold < 2^57: its high word is far below 2p).
 struct LazyEF {
+  static constexpr uint32_t C32 = (1u << 25) - 2;  // 2^32 mod p
   uint64_t acc[4];
-  EF sum;
   int pending;
   __device__ __forceinline__ void init() {
 #pragma unroll
     for (int e = 0; e < 4; e++) acc[e] = 0;
-    sum = ef_zero();
     pending = 0;
   }
-  __device__ __forceinline__ void flush() {
+  __device__ __forceinline__ void fold() {
 #pragma unroll
-    for (int e = 0; e < 4; e++) {
-      sum.c[e] = madd(sum.c[e], mreduce(acc[e]));
-      acc[e] = 0;
-    }
+    for (int e = 0; e < 4; e++) acc[e] = (uint64_t)(uint32_t)(acc[e] >> 32) * C32 + (uint32_t)acc[e];
     pending = 0;
   }
   __device__ __forceinline__ void add(const EF& coef, uint32_t v) {
 #pragma unroll
     for (int e = 0; e < 4; e++) acc[e] += (uint64_t)coef.c[e] * v;
-    if (++pending == 4) flush();
+    if (++pending == 4) fold();
   }
   __device__ __forceinline__ EF get() {
-    flush();
-    return sum;
+    fold();
+    EF r;
+#pragma unroll
+    for (int e = 0; e < 4; e++) r.c[e] = mreduce(acc[e]);
+    return r;
   }
 };
 
 // ------------------------------------------------------------------ openings
-constexpr int OPEN_T = 256, OPEN_R = 4, OPEN_CH = OPEN_T * OPEN_R;
+constexpr int OPEN_T = 256, OPEN_R = 8, OPEN_CH = OPEN_T * OPEN_R;
 
 __device__ __forceinline__ EF wave_sum(EF v) {
 #pragma unroll
@@ -96,7 +96,22 @@ __device__ __forceinline__ EF wave_sum(EF v) {
   return v;
 }
 
-// partial[chunk * w + c] = sum_{t in chunk} W_t * col_c[t],  W_t = -x_t * invd[t]
+// Sum over the 64 lanes of a wave: DPP rotations inside each 16-lane row, then two
+// cross-row exchanges.  Every lane ends with the total.
+__device__ __forceinline__ uint32_t wave_sum_u(uint32_t v) {
+  v = madd(v, dpp<DPP_ROR1>(v));
+  v = madd(v, dpp<DPP_ROR2>(v));
+  v = madd(v, dpp<DPP_ROR4>(v));
+  v = madd(v, dpp<DPP_ROR8>(v));
+  v = madd(v, (uint32_t)__shfl_xor((int)v, 16, 64));
+  return madd(v, (uint32_t)__shfl_xor((int)v, 32, 64));
+}
+
+// Barycentric opening of one matrix at one point:
+// partial[chunk * w + c] = sum_{t in chunk} W_t col_c[t],  W_t = -x_t invd[t].
+// A thread owns OPEN_R rows and keeps their weights in registers across all columns (the
+// per-column wave reduction is amortized over OPEN_R rows); the next column's loads are
+// issued before the current column's reduction.
 __global__ __launch_bounds__(OPEN_T) void k_open_partial(const uint32_t* __restrict__ mat,
                                                          size_t height, int w, size_t n, int logH,
                                                          const EF* __restrict__ invd,
@@ -105,36 +120,44 @@ __global__ __launch_bounds__(OPEN_T) void k_open_partial(const uint32_t* __restr
   __shared__ EF sh[OPEN_T / 64][64];
   const size_t c0 = (size_t)blockIdx.x * OPEN_CH;
   EF W[OPEN_R];
-  size_t rows[OPEN_R];
+  uint32_t rows[OPEN_R];
 #pragma unroll
   for (int r = 0; r < OPEN_R; r++) {
     const size_t t = c0 + (size_t)r * OPEN_T + threadIdx.x;
-    rows[r] = t;
-    if (t < n) {
-      const uint32_t x = coset_point((uint32_t)t, logH, twf);
-      W[r] = ef_neg(ef_mul_base(invd[t], x));
-    } else {
-      W[r] = ef_zero();
-    }
+    rows[r] = (uint32_t)t;
+    W[r] = ef_zero();
+    if (t < n) W[r] = ef_neg(ef_mul_base(invd[t], coset_point((uint32_t)t, logH, twf)));
   }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint32_t v[OPEN_R], nv[OPEN_R];
+#pragma unroll
+  for (int r = 0; r < OPEN_R; r++) v[r] = rows[r] < n ? mat[rows[r]] : 0u;
   for (int cb = 0; cb < w; cb += 64) {
     const int cw = min(64, w - cb);
     for (int c = 0; c < cw; c++) {
-      const uint32_t* col = mat + (size_t)(cb + c) * height;
-      LazyEF lz;  // OPEN_R = 4 products per component: one reduction per column
+      const int cn = cb + c + 1;
+      if (cn < w) {
+        const uint32_t* coln = mat + (size_t)cn * height;
+#pragma unroll
+        for (int r = 0; r < OPEN_R; r++) nv[r] = rows[r] < n ? coln[rows[r]] : 0u;
+      }
+      LazyEF lz;
       lz.init();
 #pragma unroll
-      for (int r = 0; r < OPEN_R; r++) lz.add(W[r], rows[r] < n ? col[rows[r]] : 0u);
-      EF acc = wave_sum(lz.get());
+      for (int r = 0; r < OPEN_R; r++) lz.add(W[r], v[r]);
+      EF acc = lz.get();
+#pragma unroll
+      for (int e = 0; e < 4; e++) acc.c[e] = wave_sum_u(acc.c[e]);
       if (lane == 0) sh[wave][c] = acc;
+#pragma unroll
+      for (int r = 0; r < OPEN_R; r++) v[r] = nv[r];
     }
     __syncthreads();
     if (threadIdx.x < (unsigned)cw) {
-      EF s = sh[0][threadIdx.x];
+      EF a = sh[0][threadIdx.x];
 #pragma unroll
-      for (int k = 1; k < OPEN_T / 64; k++) s = ef_add(s, sh[k][threadIdx.x]);
-      partial[(size_t)blockIdx.x * w + cb + threadIdx.x] = s;
+      for (int k = 1; k < OPEN_T / 64; k++) a = ef_add(a, sh[k][threadIdx.x]);
+      partial[(size_t)blockIdx.x * w + cb + threadIdx.x] = a;
     }
     __syncthreads();
   }
@@ -170,7 +193,16 @@ __global__ __launch_bounds__(256) void k_reduce(const RedCol* __restrict__ cols,
       const RedMat rm = mats[m];
       LazyEF acc;
       acc.init();
-      for (int c = rm.first; c < rm.first + rm.count; c++) acc.add(cols[c].ca, cols[c].col[t]);
+      const int end = rm.first + rm.count;
+      int c = rm.first;
+      for (; c + 4 <= end; c += 4) {  // four column loads in flight per step
+        uint32_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) v[k] = cols[c + k].col[t];
+#pragma unroll
+        for (int k = 0; k < 4; k++) acc.add(cols[c + k].ca, v[k]);
+      }
+      for (; c < end; c++) acc.add(cols[c].ca, cols[c].col[t]);
       const EF s = acc.get();
       sa = ef_add(sa, s);
       if (rm.has_b) sb = ef_add(sb, ef_mul(s, rm.kb));
@@ -237,18 +269,20 @@ void inv_denoms(const EF& z, int logH, EF* out, hipStream_t st) {
   KCHECK();
 }
 
-void open_matrix(const uint32_t* mat, size_t height, int w, const EF* invd, const EF& scale,
-                 EF* out_dev, hipStream_t st) {
+void open_matrix(const uint32_t* mat, size_t height, int w, const EF* invd_a, const EF& scale_a,
+                 EF* out_a, const EF* invd_b, const EF& scale_b, EF* out_b, hipStream_t st) {
   const size_t n = height / 2;  // low coset = first half of the bit-reversed LDE
   const int logH = log2i(height);
   const int nchunks = (int)ceil_div(n, OPEN_CH);
   DBuf<EF> partial((size_t)nchunks * w);
-  hipLaunchKernelGGL(k_open_partial, dim3(nchunks), dim3(OPEN_T), 0, st, mat, height, w, n, logH,
-                     invd, (const uint32_t*)twiddles().fwd.p, partial.p);
-  KCHECK();
-  hipLaunchKernelGGL(k_open_final, dim3(w), dim3(256), 0, st, (const EF*)partial.p, nchunks, w,
-                     scale, out_dev);
-  KCHECK();
+  for (int p = 0; p < (invd_b ? 2 : 1); p++) {
+    hipLaunchKernelGGL(k_open_partial, dim3(nchunks), dim3(OPEN_T), 0, st, mat, height, w, n, logH,
+                       p ? invd_b : invd_a, (const uint32_t*)twiddles().fwd.p, partial.p);
+    KCHECK();
+    hipLaunchKernelGGL(k_open_final, dim3(w), dim3(256), 0, st, (const EF*)partial.p, nchunks, w,
+                       p ? scale_b : scale_a, p ? out_b : out_a);
+    KCHECK();
+  }
 }
 
 void reduce_height(const std::vector<RedCol>& cols, const std::vector<RedMat>& mats, size_t H,

@@ -382,14 +382,15 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
       const int lh = m.log_n + LOG_BLOWUP;
       const EF three_n = ef_base(mpow(to_mont(3), m.n));
       const uint32_t n_f = to_mont((uint32_t)(m.n % P));
+      EF scale[2];
       for (int j = 0; j < mp[r][i].npts; j++) {
-        const EF z = mp[r][i].pts[j];
-        const EF zn = ef_pow(z, m.n);
-        const EF scale = ef_mul(ef_sub(zn, three_n), ef_inv(ef_mul_base(three_n, n_f)));
-        const EF* invd = j == 0 ? invd_zeta.p : invd_next.at(lh).p;
-        open_matrix(m.lde.buf.p, m.lde.height, m.lde.width, invd, scale, opened_d.p + mp[r][i].off[j],
-                    st);
+        const EF zn = ef_pow(mp[r][i].pts[j], m.n);
+        scale[j] = ef_mul(ef_sub(zn, three_n), ef_inv(ef_mul_base(three_n, n_f)));
       }
+      const bool two = mp[r][i].npts == 2;
+      open_matrix(m.lde.buf.p, m.lde.height, m.lde.width, invd_zeta.p, scale[0],
+                  opened_d.p + mp[r][i].off[0], two ? invd_next.at(lh).p : nullptr,
+                  two ? scale[1] : scale[0], two ? opened_d.p + mp[r][i].off[1] : nullptr, st);
     }
   std::vector<EF> opened(nvals);
   HIP_CHECK(hipMemcpyAsync(opened.data(), opened_d.p, nvals * sizeof(EF), hipMemcpyDeviceToHost, st));
