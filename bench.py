@@ -33,7 +33,7 @@ def ntt_traffic():
     (scripts/gpu_pmc.sh: FETCH_SIZE x2 per MI355X_MICROARCH.md + WRITE_SIZE, separate runs)."""
     try:
         k = json.load(open(PMC_SUMMARY))["kernels"]
-        rows = [v for n, v in k.items() if "k_ntt_r16" in n or "k_lde_mid" in n]
+        rows = [v for n, v in k.items() if any(x in n for x in ("k_ntt_r16", "k_ntt_tile", "k_lde_mid"))]
         launches = sum(v["launches"] for v in rows)
         traffic = sum(v["traffic_kB_fetch_x2_plus_write"] * v["launches"] for v in rows) * 1024
         alg = sum(v["algorithmic_kB"] * v["launches"] for v in rows) * 1024
@@ -163,9 +163,9 @@ def main():
                          "traffic": round(traffic_b) if traffic_b else None,
                          "traffic_over_algorithmic": round(traffic_ratio, 4) if traffic_ratio else None,
                          "traffic_source": "profiles/r01/pmc_summary.json (bytes per launch)",
-                         "kernel": "NTT kernels: k_ntt_r16 (radix-16 pass, 8 B per element: one "
-                                   "read + one write) and k_lde_mid (fused iDFT pass 2 + coset "
-                                   "scale + DFT pass 1, 12 B per input element)",
+                         "kernel": "NTT kernels: k_ntt_tile (radix-16 contiguous pass, 8 B per "
+                                   "element: one read + one write) and k_lde_mid (fused iDFT "
+                                   "pass 2 + coset scale + DFT pass 1, 12 B per input element)",
                          "launches": tm.ntt_kernel_launches,
                          "avg_launch_us": round(ntt_avg_us, 2),
                          "note": "per-launch HIP events on the prover stream; whole-LDE rate "

@@ -1,7 +1,7 @@
 """Summarize rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes per kernel.
 
 For the NTT kernels (the bench roofline kernels) it reports, per launch, the algorithmic
-bytes next to the counted traffic: k_ntt_r16 8 B per element (one read + one write),
+bytes next to the counted traffic: k_ntt_tile / k_ntt_r16 8 B per element (one read + one write),
 k_lde_mid 12 B per input element (read n, write the 2n LDE); a launch covers Grid_Size * 16
 input elements.
 MI355X_MICROARCH.md: FETCH_SIZE under-reports wide coalesced reads by exactly 2x on gfx950;
@@ -27,7 +27,7 @@ def per_kernel(rows):
     agg = collections.defaultdict(lambda: {"launches": 0, "value": 0.0, "grid": 0})
     for r in rows:
         name = r.get("Kernel_Name", "?")
-        key = name.split("(")[0]
+        key = name.split("(")[0]  # template arguments kept: k_ntt_tile<true, 14> etc.
         a = agg[key]
         a["launches"] += 1
         a["value"] += float(r.get("Counter_Value", 0) or 0)
@@ -45,7 +45,7 @@ def main(root):
         e = {"launches": n,
              "fetch_kB": round(f["value"] / f["launches"], 1) if f else None,
              "write_kB": round(w["value"] / w["launches"], 1) if w else None}
-        per_elem = 8 if "k_ntt_r16" in k else 12 if "k_lde_mid" in k else 0
+        per_elem = 8 if ("k_ntt_r16" in k or "k_ntt_tile" in k) else 12 if "k_lde_mid" in k else 0
         if per_elem and f and w:  # NTT kernels: a launch covers Grid_Size * 16 input elements
             elems = f["grid"] / f["launches"] * 16
             e["algorithmic_kB"] = round(per_elem * elems / 1024, 1)
