@@ -37,6 +37,16 @@ void reduce_height(const std::vector<RedCol>& cols, const std::vector<RedMat>& m
 void fri_fold(const kb::EF* in, kb::EF* out, size_t h, const kb::EF& beta, const kb::EF* add,
               hipStream_t st);
 uint32_t grind(const GrindState& gs, int bits, hipStream_t st);
-void gather_words(const std::vector<uint64_t>& addrs, std::vector<uint32_t>& out, hipStream_t st);
+// Query openings: word k of segment s for query index I is
+//   base[((I >> shift) ^ xr) * unit + k * stride],  k < count
+// (matrix rows: unit 1, stride = height; Merkle siblings: unit 8; FRI siblings: unit 4).
+struct GatherSeg {
+  const uint32_t* base;
+  uint64_t stride;
+  uint32_t shift, xr, unit, count;
+};
+// out[q * words_per_query + ...] = the segments' words for qidx[q], segments in order.
+void gather_queries(const std::vector<GatherSeg>& segs, const std::vector<uint32_t>& qidx,
+                    std::vector<uint32_t>& out, hipStream_t st);
 
 }  // namespace bfz

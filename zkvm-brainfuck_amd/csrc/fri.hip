@@ -252,11 +252,19 @@ __global__ __launch_bounds__(256) void k_grind(GrindState gs, uint32_t start, ui
   if ((v & ((1u << bits) - 1)) == 0) atomicMin(best, w);
 }
 
-// ------------------------------------------------------------------ gather
-__global__ __launch_bounds__(256) void k_gather_words(const uint64_t* __restrict__ addrs, size_t n,
-                                                      uint32_t* __restrict__ out) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = *reinterpret_cast<const uint32_t*>(addrs[i]);
+// ------------------------------------------------------------------ query gather
+__global__ __launch_bounds__(256) void k_gather_segs(const GatherSeg* __restrict__ segs, int nseg,
+                                                     const uint32_t* __restrict__ seg_off,
+                                                     uint32_t words_per_q,
+                                                     const uint32_t* __restrict__ qidx, int nq,
+                                                     uint32_t* __restrict__ out) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)nseg * nq) return;
+  const int q = (int)(t / nseg), s = (int)(t % nseg);
+  const GatherSeg g = segs[s];
+  const uint64_t pos = (uint64_t)((qidx[q] >> g.shift) ^ g.xr) * g.unit;
+  uint32_t* o = out + (size_t)q * words_per_q + seg_off[s];
+  for (uint32_t k = 0; k < g.count; k++) o[k] = g.base[pos + k * g.stride];
 }
 
 // ================================================================== host wrappers
@@ -329,16 +337,28 @@ uint32_t grind(const GrindState& gs, int bits, hipStream_t st) {
   throw std::runtime_error("grind: no witness");
 }
 
-void gather_words(const std::vector<uint64_t>& addrs, std::vector<uint32_t>& out, hipStream_t st) {
-  out.assign(addrs.size(), 0);
-  if (addrs.empty()) return;
-  DBuf<uint64_t> a(addrs.size());
-  DBuf<uint32_t> o(addrs.size());
-  HIP_CHECK(hipMemcpyAsync(a.p, addrs.data(), addrs.size() * 8, hipMemcpyHostToDevice, st));
-  hipLaunchKernelGGL(k_gather_words, dim3(ceil_div(addrs.size(), 256)), dim3(256), 0, st,
-                     (const uint64_t*)a.p, addrs.size(), o.p);
+void gather_queries(const std::vector<GatherSeg>& segs, const std::vector<uint32_t>& qidx,
+                    std::vector<uint32_t>& out, hipStream_t st) {
+  std::vector<uint32_t> off(segs.size());
+  uint32_t wpq = 0;
+  for (size_t s = 0; s < segs.size(); s++) {
+    off[s] = wpq;
+    wpq += segs[s].count;
+  }
+  out.assign((size_t)wpq * qidx.size(), 0);
+  if (out.empty()) return;
+  DBuf<GatherSeg> dseg(segs.size());
+  DBuf<uint32_t> doff(off.size()), dq(qidx.size()), dout(out.size());
+  HIP_CHECK(hipMemcpyAsync(dseg.p, segs.data(), segs.size() * sizeof(GatherSeg),
+                           hipMemcpyHostToDevice, st));
+  HIP_CHECK(hipMemcpyAsync(doff.p, off.data(), off.size() * 4, hipMemcpyHostToDevice, st));
+  HIP_CHECK(hipMemcpyAsync(dq.p, qidx.data(), qidx.size() * 4, hipMemcpyHostToDevice, st));
+  const size_t nthreads = segs.size() * qidx.size();
+  hipLaunchKernelGGL(k_gather_segs, dim3(ceil_div(nthreads, 256)), dim3(256), 0, st,
+                     (const GatherSeg*)dseg.p, (int)segs.size(), (const uint32_t*)doff.p, wpq,
+                     (const uint32_t*)dq.p, (int)qidx.size(), dout.p);
   KCHECK();
-  HIP_CHECK(hipMemcpyAsync(out.data(), o.p, addrs.size() * 4, hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipMemcpyAsync(out.data(), dout.p, out.size() * 4, hipMemcpyDeviceToHost, st));
   HIP_CHECK(hipStreamSynchronize(st));
 }
 

@@ -498,36 +498,28 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
   for (int q = 0; q < nq; q++) qidx[q] = ch.sample_bits(Lmax);
 
   // ---- query openings: gather every opened word in proof order
-  std::vector<uint64_t> addrs;
-  auto push_digest = [&](const uint32_t* d) {
-    for (int e = 0; e < 8; e++) addrs.push_back((uint64_t)(uintptr_t)(d + e));
-  };
+  // Opening segments in serialization order (same for every query; see GatherSeg).
+  std::vector<GatherSeg> segs;
   const int ncommit = (int)trees.size();
-  for (int q = 0; q < nq; q++) {
-    const size_t index = qidx[q];
-    for (int r = 0; r < 4; r++) {
-      const Round& R = *rounds[r];
-      const int lrm = (int)R.tree.layers.size() - 1;
-      const size_t ri = index >> (Lmax - lrm);
-      for (const CMat& m : R.mats) {
-        const int lh = log2i(m.lde.height);
-        const size_t row = ri >> (lrm - lh);
-        for (int c = 0; c < m.lde.width; c++)
-          addrs.push_back((uint64_t)(uintptr_t)(m.lde.buf.p + (size_t)c * m.lde.height + row));
-      }
-      for (int L = 0; L < lrm; L++) push_digest(R.tree.layers[L].p + 8 * ((ri >> L) ^ 1));
+  for (int r = 0; r < 4; r++) {
+    const Round& R = *rounds[r];
+    const int lrm = (int)R.tree.layers.size() - 1;
+    for (const CMat& m : R.mats) {  // row (index >> (Lmax - lh)) of every column
+      const int lh = log2i(m.lde.height);
+      segs.push_back({m.lde.buf.p, (uint64_t)m.lde.height, (uint32_t)(Lmax - lh), 0, 1,
+                      (uint32_t)m.lde.width});
     }
-    for (int i = 0; i < ncommit; i++) {
-      const size_t ii = index >> i;
-      const uint32_t* sib = (const uint32_t*)(layers[i].p + (ii ^ 1));
-      for (int e = 0; e < 4; e++) addrs.push_back((uint64_t)(uintptr_t)(sib + e));
-      const size_t pair = ii >> 1;
-      const int lm = (int)trees[i].layers.size() - 1;
-      for (int L = 0; L < lm; L++) push_digest(trees[i].layers[L].p + 8 * ((pair >> L) ^ 1));
-    }
+    for (int L = 0; L < lrm; L++)  // sibling digest at layer L
+      segs.push_back({R.tree.layers[L].p, 1, (uint32_t)(Lmax - lrm + L), 1, 8, 8});
+  }
+  for (int i = 0; i < ncommit; i++) {
+    segs.push_back({(const uint32_t*)layers[i].p, 1, (uint32_t)i, 1, 4, 4});  // sibling EF
+    const int lm = (int)trees[i].layers.size() - 1;
+    for (int L = 0; L < lm; L++)
+      segs.push_back({trees[i].layers[L].p, 1, (uint32_t)(i + 1 + L), 1, 8, 8});
   }
   std::vector<uint32_t> words;
-  gather_words(addrs, words, st);
+  gather_queries(segs, qidx, words, st);
   if (ev.on) ev.end(e4, st, &tms->fri);
 
   // ---- serialize (BFZ1 normal form)
