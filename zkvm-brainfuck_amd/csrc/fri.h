@@ -37,6 +37,13 @@ void reduce_height(const std::vector<RedCol>& cols, const std::vector<RedMat>& m
 void fri_fold(const kb::EF* in, kb::EF* out, size_t h, const kb::EF& beta, const kb::EF* add,
               hipStream_t st);
 uint32_t grind(const GrindState& gs, int bits, hipStream_t st);
+// One FRI commit-phase transcript step on the device (DuplexChallenger with an empty input
+// buffer): observe the 8-word root, duplex, sample an EF (pops out[7], out[6], out[5], out[4]).
+// state: 16 words (Montgomery), updated in place; beta: EF written for the fold.
+void fri_challenge(uint32_t* state, const uint32_t* root, kb::EF* beta, hipStream_t st);
+// Fold with beta read from device memory.
+void fri_fold_dev(const kb::EF* in, kb::EF* out, size_t h, const kb::EF* beta, const kb::EF* add,
+                  hipStream_t st);
 // Query openings: word k of segment s for query index I is
 //   base[((I >> shift) ^ xr) * unit + k * stride],  k < count
 // (matrix rows: unit 1, stride = height; Merkle siblings: unit 8; FRI siblings: unit 4).

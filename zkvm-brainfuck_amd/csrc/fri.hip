@@ -230,6 +230,37 @@ __global__ __launch_bounds__(256) void k_fri_fold(const EF* __restrict__ in, EF*
   out[i] = r;
 }
 
+__global__ __launch_bounds__(256) void k_fri_fold_dev(const EF* __restrict__ in,
+                                                      EF* __restrict__ out, size_t h, int logh,
+                                                      const EF* __restrict__ beta,
+                                                      const uint32_t* __restrict__ twi,
+                                                      const EF* __restrict__ add) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= h) return;
+  const uint32_t halfv = to_mont_c((P + 1) / 2);
+  const EF half_beta = ef_mul_base(*beta, halfv);
+  const uint32_t g = twi[h + dbitrev((uint32_t)i, logh)];
+  const EF p = ef_mul_base(half_beta, g);
+  const EF lo = in[2 * i], hi = in[2 * i + 1];
+  EF r = ef_add(ef_mul(ef_add_base(p, halfv), lo), ef_mul(ef_sub(ef_base(halfv), p), hi));
+  if (add) r = ef_add(r, add[i]);
+  out[i] = r;
+}
+
+// One 16-lane row: lane l holds state word l (lane-mode permutation).
+__global__ __launch_bounds__(64) void k_fri_challenge(uint32_t* __restrict__ state,
+                                                      const uint32_t* __restrict__ root,
+                                                      EF* __restrict__ beta) {
+  const int lane = threadIdx.x & 15;
+  const bool row0 = threadIdx.x < 16;
+  uint32_t v = lane < 8 ? root[lane] : state[lane];
+  v = poseidon2_permute_lane(v, lane);
+  if (row0) {
+    state[lane] = v;
+    if (lane >= 4 && lane < 8) beta->c[7 - lane] = v;
+  }
+}
+
 // ------------------------------------------------------------------ grind
 // Challenger state: sponge state st[16], pending inputs in[0..nin).  observe(w) then
 // sample_bits(bits) == 0  <=>  perm(st with in[0..nin), w written at 0..nin)[7] low bits 0.
@@ -315,6 +346,19 @@ void fri_fold(const EF* in, EF* out, size_t h, const EF& beta, const EF* add, hi
   const EF half_beta = ef_mul_base(beta, to_mont_c((P + 1) / 2));
   hipLaunchKernelGGL(k_fri_fold, dim3(ceil_div(h, 256)), dim3(256), 0, st, in, out, h, logh,
                      half_beta, (const uint32_t*)twiddles().inv.p, add);
+  KCHECK();
+}
+
+void fri_challenge(uint32_t* state, const uint32_t* root, EF* beta, hipStream_t st) {
+  hipLaunchKernelGGL(k_fri_challenge, dim3(1), dim3(64), 0, st, state, root, beta);
+  KCHECK();
+}
+
+void fri_fold_dev(const EF* in, EF* out, size_t h, const EF* beta, const EF* add, hipStream_t st) {
+  const int logh = log2i(h);
+  twiddles().ensure(logh + 1);
+  hipLaunchKernelGGL(k_fri_fold_dev, dim3(ceil_div(h, 256)), dim3(256), 0, st, in, out, h, logh,
+                     beta, (const uint32_t*)twiddles().inv.p, add);
   KCHECK();
 }
 

@@ -32,7 +32,8 @@ void poseidon2_batch_small(uint32_t* states, size_t n, hipStream_t st);
 // Hash of 8-element rows (FRI commit-phase leaves: pairs of EF values), one permutation each.
 void hash_rows8(const uint32_t* rows, size_t n, uint32_t* digests, hipStream_t st);
 
-// Digest layers above an existing leaf layer (no injection).
-void merkle_layers_from_leaves(MerkleTree& tree, hipStream_t st);
+// Digest layers above an existing leaf layer (no injection).  With fetch_root = false the
+// root stays on the device (tree.layers.back()) and tree.root is not filled.
+void merkle_layers_from_leaves(MerkleTree& tree, hipStream_t st, bool fetch_root = true);
 
 }  // namespace bfz

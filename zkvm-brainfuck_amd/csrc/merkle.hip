@@ -243,7 +243,7 @@ static ColList make_cols(const std::vector<const MatRef*>& ms) {
 // Layers 1..nl above layers[0]; sorted[next..] are the matrices still to inject (heights
 // descending).  Big layers get one launch each; the rest go to k_compress_top in one launch.
 static void build_layers(MerkleTree& t, size_t len, const std::vector<const MatRef*>& sorted,
-                         size_t next, hipStream_t st) {
+                         size_t next, hipStream_t st, bool fetch_root = true) {
   const int nl = log2i(len);
   int L = 1;
   for (; L <= nl && (len >> 1) > (size_t)TOP_NODES; L++) {
@@ -280,6 +280,7 @@ static void build_layers(MerkleTree& t, size_t len, const std::vector<const MatR
     KCHECK();
   }
   if (next != sorted.size()) throw std::runtime_error("merkle: non power-of-two heights");
+  if (!fetch_root) return;
   HIP_CHECK(hipMemcpyAsync(t.root, t.layers[nl].p, 32, hipMemcpyDeviceToHost, st));
   HIP_CHECK(hipStreamSynchronize(st));
 }
@@ -304,10 +305,10 @@ void merkle_build(const std::vector<MatRef>& mats, MerkleTree& t, hipStream_t st
   build_layers(t, h0, sorted, next, st);
 }
 
-void merkle_layers_from_leaves(MerkleTree& t, hipStream_t st) {
+void merkle_layers_from_leaves(MerkleTree& t, hipStream_t st, bool fetch_root) {
   const size_t len = t.mats.empty() ? 0 : t.mats[0].height;
   t.layers.resize(log2i(len) + 1);
-  build_layers(t, len, {}, 0, st);
+  build_layers(t, len, {}, 0, st, fetch_root);
 }
 
 void poseidon2_batch(uint32_t* states, size_t n, hipStream_t st) {

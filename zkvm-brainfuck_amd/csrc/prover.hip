@@ -462,8 +462,16 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
   std::vector<MerkleTree> trees;
   layers.push_back(std::move(ro.at(Lmax)));
   ro.erase(Lmax);
+  // The transcript steps of the rounds run on the device (fri_challenge): the input buffer is
+  // empty here (fri_alpha was just sampled), so each round is observe(root) -> one duplex ->
+  // beta = 4 pops, and no host round trip is needed until the final polynomial.
+  if (ch.nin != 0) throw std::runtime_error("FRI: unexpected pending challenger input");
+  DBuf<uint32_t> dstate(16);
+  HIP_CHECK(hipMemcpyAsync(dstate.p, ch.st, 64, hipMemcpyHostToDevice, st));
+  const int nrounds = Lmax - LOG_BLOWUP;
+  DBuf<EF> betas(std::max(nrounds, 1));
   size_t len = (size_t)1 << Lmax;
-  while (len > ((size_t)1 << LOG_BLOWUP)) {
+  for (int rd = 0; len > ((size_t)1 << LOG_BLOWUP); rd++) {
     const size_t h = len / 2;
     trees.emplace_back();
     MerkleTree& t = trees.back();
@@ -471,19 +479,28 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
     t.layers.clear();
     t.layers.emplace_back(8 * h);
     hash_rows8((const uint32_t*)layers.back().p, h, t.layers[0].p, st);
-    merkle_layers_from_leaves(t, st);
-    ch.observe_digest(t.root);
-    const EF beta = ch.sample_ef();
+    merkle_layers_from_leaves(t, st, /*fetch_root=*/false);
+    fri_challenge(dstate.p, t.layers.back().p, betas.p + rd, st);
     DBuf<EF> next(h);
     const int lgh = log2i(h);
     const EF* add = ro.count(lgh) ? ro.at(lgh).p : nullptr;
-    fri_fold(layers.back().p, next.p, h, beta, add, st);
+    fri_fold_dev(layers.back().p, next.p, h, betas.p + rd, add, st);
     layers.push_back(std::move(next));
     len = h;
   }
+  for (MerkleTree& t : trees)
+    HIP_CHECK(hipMemcpyAsync(t.root, t.layers.back().p, 32, hipMemcpyDeviceToHost, st));
+  uint32_t st_after[16];
+  HIP_CHECK(hipMemcpyAsync(st_after, dstate.p, 64, hipMemcpyDeviceToHost, st));
   EF fin[2];
   HIP_CHECK(hipMemcpyAsync(fin, layers.back().p, 2 * sizeof(EF), hipMemcpyDeviceToHost, st));
   HIP_CHECK(hipStreamSynchronize(st));
+  if (!trees.empty()) {  // host challenger = state after the last round's duplex, 4 outputs left
+    for (int i = 0; i < 16; i++) ch.st[i] = st_after[i];
+    for (int i = 0; i < 8; i++) ch.out[i] = st_after[i];
+    ch.nout = 4;
+    ch.nin = 0;
+  }
   if (!ef_eq(fin[0], fin[1]))
     throw std::runtime_error("FRI: final polynomial is not constant (trace violates the AIR)");
   ch.observe_ef(fin[0]);
