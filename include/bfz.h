@@ -95,6 +95,18 @@ int bfz_record_prove(const bfz_pk* pk, const bfz_record* rec, uint8_t** proof, s
                      bfz_timings* timings);
 void bfz_record_free(bfz_record* rec);
 
+/* One proof sharded over `world` GPUs (one process per GPU, every rank calls this with the
+ * same record): each rank hashes its subtree of every large Merkle tree (the commits and the
+ * FRI commit phase, crates/stark/src/prover.rs:209-236,460-470); the ranks exchange subtree
+ * roots and query openings through the callbacks (torch.distributed / RCCL on the host
+ * side).  Every rank returns the same proof, byte-identical to bfz_record_prove's.  The
+ * callbacks return 0 on success. */
+typedef int (*bfz_allgather_fn)(void* ctx, const void* send, size_t bytes, void* recv);
+typedef int (*bfz_allreduce_u32_fn)(void* ctx, uint32_t* data, size_t n);
+int bfz_record_prove_sharded(const bfz_pk* pk, const bfz_record* rec, int rank, int world,
+                             bfz_allgather_fn allgather, bfz_allreduce_u32_fn allreduce_sum,
+                             void* ctx, uint8_t** proof, size_t* proof_len, bfz_timings* timings);
+
 int bfz_set_num_queries(int num_queries); /* FRI_QUERIES (kb31_poseidon2.rs:59-62) */
 
 int bfz_coset_lde(const uint32_t* evals, size_t n, size_t w, uint32_t shift, uint32_t* lde_out);

@@ -1,0 +1,11 @@
+# Multi-rank rehearsal on a one-GPU box: both bench modes with 2 ranks pinned to GPU 0
+# (timings are not scaling numbers -- the ranks share one GPU).
+export TMPDIR=/tmp
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+for mode in replicas sharded; do
+  BFZ_DEVICE=0 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+    --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 1 \
+    --no-cpu-baseline --mode $mode > gpurun_out/rehearsal_$mode.json 2> gpurun_out/rehearsal_$mode.err || exit $?
+done
+echo "exit 0"

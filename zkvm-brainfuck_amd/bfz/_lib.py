@@ -31,6 +31,10 @@ class Timings(ctypes.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+# collective callbacks of bfz_record_prove_sharded (bfz_allgather_fn / bfz_allreduce_u32_fn)
+ALLGATHER_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_void_p, c_size_t, c_void_p)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, c_void_p, POINTER(c_uint32), c_size_t)
+
 # (name, restype, argtypes) for every symbol declared in include/bfz.h
 SIGNATURES = [
     ("bfz_init", c_int, [c_int]),
@@ -57,6 +61,9 @@ SIGNATURES = [
     ("bfz_record_prove", c_int, [c_void_p, c_void_p, POINTER(POINTER(c_uint8)), POINTER(c_size_t),
                                  POINTER(Timings)]),
     ("bfz_record_free", None, [c_void_p]),
+    ("bfz_record_prove_sharded", c_int, [c_void_p, c_void_p, c_int, c_int, ALLGATHER_FN,
+                                         ALLREDUCE_FN, c_void_p, POINTER(POINTER(c_uint8)),
+                                         POINTER(c_size_t), POINTER(Timings)]),
     ("bfz_set_num_queries", c_int, [c_int]),
     ("bfz_coset_lde", c_int, [POINTER(c_uint32), c_size_t, c_size_t, c_uint32, POINTER(c_uint32)]),
     ("bfz_commit", c_int, [POINTER(POINTER(c_uint32)), POINTER(c_size_t), POINTER(c_size_t),

@@ -1,0 +1,79 @@
+"""One core proof sharded over the ranks of a torch.distributed group.
+
+Every rank holds the same record and proving key; bfz_record_prove_sharded hashes this
+rank's subtree of every large Merkle tree and calls back here for the two exchanges: an
+all-gather of subtree roots and a sum all-reduce of the owner-masked query openings.  With the
+nccl backend (RCCL on ROCm) the exchanged buffers travel as device tensors over xGMI; with
+gloo they stay on the host (used by the tests, which run several ranks on one GPU).
+"""
+from __future__ import annotations
+
+import ctypes
+import traceback
+
+import numpy as np
+
+from . import _lib
+
+
+class Collectives:
+    """ctypes callbacks over a torch.distributed process group."""
+
+    def __init__(self, dist, group=None, device=None):
+        import torch
+        self.dist, self.group, self.torch = dist, group, torch
+        self.world = dist.get_world_size(group)
+        backend = str(dist.get_backend(group)).lower()
+        self.dev = (torch.device("cuda", device if device is not None else 0)
+                    if "nccl" in backend else torch.device("cpu"))
+        self.allgather = _lib.ALLGATHER_FN(self._allgather)
+        self.allreduce = _lib.ALLREDUCE_FN(self._allreduce)
+
+    def _allgather(self, _ctx, send, nbytes, recv):
+        try:
+            torch = self.torch
+            buf = (ctypes.c_uint8 * nbytes).from_address(send)
+            t = torch.frombuffer(bytearray(buf), dtype=torch.uint8).to(self.dev)
+            parts = [torch.empty_like(t) for _ in range(self.world)]
+            self.dist.all_gather(parts, t, group=self.group)
+            out = torch.cat(parts).cpu().numpy()
+            ctypes.memmove(recv, out.ctypes.data, out.nbytes)
+            return 0
+        except Exception:  # noqa: BLE001 - reported to the C side as a failed collective
+            traceback.print_exc()
+            return 1
+
+    def _allreduce(self, _ctx, data, n):
+        try:
+            torch = self.torch
+            arr = np.ctypeslib.as_array(data, shape=(n,))
+            # exactly one rank contributes each word (< 2^31): an int32 sum is exact
+            t = torch.from_numpy(arr.view(np.int32).copy()).to(self.dev)
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
+            arr[:] = t.cpu().numpy().view(np.uint32)
+            return 0
+        except Exception:  # noqa: BLE001
+            traceback.print_exc()
+            return 1
+
+
+def prove_record_sharded(pk_handle, rec, coll: Collectives, rank: int, timings=None) -> bytes:
+    """bfz_record_prove_sharded for this rank; returns the (rank-independent) proof bytes."""
+    L = _lib.lib()
+    ptr = ctypes.POINTER(ctypes.c_uint8)()
+    plen = ctypes.c_size_t()
+    _lib.check(L.bfz_record_prove_sharded(
+        ctypes.c_void_p(pk_handle), rec, rank, coll.world, coll.allgather, coll.allreduce, None,
+        ctypes.byref(ptr), ctypes.byref(plen), ctypes.byref(timings) if timings else None))
+    return _lib.take_bytes(ptr, plen.value)
+
+
+def new_record(pk_handle, stdin: bytes):
+    """bfz_record_new: execute + upload the events (the proof's inputs) to this rank's GPU."""
+    L = _lib.lib()
+    rec = ctypes.c_void_p()
+    cycles = ctypes.c_uint64()
+    buf, n = _lib.u8buf(bytes(stdin))
+    _lib.check(L.bfz_record_new(ctypes.c_void_p(pk_handle), buf, n, ctypes.byref(rec),
+                                ctypes.byref(cycles)))
+    return rec, cycles.value

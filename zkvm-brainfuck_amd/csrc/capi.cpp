@@ -221,6 +221,29 @@ int bfz_record_new(const bfz_pk* pk, const uint8_t* in, size_t nin, bfz_record**
   });
 }
 
+namespace {
+void fill_timings(const bfz::StageTimes& st, bfz_timings* t) {
+  if (!t) return;
+  t->trace_ms = st.trace;
+  t->main_commit_ms = st.main_commit;
+  t->perm_ms = st.perm;
+  t->quotient_ms = st.quotient;
+  t->open_ms = st.open;
+  t->fri_ms = st.fri;
+  t->total_ms = st.total;
+  t->lde_ms = st.lde_ms;
+  t->lde_bytes = st.lde_bytes;
+  t->lde_calls = st.lde_calls;
+  t->ntt_kernel_ms = st.ntt_kernel_ms;
+  t->ntt_kernel_bytes = st.ntt_kernel_bytes;
+  t->ntt_kernel_launches = st.ntt_kernel_launches;
+}
+struct ShardScope {  // installs the shard context for one proof
+  explicit ShardScope(bfz::ShardCtx* c) { bfz::shard_ctx() = c; }
+  ~ShardScope() { bfz::shard_ctx() = nullptr; }
+};
+}  // namespace
+
 int bfz_record_prove(const bfz_pk* pk, const bfz_record* rec, uint8_t** proof, size_t* len,
                      bfz_timings* t) {
   return guarded([&] {
@@ -228,21 +251,34 @@ int bfz_record_prove(const bfz_pk* pk, const bfz_record* rec, uint8_t** proof, s
     o.timing = t != nullptr;
     bfz::StageTimes st;
     auto v = bfz::prove_events(*pk->pk, rec->ev, o, &st);
-    if (t) {
-      t->trace_ms = st.trace;
-      t->main_commit_ms = st.main_commit;
-      t->perm_ms = st.perm;
-      t->quotient_ms = st.quotient;
-      t->open_ms = st.open;
-      t->fri_ms = st.fri;
-      t->total_ms = st.total;
-      t->lde_ms = st.lde_ms;
-      t->lde_bytes = st.lde_bytes;
-      t->lde_calls = st.lde_calls;
-      t->ntt_kernel_ms = st.ntt_kernel_ms;
-      t->ntt_kernel_bytes = st.ntt_kernel_bytes;
-      t->ntt_kernel_launches = st.ntt_kernel_launches;
-    }
+    fill_timings(st, t);
+    return emit(std::move(v), proof, len);
+  });
+}
+
+int bfz_record_prove_sharded(const bfz_pk* pk, const bfz_record* rec, int rank, int world,
+                             bfz_allgather_fn allgather, bfz_allreduce_u32_fn allreduce_sum,
+                             void* ctx, uint8_t** proof, size_t* len, bfz_timings* t) {
+  return guarded([&] {
+    if (world < 1 || rank < 0 || rank >= world || (world & (world - 1)))
+      throw std::runtime_error("sharded prove: world must be a power of two, 0 <= rank < world");
+    if (world > 1 && (!allgather || !allreduce_sum))
+      throw std::runtime_error("sharded prove: collectives required");
+    bfz::ShardCtx c;
+    c.rank = rank;
+    c.world = world;
+    c.allgather = [&](const void* send, size_t bytes, void* recv) {
+      if (allgather(ctx, send, bytes, recv)) throw std::runtime_error("allgather callback failed");
+    };
+    c.allreduce_sum_u32 = [&](uint32_t* data, size_t n) {
+      if (allreduce_sum(ctx, data, n)) throw std::runtime_error("allreduce callback failed");
+    };
+    ShardScope scope(&c);
+    bfz::ProveOptions o = opts();
+    o.timing = t != nullptr;
+    bfz::StageTimes st;
+    auto v = bfz::prove_events(*pk->pk, rec->ev, o, &st);
+    fill_timings(st, t);
     return emit(std::move(v), proof, len);
   });
 }

@@ -47,13 +47,19 @@ void fri_fold_dev(const kb::EF* in, kb::EF* out, size_t h, const kb::EF* beta, c
 // Query openings: word k of segment s for query index I is
 //   base[((I >> shift) ^ xr) * unit + k * stride],  k < count
 // (matrix rows: unit 1, stride = height; Merkle siblings: unit 8; FRI siblings: unit 4).
+// When the tree is sharded, word k of a segment is owned by rank (element >> own_shift)
+// (own_shift < 0: replicated data, owned by rank 0); other ranks write 0 and the ranks' words
+// are summed.
 struct GatherSeg {
   const uint32_t* base;
   uint64_t stride;
   uint32_t shift, xr, unit, count;
+  int32_t own_shift;
+  int32_t pad;
 };
-// out[q * words_per_query + ...] = the segments' words for qidx[q], segments in order.
+// out[q * words_per_query + ...] = the segments' words for qidx[q], segments in order
+// (this rank's share when rank/world describe a sharded proof).
 void gather_queries(const std::vector<GatherSeg>& segs, const std::vector<uint32_t>& qidx,
-                    std::vector<uint32_t>& out, hipStream_t st);
+                    std::vector<uint32_t>& out, int rank, hipStream_t st);
 
 }  // namespace bfz

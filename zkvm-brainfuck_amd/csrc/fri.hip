@@ -288,14 +288,16 @@ __global__ __launch_bounds__(256) void k_gather_segs(const GatherSeg* __restrict
                                                      const uint32_t* __restrict__ seg_off,
                                                      uint32_t words_per_q,
                                                      const uint32_t* __restrict__ qidx, int nq,
-                                                     uint32_t* __restrict__ out) {
+                                                     int rank, uint32_t* __restrict__ out) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (size_t)nseg * nq) return;
   const int q = (int)(t / nseg), s = (int)(t % nseg);
   const GatherSeg g = segs[s];
-  const uint64_t pos = (uint64_t)((qidx[q] >> g.shift) ^ g.xr) * g.unit;
+  const uint32_t e = (qidx[q] >> g.shift) ^ g.xr;
+  const int owner = g.own_shift >= 0 ? (int)(e >> g.own_shift) : 0;
+  const uint64_t pos = (uint64_t)e * g.unit;
   uint32_t* o = out + (size_t)q * words_per_q + seg_off[s];
-  for (uint32_t k = 0; k < g.count; k++) o[k] = g.base[pos + k * g.stride];
+  for (uint32_t k = 0; k < g.count; k++) o[k] = owner == rank ? g.base[pos + k * g.stride] : 0u;
 }
 
 // ================================================================== host wrappers
@@ -382,7 +384,7 @@ uint32_t grind(const GrindState& gs, int bits, hipStream_t st) {
 }
 
 void gather_queries(const std::vector<GatherSeg>& segs, const std::vector<uint32_t>& qidx,
-                    std::vector<uint32_t>& out, hipStream_t st) {
+                    std::vector<uint32_t>& out, int rank, hipStream_t st) {
   std::vector<uint32_t> off(segs.size());
   uint32_t wpq = 0;
   for (size_t s = 0; s < segs.size(); s++) {
@@ -400,7 +402,7 @@ void gather_queries(const std::vector<GatherSeg>& segs, const std::vector<uint32
   const size_t nthreads = segs.size() * qidx.size();
   hipLaunchKernelGGL(k_gather_segs, dim3(ceil_div(nthreads, 256)), dim3(256), 0, st,
                      (const GatherSeg*)dseg.p, (int)segs.size(), (const uint32_t*)doff.p, wpq,
-                     (const uint32_t*)dq.p, (int)qidx.size(), dout.p);
+                     (const uint32_t*)dq.p, (int)qidx.size(), rank, dout.p);
   KCHECK();
   HIP_CHECK(hipMemcpyAsync(out.data(), dout.p, out.size() * 4, hipMemcpyDeviceToHost, st));
   HIP_CHECK(hipStreamSynchronize(st));

@@ -1,6 +1,7 @@
 // Poseidon2 Merkle commitment on the device: MerkleTreeMmcs<.., PaddingFreeSponge<Perm,16,8,8>,
 // TruncatedPermutation<Perm,2,8,16>, 8> (crates/stark/src/kb31_poseidon2.rs:24-28).
 #pragma once
+#include <functional>
 #include <vector>
 
 #include "gpu.h"
@@ -17,8 +18,23 @@ struct MerkleTree {
   std::vector<DBuf<uint32_t>> layers;  // layers[L]: (max_height >> L) digests x 8 (Montgomery)
   std::vector<MatRef> mats;            // committed matrices in commit order
   uint32_t root[8];                    // Montgomery form
+  int sharded_below = 0;               // layers [0, sharded_below) hold only this rank's range
+  int shard_log = 0;                   // log2(world) when sharded
   size_t max_height() const { return mats.empty() ? 0 : ((size_t)1 << (layers.size() - 1)); }
 };
+
+// Multi-GPU sharding of the Merkle trees of one proof.  While a context
+// is installed (shard_ctx() != nullptr, world > 1), trees with at least world *
+// SHARD_MIN_LEAVES leaves are built as one subtree per rank plus redundant top layers.
+struct ShardCtx {
+  int rank = 0, world = 1;
+  // all-gather `bytes` from every rank into recv (world * bytes, rank order)
+  std::function<void(const void* send, size_t bytes, void* recv)> allgather;
+  // element-wise sum over ranks, in place
+  std::function<void(uint32_t* data, size_t n)> allreduce_sum_u32;
+};
+constexpr size_t SHARD_MIN_LEAVES = 1024;
+ShardCtx*& shard_ctx();
 
 // Builds the tree (heights must be powers of two) and copies the root to the host.
 void merkle_build(const std::vector<MatRef>& mats, MerkleTree& tree, hipStream_t st);
@@ -29,11 +45,10 @@ void poseidon2_batch(uint32_t* states, size_t n, hipStream_t st);
 // Same, latency-optimised (16 lanes per state; for few states).
 void poseidon2_batch_small(uint32_t* states, size_t n, hipStream_t st);
 
-// Hash of 8-element rows (FRI commit-phase leaves: pairs of EF values), one permutation each.
-void hash_rows8(const uint32_t* rows, size_t n, uint32_t* digests, hipStream_t st);
-
-// Digest layers above an existing leaf layer (no injection).  With fetch_root = false the
-// root stays on the device (tree.layers.back()) and tree.root is not filled.
-void merkle_layers_from_leaves(MerkleTree& tree, hipStream_t st, bool fetch_root = true);
+// Tree over h rows of 8 elements (FRI commit-phase leaves: pairs of EF values, one
+// permutation each).  With fetch_root = false the root stays on the device
+// (tree.layers.back()) and tree.root is not filled.
+void merkle_from_rows8(MerkleTree& tree, const uint32_t* rows, size_t h, hipStream_t st,
+                       bool fetch_root = true);
 
 }  // namespace bfz

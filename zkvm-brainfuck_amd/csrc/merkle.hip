@@ -28,10 +28,12 @@ __device__ __forceinline__ void sponge_cols(uint32_t st[16], const ColList& cl, 
   }
 }
 
-__global__ __launch_bounds__(256) void k_hash_leaves(ColList cl, size_t height,
+// Rows [r0, r0 + count) (a shard's range; the whole matrix when unsharded).
+__global__ __launch_bounds__(256) void k_hash_leaves(ColList cl, size_t r0, size_t count,
                                                      uint32_t* __restrict__ out) {
-  const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= height) return;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const size_t r = r0 + i;
   uint32_t st[16];
 #pragma unroll
   for (int i = 0; i < 16; i++) st[i] = 0;
@@ -89,10 +91,13 @@ __device__ __forceinline__ void store8(uint32_t* p, const uint32_t st[16]) {
   o[1] = make_uint4(st[4], st[5], st[6], st[7]);
 }
 
-__global__ __launch_bounds__(256) void k_compress(const uint32_t* __restrict__ prev, size_t nlen,
-                                                  uint32_t* __restrict__ out, ColList inj) {
-  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= nlen) return;
+// Nodes [j0, j0 + count) of a layer.
+__global__ __launch_bounds__(256) void k_compress(const uint32_t* __restrict__ prev, size_t j0,
+                                                  size_t count, uint32_t* __restrict__ out,
+                                                  ColList inj) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const size_t j = j0 + i;
   uint32_t st[16];
   load16(st, prev + 16 * j);
   merkle_node(st, inj, 0, inj.n, j);
@@ -175,20 +180,22 @@ __global__ __launch_bounds__(1024) void k_compress_top(const uint32_t* __restric
 // this size is one permutation latency long (~12 us) while 16 lanes per node finish sooner.
 constexpr size_t LANE_LAYER_MAX = (size_t)1 << 14;
 __global__ __launch_bounds__(256) void k_compress_lanes(const uint32_t* __restrict__ prev,
-                                                        size_t nlen, uint32_t* __restrict__ out,
-                                                        ColList inj) {
-  const size_t j = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+                                                        size_t j0, size_t count,
+                                                        uint32_t* __restrict__ out, ColList inj) {
+  const size_t i = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
   const int lane = threadIdx.x & 15;
-  if (j >= nlen) return;
+  if (i >= count) return;
+  const size_t j = j0 + i;
   const uint32_t v = merkle_node_lane(prev[16 * j + lane], inj, 0, inj.n, j, lane);
   if (lane < 8) out[8 * j + lane] = v;
 }
 
 __global__ __launch_bounds__(256) void k_hash_rows8_lanes(const uint32_t* __restrict__ rows,
-                                                          size_t n, uint32_t* __restrict__ out) {
-  const size_t i = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+                                                          size_t r0, size_t count,
+                                                          uint32_t* __restrict__ out) {
+  const size_t i = r0 + (((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4);
   const int lane = threadIdx.x & 15;
-  if (i >= n) return;
+  if (i >= r0 + count) return;
   const uint32_t v = poseidon2_permute_lane(lane < 8 ? rows[8 * i + lane] : 0u, lane);
   if (lane < 8) out[8 * i + lane] = v;
 }
@@ -212,10 +219,10 @@ __global__ __launch_bounds__(256) void k_permute_batch(uint32_t* __restrict__ s,
   for (int k = 0; k < 16; k++) s[16 * i + k] = st[k];
 }
 
-__global__ __launch_bounds__(256) void k_hash_rows8(const uint32_t* __restrict__ rows, size_t n,
-                                                    uint32_t* __restrict__ out) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+__global__ __launch_bounds__(256) void k_hash_rows8(const uint32_t* __restrict__ rows, size_t r0,
+                                                    size_t count, uint32_t* __restrict__ out) {
+  const size_t i = r0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= r0 + count) return;
   uint32_t st[16];
   const uint4* in = reinterpret_cast<const uint4*>(rows + 8 * i);
   uint4 a = in[0], b = in[1];
@@ -240,24 +247,32 @@ static ColList make_cols(const std::vector<const MatRef*>& ms) {
   return cl;
 }
 
-// Layers 1..nl above layers[0]; sorted[next..] are the matrices still to inject (heights
-// descending).  Big layers get one launch each; the rest go to k_compress_top in one launch.
-static void build_layers(MerkleTree& t, size_t len, const std::vector<const MatRef*>& sorted,
+// One layer's nodes [j0, j0 + count) from layers[L-1] (lane mode for small launches).
+static void launch_layer(MerkleTree& t, int L, size_t j0, size_t count,
+                         const std::vector<const MatRef*>& grp, hipStream_t st) {
+  const uint32_t* prev = t.layers[L - 1].p;
+  if (count <= LANE_LAYER_MAX)
+    hipLaunchKernelGGL(k_compress_lanes, dim3(ceil_div(16 * count, 256)), dim3(256), 0, st, prev,
+                       j0, count, t.layers[L].p, make_cols(grp));
+  else
+    hipLaunchKernelGGL(k_compress, dim3(ceil_div(count, 256)), dim3(256), 0, st, prev, j0, count,
+                       t.layers[L].p, make_cols(grp));
+  KCHECK();
+}
+
+// Layers L0..nl with layers[L0-1] (len nodes) complete; sorted[next..] are the matrices
+// still to inject (heights descending).  Big layers get one launch each; the rest go to
+// k_compress_top in one launch.
+static void build_layers(MerkleTree& t, int L0, size_t len, const std::vector<const MatRef*>& sorted,
                          size_t next, hipStream_t st, bool fetch_root = true) {
-  const int nl = log2i(len);
-  int L = 1;
+  const int nl = (int)t.layers.size() - 1;
+  int L = L0;
   for (; L <= nl && (len >> 1) > (size_t)TOP_NODES; L++) {
     const size_t nlen = len >> 1;
     std::vector<const MatRef*> grp;
     while (next < sorted.size() && sorted[next]->height == nlen) grp.push_back(sorted[next++]);
     t.layers[L].reset(8 * nlen);
-    if (nlen <= LANE_LAYER_MAX)
-      hipLaunchKernelGGL(k_compress_lanes, dim3(ceil_div(16 * nlen, 256)), dim3(256), 0, st,
-                         (const uint32_t*)t.layers[L - 1].p, nlen, t.layers[L].p, make_cols(grp));
-    else
-      hipLaunchKernelGGL(k_compress, dim3(ceil_div(nlen, 256)), dim3(256), 0, st,
-                         (const uint32_t*)t.layers[L - 1].p, nlen, t.layers[L].p, make_cols(grp));
-    KCHECK();
+    launch_layer(t, L, 0, nlen, grp, st);
     len = nlen;
   }
   if (L <= nl) {
@@ -285,6 +300,49 @@ static void build_layers(MerkleTree& t, size_t len, const std::vector<const MatR
   HIP_CHECK(hipStreamSynchronize(st));
 }
 
+// ------------------------------------------------------------------ sharded trees
+ShardCtx*& shard_ctx() {
+  static ShardCtx* c = nullptr;
+  return c;
+}
+
+static bool shard_tree(size_t h0) {
+  const ShardCtx* c = shard_ctx();
+  return c && c->world > 1 && h0 >= (size_t)c->world * SHARD_MIN_LEAVES;
+}
+
+// Rank k owns nodes [k len / G, (k+1) len / G) of every layer with len >= G nodes (one
+// subtree, injected rows included); the layer of G nodes is all-gathered and the layers above
+// it are built redundantly by every rank.  leaves(r0, count) hashes the rank's own rows.
+template <class Leaves>
+static void build_sharded(MerkleTree& t, size_t h0, const std::vector<const MatRef*>& sorted,
+                          size_t next, Leaves leaves, hipStream_t st, bool fetch_root) {
+  const ShardCtx& c = *shard_ctx();
+  const size_t G = (size_t)c.world, k = (size_t)c.rank;
+  const int nl = log2i(h0), lg = log2i(G);
+  t.sharded_below = nl - lg;  // layers [0, nl - lg) hold only this rank's range
+  t.shard_log = lg;
+  leaves(k * (h0 / G), h0 / G);
+  size_t len = h0;
+  for (int L = 1; L <= nl - lg; L++) {
+    const size_t nlen = len >> 1;
+    std::vector<const MatRef*> grp;
+    while (next < sorted.size() && sorted[next]->height == nlen) grp.push_back(sorted[next++]);
+    t.layers[L].reset(8 * nlen);
+    launch_layer(t, L, k * (nlen / G), nlen / G, grp, st);
+    len = nlen;
+  }
+  uint32_t mine[8];  // layer nl - lg has G nodes; node k is ours
+  std::vector<uint32_t> all(8 * G);
+  DBuf<uint32_t>& lay = t.layers[nl - lg];
+  HIP_CHECK(hipMemcpyAsync(mine, lay.p + 8 * k, 32, hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+  c.allgather(mine, 32, all.data());
+  HIP_CHECK(hipMemcpyAsync(lay.p, all.data(), all.size() * 4, hipMemcpyHostToDevice, st));
+  HIP_CHECK(hipStreamSynchronize(st));  // `all` goes out of scope
+  build_layers(t, nl - lg + 1, G, sorted, next, st, fetch_root);
+}
+
 void merkle_build(const std::vector<MatRef>& mats, MerkleTree& t, hipStream_t st) {
   if (mats.empty()) throw std::runtime_error("merkle: no matrices");
   t.mats = mats;
@@ -295,20 +353,52 @@ void merkle_build(const std::vector<MatRef>& mats, MerkleTree& t, hipStream_t st
   const size_t h0 = sorted[0]->height;
   t.layers.clear();
   t.layers.resize(log2i(h0) + 1);
+  t.sharded_below = 0;
   size_t next = 0;
   std::vector<const MatRef*> grp;
   while (next < sorted.size() && sorted[next]->height == h0) grp.push_back(sorted[next++]);
   t.layers[0].reset(8 * h0);
-  hipLaunchKernelGGL(k_hash_leaves, dim3(ceil_div(h0, 256)), dim3(256), 0, st, make_cols(grp), h0,
-                     t.layers[0].p);
-  KCHECK();
-  build_layers(t, h0, sorted, next, st);
+  const ColList cl = make_cols(grp);
+  auto leaves = [&](size_t r0, size_t count) {
+    hipLaunchKernelGGL(k_hash_leaves, dim3(ceil_div(count, 256)), dim3(256), 0, st, cl, r0,
+                       count, t.layers[0].p);
+    KCHECK();
+  };
+  if (shard_tree(h0)) {
+    build_sharded(t, h0, sorted, next, leaves, st, true);
+    return;
+  }
+  leaves(0, h0);
+  build_layers(t, 1, h0, sorted, next, st);
 }
 
-void merkle_layers_from_leaves(MerkleTree& t, hipStream_t st, bool fetch_root) {
-  const size_t len = t.mats.empty() ? 0 : t.mats[0].height;
-  t.layers.resize(log2i(len) + 1);
-  build_layers(t, len, {}, 0, st, fetch_root);
+static void hash_rows8_range(const uint32_t* rows, size_t r0, size_t count, uint32_t* digests,
+                             hipStream_t st) {
+  if (count <= LANE_LAYER_MAX)
+    hipLaunchKernelGGL(k_hash_rows8_lanes, dim3(ceil_div(16 * count, 256)), dim3(256), 0, st, rows,
+                       r0, count, digests);
+  else
+    hipLaunchKernelGGL(k_hash_rows8, dim3(ceil_div(count, 256)), dim3(256), 0, st, rows, r0, count,
+                       digests);
+  KCHECK();
+}
+
+void merkle_from_rows8(MerkleTree& t, const uint32_t* rows, size_t h, hipStream_t st,
+                       bool fetch_root) {
+  t.mats = {MatRef{rows, h, 8}};
+  t.layers.clear();
+  t.layers.resize(log2i(h) + 1);
+  t.layers[0].reset(8 * h);
+  t.sharded_below = 0;
+  auto leaves = [&](size_t r0, size_t count) {
+    hash_rows8_range(rows, r0, count, t.layers[0].p, st);
+  };
+  if (shard_tree(h)) {
+    build_sharded(t, h, {}, 0, leaves, st, fetch_root);
+    return;
+  }
+  leaves(0, h);
+  build_layers(t, 1, h, {}, 0, st, fetch_root);
 }
 
 void poseidon2_batch(uint32_t* states, size_t n, hipStream_t st) {
@@ -318,15 +408,6 @@ void poseidon2_batch(uint32_t* states, size_t n, hipStream_t st) {
 
 void poseidon2_batch_small(uint32_t* states, size_t n, hipStream_t st) {
   hipLaunchKernelGGL(k_permute_lanes, dim3(ceil_div(16 * n, 256)), dim3(256), 0, st, states, n);
-  KCHECK();
-}
-
-void hash_rows8(const uint32_t* rows, size_t n, uint32_t* digests, hipStream_t st) {
-  if (n <= LANE_LAYER_MAX)
-    hipLaunchKernelGGL(k_hash_rows8_lanes, dim3(ceil_div(16 * n, 256)), dim3(256), 0, st, rows, n,
-                       digests);
-  else
-    hipLaunchKernelGGL(k_hash_rows8, dim3(ceil_div(n, 256)), dim3(256), 0, st, rows, n, digests);
   KCHECK();
 }
 

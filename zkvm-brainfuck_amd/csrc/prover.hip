@@ -475,11 +475,7 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
     const size_t h = len / 2;
     trees.emplace_back();
     MerkleTree& t = trees.back();
-    t.mats = {MatRef{(const uint32_t*)layers.back().p, h, 8}};
-    t.layers.clear();
-    t.layers.emplace_back(8 * h);
-    hash_rows8((const uint32_t*)layers.back().p, h, t.layers[0].p, st);
-    merkle_layers_from_leaves(t, st, /*fetch_root=*/false);
+    merkle_from_rows8(t, (const uint32_t*)layers.back().p, h, st, /*fetch_root=*/false);
     fri_challenge(dstate.p, t.layers.back().p, betas.p + rd, st);
     DBuf<EF> next(h);
     const int lgh = log2i(h);
@@ -516,6 +512,10 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
 
   // ---- query openings: gather every opened word in proof order
   // Opening segments in serialization order (same for every query; see GatherSeg).
+  auto owner_shift = [](const MerkleTree& t, int L) {  // layer L of a sharded tree
+    const int nl = (int)t.layers.size() - 1;
+    return L < t.sharded_below ? nl - L - t.shard_log : -1;
+  };
   std::vector<GatherSeg> segs;
   const int ncommit = (int)trees.size();
   for (int r = 0; r < 4; r++) {
@@ -524,19 +524,23 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
     for (const CMat& m : R.mats) {  // row (index >> (Lmax - lh)) of every column
       const int lh = log2i(m.lde.height);
       segs.push_back({m.lde.buf.p, (uint64_t)m.lde.height, (uint32_t)(Lmax - lh), 0, 1,
-                      (uint32_t)m.lde.width});
+                      (uint32_t)m.lde.width, -1, 0});
     }
     for (int L = 0; L < lrm; L++)  // sibling digest at layer L
-      segs.push_back({R.tree.layers[L].p, 1, (uint32_t)(Lmax - lrm + L), 1, 8, 8});
+      segs.push_back({R.tree.layers[L].p, 1, (uint32_t)(Lmax - lrm + L), 1, 8, 8,
+                      owner_shift(R.tree, L), 0});
   }
   for (int i = 0; i < ncommit; i++) {
-    segs.push_back({(const uint32_t*)layers[i].p, 1, (uint32_t)i, 1, 4, 4});  // sibling EF
+    segs.push_back({(const uint32_t*)layers[i].p, 1, (uint32_t)i, 1, 4, 4, -1, 0});  // sibling EF
     const int lm = (int)trees[i].layers.size() - 1;
     for (int L = 0; L < lm; L++)
-      segs.push_back({trees[i].layers[L].p, 1, (uint32_t)(i + 1 + L), 1, 8, 8});
+      segs.push_back({trees[i].layers[L].p, 1, (uint32_t)(i + 1 + L), 1, 8, 8,
+                      owner_shift(trees[i], L), 0});
   }
   std::vector<uint32_t> words;
-  gather_queries(segs, qidx, words, st);
+  const ShardCtx* shard = shard_ctx();
+  gather_queries(segs, qidx, words, shard ? shard->rank : 0, st);
+  if (shard && shard->world > 1) shard->allreduce_sum_u32(words.data(), words.size());
   if (ev.on) ev.end(e4, st, &tms->fri);
 
   // ---- serialize (BFZ1 normal form)
