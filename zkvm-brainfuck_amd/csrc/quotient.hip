@@ -22,17 +22,43 @@ constexpr int QMAIN_W[NUM_CHIPS] = {31, 1, 7, 45, 12, 2, 41, 5};
 constexpr int QPREP_W[NUM_CHIPS] = {0, 6, 0, 0, 0, 2, 0, 0};
 constexpr int QPERM_W[NUM_CHIPS] = {9, 2, 4, 2, 3, 2, 2, 2};
 
+// Lazy fold of the constraints: raw 64-bit products of Montgomery values accumulate with
+// v_mad_u64_u32 (a base constraint times its EF alpha power is one multiply-add per
+// component instead of a Montgomery product + modular add).  Budget: a raw product is < p^2
+// (1 unit), a reduced EF term added at scale 2^32 is < 2 p^2 (2 units); the accumulator is
+// folded (hi * (2^32 mod p) + lo < 2^57) before 4 units would be exceeded (4 p^2 + 2^57 <
+// 2^64), and reduced once at the end -- the same field element as the eager sum.
 struct PowAcc {
-  EF acc;
+  static constexpr uint32_t C32 = (1u << 25) - 2;  // 2^32 mod p
+  uint64_t a64[4];
+  int units;
   const EF* __restrict__ ap;
   int k;
+  __device__ __forceinline__ void fold() {
+#pragma unroll
+    for (int e = 0; e < 4; e++) a64[e] = (uint64_t)(uint32_t)(a64[e] >> 32) * C32 + (uint32_t)a64[e];
+    units = 0;
+  }
   __device__ __forceinline__ void emit(uint32_t c) {
-    acc = ef_add(acc, ef_mul_base(ap[k], c));
-    k++;
+    if (units + 1 > 4) fold();
+    const EF a = ap[k++];
+#pragma unroll
+    for (int e = 0; e < 4; e++) a64[e] += (uint64_t)a.c[e] * c;
+    units += 1;
   }
   __device__ __forceinline__ void emit_ext(const EF& c) {
-    acc = ef_add(acc, ef_mul(ap[k], c));
-    k++;
+    if (units + 2 > 4) fold();
+    const EF r = ef_mul(ap[k++], c);
+#pragma unroll
+    for (int e = 0; e < 4; e++) a64[e] += (uint64_t)r.c[e] << 32;
+    units += 2;
+  }
+  __device__ __forceinline__ EF value() {
+    fold();
+    EF r;
+#pragma unroll
+    for (int e = 0; e < 4; e++) r.c[e] = mreduce(a64[e]);
+    return r;
   }
 };
 
@@ -83,12 +109,12 @@ __global__ __launch_bounds__(256) void k_quotient(const uint32_t* __restrict__ m
   const uint32_t zi = mmul(zh, inv_ab);
   const uint32_t is_first = mmul(zi, b), is_last = mmul(zi, a), is_trans = b;
 
-  PowAcc acc{ef_zero(), qp.alpha_pows, 0};
+  PowAcc acc{{0, 0, 0, 0}, 0, qp.alpha_pows, 0};
   Air<BaseOps, PowAcc> air{L, Nx, PL, PN, is_first, is_last, is_trans, acc};
   air.template eval_air<CHIP>();
   air.template eval_perm<CHIP>(pl, pn, qp.perm_alpha, qp.beta_pows, qp.cumsum, ef_base(is_first),
                                ef_base(is_last), ef_base(is_trans));
-  const EF q = ef_mul_base(acc.acc, zh_inv);
+  const EF q = ef_mul_base(acc.value(), zh_inv);
   const size_t chunk = t >> (logN - 1), pos = t & (n - 1);
 #pragma unroll
   for (int e = 0; e < 4; e++) qout[(chunk * 4 + e) * n + pos] = q.c[e];
