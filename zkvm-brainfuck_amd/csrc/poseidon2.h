@@ -17,6 +17,8 @@ namespace kb {
 struct P2Tables {
   uint32_t ext_init[4][16];
   uint32_t ext_term[4][16];
+  uint32_t ext_init_r2[4][16];  // rc^M * R mod p: added to a 64-bit R^2-form value
+  uint32_t ext_term_r2[4][16];
   uint32_t internal[13];
   uint32_t diag[16];
   uint32_t dabs[16];  // |d_i| (Montgomery)
@@ -35,6 +37,8 @@ constexpr P2Tables make_p2_tables() {
     for (int i = 0; i < 16; i++) {
       t.ext_init[r][i] = to_mont_c(RC_RAW[r * 16 + i] % P);
       t.ext_term[r][i] = to_mont_c(RC_RAW[(17 + r) * 16 + i] % P);
+      t.ext_init_r2[r][i] = to_mont_c(t.ext_init[r][i]);
+      t.ext_term_r2[r][i] = to_mont_c(t.ext_term[r][i]);
     }
   for (int r = 0; r < 13; r++) t.internal[r] = to_mont_c(RC_RAW[(4 + r) * 16] % P);
   uint32_t d[16] = {cneg(2),        1,          2,         cinv(2),          3,
@@ -106,18 +110,61 @@ KB_HD void mds_light(uint32_t s[16]) {
 
 // N independent permutations advanced round by round, so the scheduler can interleave their
 // dependency chains (the internal rounds are one serial chain per state).
+// ---- external rounds in 64-bit R^2-form -------------------------------------------------
+// The S-box leaves its last product unreduced (x2^M * x^M = x^3 R^2 mod p, folded below 2^57),
+// the MDS-light layer adds in 64 bits (a half-rate v_lshl_add_u64 each, no reductions; a
+// row's coefficients sum to 35, so values stay below 2^62.2), the next round constant is
+// added as rc^M R mod p (the high word grows by at most 1, so it stays below p) and one
+// Montgomery reduction returns the next S-box input in Montgomery form.
+constexpr uint32_t C32 = (1u << 25) - 2;  // 2^32 mod p
+KB_HD uint64_t fold64(uint64_t x) { return (uint64_t)(uint32_t)(x >> 32) * C32 + (uint32_t)x; }
+KB_HD uint64_t cube_r2(uint32_t x) { return fold64((uint64_t)mmul(x, x) * x); }
+// Montgomery reduction of y with hi(y) < p: result in [0, p)
+KB_HD uint32_t mred1(uint64_t y) {
+  const uint32_t m = (uint32_t)y * MU;
+  const uint32_t r = opaque((uint32_t)(y >> 32)) - (uint32_t)(((uint64_t)m * P) >> 32);
+  return umin(r, r + P);
+}
+KB_HD void mds_light64(uint64_t s[16]) {
+#pragma unroll
+  for (int b = 0; b < 16; b += 4) {
+    const uint64_t x0 = s[b], x1 = s[b + 1], x2 = s[b + 2], x3 = s[b + 3];
+    const uint64_t t01 = x0 + x1, t23 = x2 + x3, t0123 = t01 + t23;
+    const uint64_t t01123 = t0123 + x1, t01233 = t0123 + x3;
+    s[b + 3] = t01233 + (x0 + x0);  // 3x0 + x1 + x2 + 2x3
+    s[b + 1] = t01123 + (x2 + x2);  // x0 + 2x1 + 3x2 + x3
+    s[b + 0] = t01123 + t01;        // 2x0 + 3x1 + x2 + x3
+    s[b + 2] = t01233 + t23;        // x0 + x1 + 2x2 + 3x3
+  }
+  uint64_t sums[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) sums[k] = (s[k] + s[4 + k]) + (s[8 + k] + s[12 + k]);
+#pragma unroll
+  for (int i = 0; i < 16; i++) s[i] += sums[i & 3];
+}
+// Four external rounds from Montgomery state s (round constants rc / rc_r2 per round).
+KB_HD void external_rounds(uint32_t s[16], const uint32_t (&rc)[4][16],
+                           const uint32_t (&rc_r2)[4][16]) {
+  uint64_t y[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) y[i] = cube_r2(madd(s[i], rc[0][i]));
+  mds_light64(y);
+#pragma unroll
+  for (int r = 1; r < 4; r++) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) y[i] = cube_r2(mred1(y[i] + rc_r2[r][i]));
+    mds_light64(y);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; i++) s[i] = mred1(y[i]);
+}
+
 template <int N>
 KB_HD void poseidon2_permute_n(uint32_t (&s)[N][16]) {
 #pragma unroll
-  for (int k = 0; k < N; k++) mds_light(s[k]);
-#pragma unroll
-  for (int r = 0; r < 4; r++) {
-#pragma unroll
-    for (int k = 0; k < N; k++) {
-#pragma unroll
-      for (int i = 0; i < 16; i++) s[k][i] = cube(madd(s[k][i], P2.ext_init[r][i]));
-      mds_light(s[k]);
-    }
+  for (int k = 0; k < N; k++) {
+    mds_light(s[k]);
+    external_rounds(s[k], P2.ext_init, P2.ext_init_r2);
   }
 #pragma unroll
   for (int r = 0; r < 13; r++) {
@@ -149,14 +196,7 @@ KB_HD void poseidon2_permute_n(uint32_t (&s)[N][16]) {
     }
   }
 #pragma unroll
-  for (int r = 0; r < 4; r++) {
-#pragma unroll
-    for (int k = 0; k < N; k++) {
-#pragma unroll
-      for (int i = 0; i < 16; i++) s[k][i] = cube(madd(s[k][i], P2.ext_term[r][i]));
-      mds_light(s[k]);
-    }
-  }
+  for (int k = 0; k < N; k++) external_rounds(s[k], P2.ext_term, P2.ext_term_r2);
 }
 
 KB_HD void poseidon2_permute(uint32_t s[16]) {
