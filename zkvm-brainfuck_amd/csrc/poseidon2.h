@@ -174,25 +174,15 @@ KB_HD void poseidon2_permute_n(uint32_t (&s)[N][16]) {
       t[0] = cube(madd(t[0], P2.internal[r]));
       const uint32_t sum = sum16(t);
       // s_i <- sum + d_i s_i with d = [-2,1,2,1/2,3,4,-1/2,-3,-4,1/2^8,1/8,1/2^24,-1/2^8,-1/8,
-      // -1/16,-1/2^24].  Small integers use doublings; the fractions are one Montgomery
-      // multiply by |d_i| (cheaper on gfx950 than shifting: v_lshlrev/v_min are half rate,
-      // scripts/ubench_valu.hip), the sign folds into add/sub.
+      // -1/16,-1/2^24].
+      // d = -2, 1, 2: doublings; the rest in one step: d^M s + (sum in R^2-form) < p^2 + p
+      // has its high word below p, so one Montgomery reduction gives sum + d s.
+      const uint32_t sum_r2 = mmul(sum, R2);
       t[0] = msub(sum, mdbl(t[0]));
       t[1] = madd(sum, t[1]);
       t[2] = madd(sum, mdbl(t[2]));
-      t[3] = madd(sum, mmul(t[3], P2.dabs[3]));
-      t[4] = madd(sum, madd(mdbl(t[4]), t[4]));
-      t[5] = madd(sum, mdbl(mdbl(t[5])));
-      t[6] = msub(sum, mmul(t[6], P2.dabs[6]));
-      t[7] = msub(sum, madd(mdbl(t[7]), t[7]));
-      t[8] = msub(sum, mdbl(mdbl(t[8])));
-      t[9] = madd(sum, mmul(t[9], P2.dabs[9]));
-      t[10] = madd(sum, mmul(t[10], P2.dabs[10]));
-      t[11] = madd(sum, mmul(t[11], P2.dabs[11]));
-      t[12] = msub(sum, mmul(t[12], P2.dabs[12]));
-      t[13] = msub(sum, mmul(t[13], P2.dabs[13]));
-      t[14] = msub(sum, mmul(t[14], P2.dabs[14]));
-      t[15] = msub(sum, mmul(t[15], P2.dabs[15]));
+#pragma unroll
+      for (int i = 3; i < 16; i++) t[i] = mred1((uint64_t)P2.diag[i] * t[i] + sum_r2);
     }
   }
 #pragma unroll
