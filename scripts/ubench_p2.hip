@@ -20,21 +20,6 @@ __global__ __launch_bounds__(BS) void k_chain(uint32_t* out, int iters) {
   out[t] = acc;
 }
 
-template <int BS>
-__global__ __launch_bounds__(BS) void k_chain2(uint32_t* out, int iters) {
-  uint32_t s[2][16];
-  const uint32_t t = blockIdx.x * BS + threadIdx.x;
-#pragma unroll
-  for (int k = 0; k < 2; k++)
-#pragma unroll
-    for (int i = 0; i < 16; i++) s[k][i] = (t * 32 + k * 16 + i) % kb::P;
-  for (int it = 0; it < iters; it++) kb::poseidon2_permute_n<2>(s);
-  uint32_t acc = 0;
-#pragma unroll
-  for (int i = 0; i < 16; i++) acc ^= s[0][i] ^ s[1][i];
-  out[t] = acc;
-}
-
 int main() {
   const int iters = 64;
   uint32_t* out;
@@ -56,16 +41,6 @@ int main() {
       CHK(hipEventElapsedTime(&ms, e0, e1));
       printf("block %d: %.3f ms, %.2f G perms/s\n", bs, ms, (double)threads * iters / (ms * 1e-3) / 1e9);
     }
-  }
-  for (int rep = 0; rep < 2; rep++) {  // two states per thread: half the threads
-    CHK(hipEventRecord(e0));
-    hipLaunchKernelGGL(k_chain2<256>, dim3(threads / 512), dim3(256), 0, 0, out, iters);
-    CHK(hipEventRecord(e1));
-    CHK(hipEventSynchronize(e1));
-    float ms;
-    CHK(hipEventElapsedTime(&ms, e0, e1));
-    printf("x2 interleaved, block 256: %.3f ms, %.2f G perms/s\n", ms,
-           (double)threads * iters / (ms * 1e-3) / 1e9);
   }
   return 0;
 }

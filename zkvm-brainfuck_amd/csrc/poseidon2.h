@@ -70,61 +70,10 @@ KB_HD uint32_t cube(uint32_t x) {
   return umin(r, r + P);
 }
 
-// Sum of 16 reduced values.  Pair sums are < 2p and fit 32 bits; the 8 pairs accumulate
-// exactly in 64 bits with v_mad_u64_u32 (x * 1 + acc: one half-rate op, where a reduced
-// modular add costs add + sub + min), then one reduction: 2^32 = 2^25 - 2 (mod p).
-KB_HD uint32_t sum16(const uint32_t s[16]) {
-#ifdef __HIP_DEVICE_COMPILE__
-  uint32_t one;  // opaque 1 keeps the multiply-add form (an add_co/addc pair costs more)
-  asm("s_mov_b32 %0, 1" : "=s"(one));
-#else
-  const uint32_t one = 1;
-#endif
-  uint64_t acc = (uint64_t)(s[0] + s[1]);
-#pragma unroll
-  for (int k = 1; k < 8; k++) acc = (uint64_t)(s[2 * k] + s[2 * k + 1]) * one + acc;
-  constexpr uint32_t C = (1u << 25) - 2;  // < 16p < 2^35, so hi < 8
-  const uint64_t t = (uint64_t)(uint32_t)(acc >> 32) * C + (uint32_t)acc;  // < 2^32 + 2^28
-  const uint32_t hi2 = (uint32_t)(t >> 32);                                // 0 or 1
-  const uint32_t r = (uint32_t)t + ((0u - hi2) & C);                       // any u32 < 2.02p
-  return umin(r, umin(r - P, r - 2 * P));
-}
-
-KB_HD void mds_light(uint32_t s[16]) {
-#pragma unroll
-  for (int b = 0; b < 16; b += 4) {
-    uint32_t x0 = s[b], x1 = s[b + 1], x2 = s[b + 2], x3 = s[b + 3];
-    uint32_t t01 = madd(x0, x1), t23 = madd(x2, x3), t0123 = madd(t01, t23);
-    uint32_t t01123 = madd(t0123, x1), t01233 = madd(t0123, x3);
-    s[b + 3] = madd(t01233, mdbl(x0));  // 3x0 + x1 + x2 + 2x3
-    s[b + 1] = madd(t01123, mdbl(x2));  // x0 + 2x1 + 3x2 + x3
-    s[b + 0] = madd(t01123, t01);       // 2x0 + 3x1 + x2 + x3
-    s[b + 2] = madd(t01233, t23);       // x0 + x1 + 2x2 + 3x3
-  }
-  uint32_t sums[4];
-#pragma unroll
-  for (int k = 0; k < 4; k++) sums[k] = madd(madd(s[k], s[4 + k]), madd(s[8 + k], s[12 + k]));
-#pragma unroll
-  for (int i = 0; i < 16; i++) s[i] = madd(s[i], sums[i & 3]);
-}
-
-// N independent permutations advanced round by round, so the scheduler can interleave their
-// dependency chains (the internal rounds are one serial chain per state).
-// ---- external rounds in 64-bit R^2-form -------------------------------------------------
-// The S-box leaves its last product unreduced (x2^M * x^M = x^3 R^2 mod p, folded below 2^57),
-// the MDS-light layer adds in 64 bits (a half-rate v_lshl_add_u64 each, no reductions; a
-// row's coefficients sum to 35, so values stay below 2^62.2), the next round constant is
-// added as rc^M R mod p (the high word grows by at most 1, so it stays below p) and one
-// Montgomery reduction returns the next S-box input in Montgomery form.
+// MDS-light in 64-bit adds (one half-rate v_lshl_add_u64 each, no reductions): M4 =
+// [[2,3,1,1],[1,2,3,1],[1,1,2,3],[3,1,1,2]] per 4-element block, then each element gets the
+// sum of the 4 blocks at its position.  A row's coefficients sum to 35.
 constexpr uint32_t C32 = (1u << 25) - 2;  // 2^32 mod p
-KB_HD uint64_t fold64(uint64_t x) { return (uint64_t)(uint32_t)(x >> 32) * C32 + (uint32_t)x; }
-KB_HD uint64_t cube_r2(uint32_t x) { return fold64((uint64_t)mmul(x, x) * x); }
-// Montgomery reduction of y with hi(y) < p: result in [0, p)
-KB_HD uint32_t mred1(uint64_t y) {
-  const uint32_t m = (uint32_t)y * MU;
-  const uint32_t r = opaque((uint32_t)(y >> 32)) - (uint32_t)(((uint64_t)m * P) >> 32);
-  return umin(r, r + P);
-}
 KB_HD void mds_light64(uint64_t s[16]) {
 #pragma unroll
   for (int b = 0; b < 16; b += 4) {
@@ -142,57 +91,148 @@ KB_HD void mds_light64(uint64_t s[16]) {
 #pragma unroll
   for (int i = 0; i < 16; i++) s[i] += sums[i & 3];
 }
-// Four external rounds from Montgomery state s (round constants rc / rc_r2 per round).
-KB_HD void external_rounds(uint32_t s[16], const uint32_t (&rc)[4][16],
-                           const uint32_t (&rc_r2)[4][16]) {
-  uint64_t y[16];
+// ---- signed lazy form ------------------------------------------------------------------
+// Between reductions every state element is a SIGNED Montgomery value (int32, |.| < p), and
+// nothing is corrected back to [0, p) until the permutation's output.  The reduction uses a
+// signed Montgomery factor: m = (int32)(lo p^-1), r = hi - mulhi_i32(m, p).  It is exact for
+// any 64-bit two's-complement input (the low words cancel) and, with |mulhi| <= p/2, lands
+// within p/2 of the input's high word — so no bias or correction is needed anywhere:
+//  * external round (R^2-form, 64-bit): S-box a -> a^2 (reduced, in (-p/2, p)) -> a^2 * a
+//    (x^3 R^2, |.| < p^2) -> fold to |.| < 2^55.1 -> MDS-light in 64-bit adds (|.| < 2^60.2)
+//    -> + rc R^2 -> one reduction (|.| < p/2 + 2^28.2) = next S-box input, constant included.
+//  * internal round: c = reduce(t0^3 R^2); T = c + sum t_i (exact, |T| < 16p);
+//    S = reduce(T) (|S| < p/2 + 8) = sum of the plain values; t_i <- reduce(D_i t_i + S K [+ rc])
+//    with D_i = d_i R and K = R^2 as centred residues (|.| <= p/2): |input| < 3p^2/4, so
+//    |t_i| < 7p/8; the result is sum + d_i x_i in Montgomery form.  The next round's constant
+//    rides on t_0's reduction (the terminal external round's on every element after the last
+//    internal round).
+constexpr int32_t centred(uint32_t x) { return x > P / 2 ? (int32_t)(x - P) : (int32_t)x; }
+struct P2Signed {
+  int32_t rc_init[4][16];  // centred rc R^2 (R^2-form constants)
+  int32_t rc_term[4][16];
+  int32_t rc_int[13];
+  int32_t d[16];           // centred d_i R
+  int32_t k;               // centred R^2
+};
+constexpr P2Signed make_p2_signed() {
+  P2Signed t{};
+  for (int r = 0; r < 4; r++)
+    for (int i = 0; i < 16; i++) {
+      t.rc_init[r][i] = centred(P2.ext_init_r2[r][i]);
+      t.rc_term[r][i] = centred(P2.ext_term_r2[r][i]);
+    }
+  for (int r = 0; r < 13; r++) t.rc_int[r] = centred(to_mont_c(P2.internal[r]));
+  for (int i = 0; i < 16; i++) t.d[i] = centred(P2.diag[i]);
+  t.k = centred(R2);
+  return t;
+}
+constexpr P2Signed P2S = make_p2_signed();
+
+// The diagonal entries d_i R include powers of two, and a sum of int32 terms into 64 bits
+// sign-extends each term; the compiler would turn d * t + acc into 64-bit shifts and
+// add/sub pairs, and t + acc into ashr + 64-bit add (2-3 half-rate ops where one
+// v_mad_i64_i32 does).  On the device the multipliers therefore come from a constant-memory
+// table the compiler cannot see into (scalar loads, hoisted into SGPRs); a distinct 1 per sum
+// term stops it from factoring t_1 * 1 + t_2 * 1 + ... back into one sum.
+struct P2Mul {
+  int32_t d[16];
+  int32_t k;
+  int32_t one[16];
+};
+constexpr P2Mul make_p2_mul() {
+  P2Mul m{};
+  for (int i = 0; i < 16; i++) {
+    m.d[i] = P2S.d[i];
+    m.one[i] = 1;
+  }
+  m.k = P2S.k;
+  return m;
+}
+#ifdef __HIP_DEVICE_COMPILE__
+__constant__ P2Mul P2M_DEV = make_p2_mul();
+#define P2M P2M_DEV
+#else
+constexpr P2Mul P2M_HOST = make_p2_mul();
+#define P2M P2M_HOST
+#endif
+// y R^-1 mod p, within p/2 of y's (signed) high word
+// Optimization barrier for a 64-bit value (no instruction).
+KB_HD int64_t opaque64(int64_t x) {
+#ifdef __HIP_DEVICE_COMPILE__
+  asm("" : "+v"(x));
+#endif
+  return x;
+}
+KB_HD int32_t mred_s(int64_t y) {
+  const int32_t m = (int32_t)((uint32_t)y * MU);
+  const uint32_t mh = (uint32_t)(((int64_t)m * (int64_t)P) >> 32);
+  return (int32_t)(opaque((uint32_t)((uint64_t)y >> 32)) - mh);
+}
+// a = x R, |a| < p  ->  x^3 R^2 (mod p), |.| < p^2
+KB_HD int64_t cube_s(int32_t a) {
+  const int64_t A = (int64_t)a * a;
+  return (int64_t)mred_s(A) * a;
+}
+// same residue, |.| < 2^55 + 2^32
+KB_HD int64_t fold_s(int64_t u) {
+  return (int64_t)(int32_t)(u >> 32) * (int64_t)C32 + (int64_t)(uint32_t)u;
+}
+// a[i]: first-round S-box inputs (constant included); rc: constants of rounds 1..3.
+// Leaves the 4th MDS output (64-bit R^2-form) in y.
+KB_HD void external_rounds_s(const int32_t a[16], int64_t y[16], const int32_t (&rc)[4][16]) {
+  uint64_t* u = reinterpret_cast<uint64_t*>(y);
 #pragma unroll
-  for (int i = 0; i < 16; i++) y[i] = cube_r2(madd(s[i], rc[0][i]));
-  mds_light64(y);
+  for (int i = 0; i < 16; i++) y[i] = fold_s(cube_s(a[i]));
+  mds_light64(u);
 #pragma unroll
   for (int r = 1; r < 4; r++) {
 #pragma unroll
-    for (int i = 0; i < 16; i++) y[i] = cube_r2(mred1(y[i] + rc_r2[r][i]));
-    mds_light64(y);
+    for (int i = 0; i < 16; i++) y[i] = fold_s(cube_s(mred_s(y[i] + rc[r][i])));
+    mds_light64(u);
   }
-#pragma unroll
-  for (int i = 0; i < 16; i++) s[i] = mred1(y[i]);
 }
-
-template <int N>
-KB_HD void poseidon2_permute_n(uint32_t (&s)[N][16]) {
+KB_HD void poseidon2_permute(uint32_t s[16]) {
+  int64_t y[16];
+  int32_t t[16];
+  // initial MDS-light on x R^2 (s C32 < 2^56, rows sum to 35: < 2^61.2)
 #pragma unroll
-  for (int k = 0; k < N; k++) {
-    mds_light(s[k]);
-    external_rounds(s[k], P2.ext_init, P2.ext_init_r2);
-  }
+  for (int i = 0; i < 16; i++) y[i] = (int64_t)((uint64_t)s[i] * C32);
+  mds_light64(reinterpret_cast<uint64_t*>(y));
+#pragma unroll
+  for (int i = 0; i < 16; i++) t[i] = mred_s(y[i] + P2S.rc_init[0][i]);
+  external_rounds_s(t, y, P2S.rc_init);
+#pragma unroll
+  for (int i = 0; i < 16; i++) t[i] = mred_s(i == 0 ? y[i] + P2S.rc_int[0] : y[i]);
 #pragma unroll
   for (int r = 0; r < 13; r++) {
+    const int32_t c = mred_s(cube_s(t[0]));
+    int64_t part[4];  // four independent multiply-add chains
 #pragma unroll
-    for (int k = 0; k < N; k++) {
-      uint32_t* t = s[k];
-      t[0] = cube(madd(t[0], P2.internal[r]));
-      const uint32_t sum = sum16(t);
-      // s_i <- sum + d_i s_i with d = [-2,1,2,1/2,3,4,-1/2,-3,-4,1/2^8,1/8,1/2^24,-1/2^8,-1/8,
-      // -1/16,-1/2^24].
-      // d = -2, 1, 2: doublings; the rest in one step: d^M s + (sum in R^2-form) < p^2 + p
-      // has its high word below p, so one Montgomery reduction gives sum + d s.
-      const uint32_t sum_r2 = mmul(sum, R2);
-      t[0] = msub(sum, mdbl(t[0]));
-      t[1] = madd(sum, t[1]);
-      t[2] = madd(sum, mdbl(t[2]));
+    for (int k = 0; k < 4; k++) {
+      part[k] = k ? (int64_t)t[4 * k] : (int64_t)c;
 #pragma unroll
-      for (int i = 3; i < 16; i++) t[i] = mred1((uint64_t)P2.diag[i] * t[i] + sum_r2);
+      for (int i = 4 * k + 1; i < 4 * k + 4; i++) part[k] = (int64_t)P2M.one[i] * t[i] + part[k];
+    }
+    const int32_t sp = mred_s((part[0] + part[1]) + (part[2] + part[3]));
+    if (r < 12) {
+      const int64_t q = opaque64((int64_t)P2M.k * sp);  // one product, not one per element
+      t[0] = mred_s((int64_t)P2M.d[0] * c + (q + P2S.rc_int[r + 1]));
+#pragma unroll
+      for (int i = 1; i < 16; i++) t[i] = mred_s((int64_t)P2M.d[i] * t[i] + q);
+    } else {
+      const int64_t q = opaque64((int64_t)P2M.k * sp);  // one product, not one per element
+      t[0] = mred_s((int64_t)P2M.d[0] * c + (q + P2S.rc_term[0][0]));
+#pragma unroll
+      for (int i = 1; i < 16; i++) t[i] = mred_s((int64_t)P2M.d[i] * t[i] + (q + P2S.rc_term[0][i]));
     }
   }
+  external_rounds_s(t, y, P2S.rc_term);
 #pragma unroll
-  for (int k = 0; k < N; k++) external_rounds(s[k], P2.ext_term, P2.ext_term_r2);
+  for (int i = 0; i < 16; i++) {
+    const uint32_t r = (uint32_t)mred_s(y[i]);
+    s[i] = umin(r, r + P);
+  }
 }
-
-KB_HD void poseidon2_permute(uint32_t s[16]) {
-  poseidon2_permute_n<1>(*reinterpret_cast<uint32_t(*)[1][16]>(s));
-}
-
 // ---------------------------------------------------------------------------------------
 // Latency-optimised permutation: one state element per lane, a state per 16-lane DPP row
 // (lane = threadIdx.x & 15).  Cross-lane steps use DPP: quad_perm rotations for the M4 blocks,
