@@ -127,9 +127,11 @@ __device__ __forceinline__ uint32_t merkle_node_lane(uint32_t v, const ColList& 
 // All layers of <= TOP_NODES nodes in one workgroup: layer l reads the previous layer from
 // LDS (the first from HBM), writes its digests to HBM (query paths need every layer) and to
 // LDS for the next.  Layers of <= LANE_NODES nodes switch to lane mode (16 lanes per node):
-// there the permutation latency, not throughput, is the cost.
-constexpr int TOP_NODES = 512;
-constexpr int LANE_NODES = 256;   // up to 4 batches of 64 nodes per 1024-thread block
+// there the permutation latency, not throughput, is the cost.  64 nodes fill the 1024-thread
+// block in one lane-mode pass; larger layers run as k_compress_lanes launches over many CUs
+// (one CU takes ~10 us for a 512-node layer even in single-lane mode, ~4 passes for 256).
+constexpr int TOP_NODES = 64;
+constexpr int LANE_NODES = 64;
 constexpr int MAXTOP = 24;
 struct TopLayers {
   uint32_t* out[MAXTOP];
