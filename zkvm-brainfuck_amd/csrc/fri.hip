@@ -86,7 +86,7 @@ struct LazyEF {
 };
 
 // ------------------------------------------------------------------ openings
-constexpr int OPEN_T = 256, OPEN_R = 8, OPEN_CH = OPEN_T * OPEN_R;
+constexpr int OPEN_T = 256, OPEN_R = 8, OPEN_CH = OPEN_T * OPEN_R, OPEN_CB = 32;
 
 __device__ __forceinline__ EF wave_sum(EF v) {
 #pragma unroll
@@ -96,87 +96,110 @@ __device__ __forceinline__ EF wave_sum(EF v) {
   return v;
 }
 
-// Sum over the 64 lanes of a wave: DPP rotations inside each 16-lane row, then two
-// cross-row exchanges.  Every lane ends with the total.
-__device__ __forceinline__ uint32_t wave_sum_u(uint32_t v) {
+// Sum over the 16 lanes of a DPP row (every lane of the row ends with the total).
+__device__ __forceinline__ uint32_t row_sum16(uint32_t v) {
   v = madd(v, dpp<DPP_ROR1>(v));
   v = madd(v, dpp<DPP_ROR2>(v));
   v = madd(v, dpp<DPP_ROR4>(v));
-  v = madd(v, dpp<DPP_ROR8>(v));
-  v = madd(v, (uint32_t)__shfl_xor((int)v, 16, 64));
-  return madd(v, (uint32_t)__shfl_xor((int)v, 32, 64));
+  return madd(v, dpp<DPP_ROR8>(v));
 }
 
-// Barycentric opening of one matrix at one point:
-// partial[chunk * w + c] = sum_{t in chunk} W_t col_c[t],  W_t = -x_t invd[t].
-// A thread owns OPEN_R rows and keeps their weights in registers across all columns (the
-// per-column wave reduction is amortized over OPEN_R rows); the next column's loads are
-// issued before the current column's reduction.
+// Barycentric opening of one matrix at one or two points (NP):
+// partial[(chunk * w + c) * NP + k] = sum_{t in chunk} W_k,t col_c[t],  W_k,t = -x_t invd_k[t].
+// A thread owns OPEN_R rows and keeps their weights for both points in registers, so every
+// matrix element is read once for both points.  Per column the lane sums go through the
+// 16-lane DPP rows only; the 16 row sums of the block meet in LDS once per OPEN_CB columns.
+// Loads run two columns ahead (16 per thread in flight) to cover HBM latency.
+template <int NP>
 __global__ __launch_bounds__(OPEN_T) void k_open_partial(const uint32_t* __restrict__ mat,
                                                          size_t height, int w, size_t n, int logH,
-                                                         const EF* __restrict__ invd,
+                                                         const EF* __restrict__ invd_a,
+                                                         const EF* __restrict__ invd_b,
                                                          const uint32_t* __restrict__ twf,
                                                          EF* __restrict__ partial) {
-  __shared__ EF sh[OPEN_T / 64][64];
-  const size_t c0 = (size_t)blockIdx.x * OPEN_CH;
-  EF W[OPEN_R];
-  uint32_t rows[OPEN_R];
+  constexpr int NROW = OPEN_T / 16;
+  __shared__ EF sh[NP][NROW][OPEN_CB];
+  const size_t c0 = (size_t)blockIdx.x * OPEN_CH + threadIdx.x;
+  const int nr = c0 >= n ? 0 : (int)min((size_t)OPEN_R, (n - c0 + OPEN_T - 1) / OPEN_T);
+  EF W[NP][OPEN_R];
 #pragma unroll
   for (int r = 0; r < OPEN_R; r++) {
-    const size_t t = c0 + (size_t)r * OPEN_T + threadIdx.x;
-    rows[r] = (uint32_t)t;
-    W[r] = ef_zero();
-    if (t < n) W[r] = ef_neg(ef_mul_base(invd[t], coset_point((uint32_t)t, logH, twf)));
+    const size_t t = c0 + (size_t)r * OPEN_T;
+    const uint32_t x = r < nr ? coset_point((uint32_t)t, logH, twf) : 0u;
+#pragma unroll
+    for (int k = 0; k < NP; k++)
+      W[k][r] = r < nr ? ef_neg(ef_mul_base((k ? invd_b : invd_a)[t], x)) : ef_zero();
   }
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint32_t v[OPEN_R], nv[OPEN_R];
+  const int row16 = threadIdx.x >> 4, lane16 = threadIdx.x & 15;
+  // two column buffers alternate: while one is consumed the other is in flight, and the
+  // consumed one is refilled two columns ahead
+  uint32_t va[OPEN_R], vb[OPEN_R];
+  auto load = [&](int c, uint32_t (&v)[OPEN_R]) {
+    const uint32_t* col = mat + (size_t)c * height + c0;
 #pragma unroll
-  for (int r = 0; r < OPEN_R; r++) v[r] = rows[r] < n ? mat[rows[r]] : 0u;
-  for (int cb = 0; cb < w; cb += 64) {
-    const int cw = min(64, w - cb);
-    for (int c = 0; c < cw; c++) {
-      const int cn = cb + c + 1;
-      if (cn < w) {
-        const uint32_t* coln = mat + (size_t)cn * height;
+    for (int r = 0; r < OPEN_R; r++) v[r] = r < nr ? col[(size_t)r * OPEN_T] : 0u;
+  };
+  auto consume = [&](int cl, const uint32_t (&v)[OPEN_R]) {
 #pragma unroll
-        for (int r = 0; r < OPEN_R; r++) nv[r] = rows[r] < n ? coln[rows[r]] : 0u;
-      }
+    for (int k = 0; k < NP; k++) {
       LazyEF lz;
       lz.init();
 #pragma unroll
-      for (int r = 0; r < OPEN_R; r++) lz.add(W[r], v[r]);
+      for (int r = 0; r < OPEN_R; r++) lz.add(W[k][r], v[r]);
       EF acc = lz.get();
 #pragma unroll
-      for (int e = 0; e < 4; e++) acc.c[e] = wave_sum_u(acc.c[e]);
-      if (lane == 0) sh[wave][c] = acc;
-#pragma unroll
-      for (int r = 0; r < OPEN_R; r++) v[r] = nv[r];
+      for (int e = 0; e < 4; e++) acc.c[e] = row_sum16(acc.c[e]);
+      if (lane16 == 0) sh[k][row16][cl] = acc;
+    }
+  };
+  load(0, va);
+  if (w > 1) load(1, vb);
+  for (int cb = 0; cb < w; cb += OPEN_CB) {
+    const int cw = min(OPEN_CB, w - cb);
+    for (int c = 0; c < cw; c += 2) {  // OPEN_CB is even: cb + c is even, va holds it
+      consume(c, va);
+      if (cb + c + 2 < w) load(cb + c + 2, va);
+      if (c + 1 < cw) {
+        consume(c + 1, vb);
+        if (cb + c + 3 < w) load(cb + c + 3, vb);
+      }
     }
     __syncthreads();
-    if (threadIdx.x < (unsigned)cw) {
-      EF a = sh[0][threadIdx.x];
+    if (threadIdx.x < (unsigned)(NP * cw)) {
+      const int k = threadIdx.x / cw, c = threadIdx.x % cw;
+      EF a = sh[k][0][c];
 #pragma unroll
-      for (int k = 1; k < OPEN_T / 64; k++) a = ef_add(a, sh[k][threadIdx.x]);
-      partial[(size_t)blockIdx.x * w + cb + threadIdx.x] = a;
+      for (int q = 1; q < NROW; q++) a = ef_add(a, sh[k][q][c]);
+      partial[((size_t)blockIdx.x * w + cb + c) * NP + k] = a;
     }
     __syncthreads();
   }
 }
 
-// out[c] = scale * sum_chunks partial[chunk * w + c]   (one block per column)
+// out_k[c] = scale_k * sum_chunks partial[(chunk * w + c) * NP + k]   (one block per column)
+template <int NP>
 __global__ __launch_bounds__(256) void k_open_final(const EF* __restrict__ partial, int nchunks,
-                                                    int w, EF scale, EF* __restrict__ out) {
-  __shared__ EF sh[4];
+                                                    int w, EF scale_a, EF scale_b,
+                                                    EF* __restrict__ out_a, EF* __restrict__ out_b) {
+  __shared__ EF sh[NP][4];
   const int c = blockIdx.x;
-  EF s = ef_zero();
-  for (int k = threadIdx.x; k < nchunks; k += blockDim.x) s = ef_add(s, partial[(size_t)k * w + c]);
-  s = wave_sum(s);
-  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  EF s[NP];
+#pragma unroll
+  for (int k = 0; k < NP; k++) s[k] = ef_zero();
+  for (int q = threadIdx.x; q < nchunks; q += blockDim.x)
+#pragma unroll
+    for (int k = 0; k < NP; k++) s[k] = ef_add(s[k], partial[((size_t)q * w + c) * NP + k]);
+#pragma unroll
+  for (int k = 0; k < NP; k++) {
+    s[k] = wave_sum(s[k]);
+    if ((threadIdx.x & 63) == 0) sh[k][threadIdx.x >> 6] = s[k];
+  }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    EF tot = sh[0];
-    for (int k = 1; k < (int)(blockDim.x / 64); k++) tot = ef_add(tot, sh[k]);
-    out[c] = ef_mul(tot, scale);
+  if (threadIdx.x < NP) {
+    const int k = threadIdx.x;
+    EF tot = sh[k][0];
+    for (int q = 1; q < (int)(blockDim.x / 64); q++) tot = ef_add(tot, sh[k][q]);
+    (k ? out_b : out_a)[c] = ef_mul(tot, k ? scale_b : scale_a);
   }
 }
 
@@ -315,15 +338,23 @@ void open_matrix(const uint32_t* mat, size_t height, int w, const EF* invd_a, co
   const size_t n = height / 2;  // low coset = first half of the bit-reversed LDE
   const int logH = log2i(height);
   const int nchunks = (int)ceil_div(n, OPEN_CH);
-  DBuf<EF> partial((size_t)nchunks * w);
-  for (int p = 0; p < (invd_b ? 2 : 1); p++) {
-    hipLaunchKernelGGL(k_open_partial, dim3(nchunks), dim3(OPEN_T), 0, st, mat, height, w, n, logH,
-                       p ? invd_b : invd_a, (const uint32_t*)twiddles().fwd.p, partial.p);
+  const int np = invd_b ? 2 : 1;
+  DBuf<EF> partial((size_t)nchunks * w * np);
+  const uint32_t* twf = (const uint32_t*)twiddles().fwd.p;
+  if (np == 2) {
+    hipLaunchKernelGGL(k_open_partial<2>, dim3(nchunks), dim3(OPEN_T), 0, st, mat, height, w, n,
+                       logH, invd_a, invd_b, twf, partial.p);
     KCHECK();
-    hipLaunchKernelGGL(k_open_final, dim3(w), dim3(256), 0, st, (const EF*)partial.p, nchunks, w,
-                       p ? scale_b : scale_a, p ? out_b : out_a);
+    hipLaunchKernelGGL(k_open_final<2>, dim3(w), dim3(256), 0, st, (const EF*)partial.p, nchunks,
+                       w, scale_a, scale_b, out_a, out_b);
+  } else {
+    hipLaunchKernelGGL(k_open_partial<1>, dim3(nchunks), dim3(OPEN_T), 0, st, mat, height, w, n,
+                       logH, invd_a, invd_a, twf, partial.p);
     KCHECK();
+    hipLaunchKernelGGL(k_open_final<1>, dim3(w), dim3(256), 0, st, (const EF*)partial.p, nchunks,
+                       w, scale_a, scale_a, out_a, out_a);
   }
+  KCHECK();
 }
 
 void reduce_height(const std::vector<RedCol>& cols, const std::vector<RedMat>& mats, size_t H,
