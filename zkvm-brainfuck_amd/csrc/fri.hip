@@ -53,38 +53,6 @@ __global__ __launch_bounds__(256) void k_inv_denoms(EF z, int logH, const uint32
   }
 }
 
-// Lazy dot products: raw 64-bit products of Montgomery values (each < p^2) accumulate with
-// v_mad_u64_u32; every 4 products the accumulator is folded, acc = hi * (2^32 mod p) + lo
-// (< 2^57, one more v_mad_u64_u32), which leaves room for 4 more (4 p^2 + 2^57 < 2^64).  One
-// Montgomery reduction at the end (fold < 2^57: its high word is far below 2p).
-struct LazyEF {
-  static constexpr uint32_t C32 = (1u << 25) - 2;  // 2^32 mod p
-  uint64_t acc[4];
-  int pending;
-  __device__ __forceinline__ void init() {
-#pragma unroll
-    for (int e = 0; e < 4; e++) acc[e] = 0;
-    pending = 0;
-  }
-  __device__ __forceinline__ void fold() {
-#pragma unroll
-    for (int e = 0; e < 4; e++) acc[e] = (uint64_t)(uint32_t)(acc[e] >> 32) * C32 + (uint32_t)acc[e];
-    pending = 0;
-  }
-  __device__ __forceinline__ void add(const EF& coef, uint32_t v) {
-#pragma unroll
-    for (int e = 0; e < 4; e++) acc[e] += (uint64_t)coef.c[e] * v;
-    if (++pending == 4) fold();
-  }
-  __device__ __forceinline__ EF get() {
-    fold();
-    EF r;
-#pragma unroll
-    for (int e = 0; e < 4; e++) r.c[e] = mreduce(acc[e]);
-    return r;
-  }
-};
-
 // ------------------------------------------------------------------ openings
 constexpr int OPEN_T = 256, OPEN_R = 8, OPEN_CH = OPEN_T * OPEN_R, OPEN_CB = 32;
 

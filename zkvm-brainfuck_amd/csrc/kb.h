@@ -197,4 +197,37 @@ KB_HD EF ef_pow(EF a, uint64_t e) {
   return r;
 }
 
+// Lazy dot products: raw 64-bit products of Montgomery values (each < p^2) accumulate with
+// v_mad_u64_u32; every 4 products the accumulator is folded, acc = hi * (2^32 mod p) + lo
+// (< 2^57, one more v_mad_u64_u32), which leaves room for 4 more (4 p^2 + 2^57 < 2^64).  One
+// Montgomery reduction at the end (fold < 2^57: its high word is far below 2p).
+struct LazyEF {
+  static constexpr uint32_t C32 = (1u << 25) - 2;  // 2^32 mod p
+  uint64_t acc[4];
+  int pending;
+  KB_HD void init() {
+#pragma unroll
+    for (int e = 0; e < 4; e++) acc[e] = 0;
+    pending = 0;
+  }
+  KB_HD void fold() {
+#pragma unroll
+    for (int e = 0; e < 4; e++) acc[e] = (uint64_t)(uint32_t)(acc[e] >> 32) * C32 + (uint32_t)acc[e];
+    pending = 0;
+  }
+  KB_HD void add(const EF& coef, uint32_t v) {
+#pragma unroll
+    for (int e = 0; e < 4; e++) acc[e] += (uint64_t)coef.c[e] * v;
+    if (++pending == 4) fold();
+  }
+  KB_HD EF get() {
+    fold();
+    EF r;
+#pragma unroll
+    for (int e = 0; e < 4; e++) r.c[e] = mreduce(acc[e]);
+    return r;
+  }
+};
+
+
 }  // namespace kb

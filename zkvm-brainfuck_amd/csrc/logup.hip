@@ -32,11 +32,12 @@ template <int CHIP, int J, int MW, int PWD>
 __device__ __forceinline__ void interaction(const uint32_t (&pr)[PWD], const uint32_t (&m)[MW],
                                             const PermChallenges& ch, EF& den, uint32_t& mult) {
   constexpr Lookup lk = LookupsOf<CHIP>::v.l[J];
-  EF r = ef_add(ch.alpha, ef_base(to_mont_c(lk.kind)));
+  // the products accumulate unreduced in 64 bits (LazyEF): one reduction per component
+  LazyEF lz;
+  lz.init();
 #pragma unroll
-  for (int v = 0; v < lk.nvals; v++)
-    r = ef_add(r, ef_mul_base(ch.beta_pows[v + 1], vcol_eval<BaseOps>(lk.vals[v], pr, m)));
-  den = r;
+  for (int v = 0; v < lk.nvals; v++) lz.add(ch.beta_pows[v + 1], vcol_eval<BaseOps>(lk.vals[v], pr, m));
+  den = ef_add(lz.get(), ef_add(ch.alpha, ef_base(to_mont_c(lk.kind))));
   const uint32_t mu = vcol_eval<BaseOps>(lk.mult, pr, m);
   mult = lk.send ? mu : mneg(mu);
 }
@@ -76,28 +77,50 @@ __global__ __launch_bounds__(256) void k_perm_rows(const uint32_t* __restrict__ 
   for (int c = 0; c < MW; c++) m[c] = mainc[(size_t)c * n + t];
 #pragma unroll
   for (int c = 0; c < PWD; c++) pr[c] = PREP_W[CHIP] > 0 ? prepc[(size_t)c * n + t] : 0;
-  EF sum = ef_zero();
-  // batches are inverted two at a time: 1/(d_a d_b) then cross-multiply
-  static_for<0, (NB + 1) / 2>([&](auto P) {
-    constexpr int BA = 2 * decltype(P)::value, BB = BA + 1;
+  // Batches are paired: pair q has denominator D_q = d_a d_b (or d_a alone).  1/D_q =
+  // conj(D_q) / N(D_q), where conj = frob1 frob2 frob3 and the norm N is a base-field value,
+  // and the norms of all pairs share one base-field inversion (Montgomery's trick): one
+  // Fermat exponentiation per row instead of one per pair.
+  constexpr int NP = (NB + 1) / 2;
+  EF xa[NP], xb[NP], cj[NP];  // xa = n_a d_b, xb = n_b d_a: v_a = xa / D, v_b = xb / D
+  uint32_t nrm[NP], pre[NP];
+  static_for<0, NP>([&](auto P) {
+    constexpr int q = decltype(P)::value, BA = 2 * q, BB = BA + 1;
     EF na, da;
     batch_frac<CHIP, BA>(pr, m, ch, na, da);
-    EF va, vb;
+    EF D = da;
     if constexpr (BB < NB) {
       EF nb, db;
       batch_frac<CHIP, BB>(pr, m, ch, nb, db);
-      const EF inv = ef_inv(ef_mul(da, db));
-      va = ef_mul(na, ef_mul(inv, db));
-      vb = ef_mul(nb, ef_mul(inv, da));
-#pragma unroll
-      for (int e = 0; e < 4; e++) perm[(size_t)(4 * BB + e) * n + t] = vb.c[e];
-      sum = ef_add(sum, vb);
+      D = ef_mul(da, db);
+      xa[q] = ef_mul(na, db);
+      xb[q] = ef_mul(nb, da);
     } else {
-      va = ef_mul(na, ef_inv(da));
+      xa[q] = na;
     }
+    cj[q] = ef_mul(ef_mul(ef_frob1(D), ef_frob2(D)), ef_frob3(D));
+    const uint64_t w0 = (uint64_t)D.c[1] * cj[q].c[3] + (uint64_t)D.c[2] * cj[q].c[2] +
+                        (uint64_t)D.c[3] * cj[q].c[1];
+    nrm[q] = madd(mreduce((uint64_t)D.c[0] * cj[q].c[0]), mul3(mreduce(w0)));
+    pre[q] = q ? mmul(pre[q - 1], nrm[q]) : nrm[q];
+  });
+  uint32_t inv = minv(pre[NP - 1]);
+  EF sum = ef_zero();
+  static_for<0, NP>([&](auto P) {
+    constexpr int q = NP - 1 - decltype(P)::value, BA = 2 * q, BB = BA + 1;
+    const uint32_t inv_n = q ? mmul(inv, pre[q - 1]) : inv;  // 1 / N(D_q)
+    if (q) inv = mmul(inv, nrm[q]);
+    const EF invD = ef_mul_base(cj[q], inv_n);
+    const EF va = ef_mul(xa[q], invD);
 #pragma unroll
     for (int e = 0; e < 4; e++) perm[(size_t)(4 * BA + e) * n + t] = va.c[e];
     sum = ef_add(sum, va);
+    if constexpr (BB < NB) {
+      const EF vb = ef_mul(xb[q], invD);
+#pragma unroll
+      for (int e = 0; e < 4; e++) perm[(size_t)(4 * BB + e) * n + t] = vb.c[e];
+      sum = ef_add(sum, vb);
+    }
   });
   rowsum[t] = sum;
 }
