@@ -132,21 +132,32 @@ KB_HD EF ef_add_base(EF a, uint32_t b) {
   return a;
 }
 KB_HD uint32_t mul3(uint32_t x) { return madd(madd(x, x), x); }
+// x mod p as a smaller 64-bit value: hi * (2^32 mod p) + lo  (< 2^57 for any x)
+KB_HD uint64_t fold32(uint64_t x) { return (uint64_t)(uint32_t)(x >> 32) * ((1u << 25) - 2) + (uint32_t)x; }
+// Montgomery reduction of y with hi(y) < p: result in [0, p)
+KB_HD uint32_t mred_lt_p(uint64_t y) {
+  const uint32_t m = mont_m((uint32_t)y);
+  const uint32_t r = (uint32_t)(y >> 32) - (uint32_t)(((uint64_t)m * P) >> 32);
+  return umin(r, r + P);
+}
 KB_HD EF ef_mul(const EF& a, const EF& b) {
-  // lazy reduction: sums of <= 3 products of values < p stay below 2^64 with hi < 2p
-  uint64_t w0 = (uint64_t)a.c[1] * b.c[3] + (uint64_t)a.c[2] * b.c[2] + (uint64_t)a.c[3] * b.c[1];
-  uint64_t w1 = (uint64_t)a.c[2] * b.c[3] + (uint64_t)a.c[3] * b.c[2];
-  uint64_t w2 = (uint64_t)a.c[3] * b.c[3];
-  uint64_t d0 = (uint64_t)a.c[0] * b.c[0];
-  uint64_t d1 = (uint64_t)a.c[0] * b.c[1] + (uint64_t)a.c[1] * b.c[0];
-  uint64_t d2 = (uint64_t)a.c[0] * b.c[2] + (uint64_t)a.c[1] * b.c[1] + (uint64_t)a.c[2] * b.c[0];
-  uint64_t d3a = (uint64_t)a.c[0] * b.c[3] + (uint64_t)a.c[1] * b.c[2];
-  uint64_t d3b = (uint64_t)a.c[2] * b.c[1] + (uint64_t)a.c[3] * b.c[0];
+  // Coefficient k = d_k + 3 w_k (x^4 = 3).  Each d_k, w_k is a sum of <= 4 raw products
+  // (< 4 p^2 < 2^64).  3 fold(w) < 2^58.2 and fold(d) < 2^57 keep d + 3 w below p 2^32, so
+  // one Montgomery reduction with a single correction gives the coefficient.
+  const uint64_t w0 = (uint64_t)a.c[1] * b.c[3] + (uint64_t)a.c[2] * b.c[2] + (uint64_t)a.c[3] * b.c[1];
+  const uint64_t w1 = (uint64_t)a.c[2] * b.c[3] + (uint64_t)a.c[3] * b.c[2];
+  const uint64_t w2 = (uint64_t)a.c[3] * b.c[3];
+  const uint64_t d0 = (uint64_t)a.c[0] * b.c[0];  // < p^2: hi < p / 2, no fold needed
+  const uint64_t d1 = (uint64_t)a.c[0] * b.c[1] + (uint64_t)a.c[1] * b.c[0];
+  const uint64_t d2 = (uint64_t)a.c[0] * b.c[2] + (uint64_t)a.c[1] * b.c[1] + (uint64_t)a.c[2] * b.c[0];
+  const uint64_t d3 = (uint64_t)a.c[0] * b.c[3] + (uint64_t)a.c[1] * b.c[2] +
+                      (uint64_t)a.c[2] * b.c[1] + (uint64_t)a.c[3] * b.c[0];  // < 4p^2: hi < 2p
+  const uint64_t f0 = fold32(w0), f1 = fold32(w1), f2 = fold32(w2);
   EF r;
-  r.c[0] = madd(mreduce(d0), mul3(mreduce(w0)));
-  r.c[1] = madd(mreduce(d1), mul3(mreduce(w1)));
-  r.c[2] = madd(mreduce(d2), mul3(mreduce(w2)));
-  r.c[3] = madd(mreduce(d3a), mreduce(d3b));
+  r.c[0] = mred_lt_p(d0 + 3 * f0);
+  r.c[1] = mred_lt_p(fold32(d1) + 3 * f1);
+  r.c[2] = mred_lt_p(fold32(d2) + 3 * f2);
+  r.c[3] = mreduce(d3);
   return r;
 }
 KB_HD bool ef_eq(const EF& a, const EF& b) {

@@ -63,7 +63,7 @@ struct PowAcc {
 };
 
 template <int CHIP>
-__global__ __launch_bounds__(256) void k_quotient(const uint32_t* __restrict__ mainc,
+__global__ __launch_bounds__(256, 3) void k_quotient(const uint32_t* __restrict__ mainc,
                                                   const uint32_t* __restrict__ prepc,
                                                   const uint32_t* __restrict__ permc, int logN,
                                                   QuotParams qp, const uint32_t* __restrict__ twf,
