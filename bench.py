@@ -25,6 +25,13 @@ sys.path.insert(0, os.path.join(ROOT, "zkvm-brainfuck_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# VALU issue peak: 256 CUs x 4 SIMDs x 32 lanes/cycle (a wave64 VALU op issues over 2 cycles,
+# MI355X_MICROARCH.md) x 2.4 GHz, in full-rate lane-ops/s; half-rate ops (mul_lo/hi, mad_u64,
+# min, 64-bit adds) count as 2.  scripts/ubench_valu.hip measures 75 T for v_sub/v_xor.
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+# Full-rate-equivalent VALU lane-ops of one Poseidon2 permutation in k_permute_batch
+# (gfx950 ISA instruction mix, profiles/r01/poseidon2_isa_mix.txt).
+P2_UNITS_PER_PERM = 6010
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01", "pmc_summary.json")
 
 
@@ -40,6 +47,21 @@ def ntt_traffic():
         return traffic / launches, traffic / alg
     except (OSError, KeyError, ValueError, ZeroDivisionError):
         return None, None
+
+
+def poseidon2_roofline(tm):
+    """VALU roofline of the Merkle hashing kernels (k_hash_leaves, k_compress, k_hash_rows8),
+    timed per launch with HIP events; these are integer-VALU bound, not HBM or MFMA."""
+    if tm.p2_kernel_ms <= 0:
+        return None
+    gps = tm.p2_perms / (tm.p2_kernel_ms * 1e-3) / 1e9
+    tops = gps * P2_UNITS_PER_PERM / 1e3
+    return {"bound": "valu", "kernels": "k_hash_leaves + k_compress + k_hash_rows8",
+            "perms_per_proof": int(tm.p2_perms), "kernel_ms": round(tm.p2_kernel_ms, 3),
+            "launches": tm.p2_launches, "achieved_gperms_s": round(gps, 2),
+            "units_per_perm": P2_UNITS_PER_PERM, "achieved": round(tops, 1),
+            "peak": round(VALU_PEAK_TOPS, 1), "unit": "T full-rate VALU lane-ops/s",
+            "frac": round(tops / VALU_PEAK_TOPS, 4)}
 
 
 def cpu_baseline(sample_stdin=200):
@@ -201,6 +223,7 @@ def main():
                          "avg_launch_us": round(ntt_avg_us, 2),
                          "note": "per-launch HIP events on the prover stream; whole-LDE rate "
                                  "(12*n*w B per coset LDE) is ntt_hbm_gbs"},
+            "poseidon2": poseidon2_roofline(tm),
             "proof_bytes": len(proof),
         }
         if not args.no_cpu_baseline:

@@ -47,6 +47,8 @@ typedef struct {
   int lde_calls;
   double ntt_kernel_ms, ntt_kernel_bytes; /* NTT pass kernel, per-launch events, 8 B/element */
   int ntt_kernel_launches;
+  double p2_kernel_ms, p2_perms; /* Poseidon2 leaf/compress kernels: time and permutations */
+  int p2_launches;
 } bfz_timings;
 
 int bfz_init(int device);

@@ -24,7 +24,8 @@ class Timings(ctypes.Structure):
         ("quotient_ms", c_double), ("open_ms", c_double), ("fri_ms", c_double),
         ("total_ms", c_double), ("lde_ms", c_double), ("lde_bytes", c_double),
         ("lde_calls", c_int), ("ntt_kernel_ms", c_double), ("ntt_kernel_bytes", c_double),
-        ("ntt_kernel_launches", c_int),
+        ("ntt_kernel_launches", c_int), ("p2_kernel_ms", c_double), ("p2_perms", c_double),
+        ("p2_launches", c_int),
     ]
 
     def as_dict(self) -> dict:

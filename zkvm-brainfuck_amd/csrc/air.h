@@ -6,6 +6,8 @@
 // function cites the reference eval it follows.  Chip::eval evaluates the AIR first and the
 // LogUp constraints after (crates/stark/src/chip.rs:222-228).
 #pragma once
+#include <type_traits>
+
 #include "kb.h"
 
 namespace bfz {
@@ -298,11 +300,19 @@ struct Air {
   template <int CHIP, int J>
   KB_HD void rlc_mult(const EF& pa, const EF* pb_pows, EF& rlc, EF& mult) const {
     constexpr Lookup lk = LookupsOf<CHIP>::v.l[J];
-    EF r = kb::ef_add(pa, kb::ef_base(kb::to_mont_c(lk.kind)));
+    if constexpr (std::is_same<Ops, BaseOps>::value) {  // lazy 64-bit products (kb::LazyEF)
+      kb::LazyEF lz;
+      lz.init();
 #pragma unroll
-    for (int v = 0; v < lk.nvals; v++)
-      r = kb::ef_add(r, Ops::mulE(pb_pows[v + 1], vcol_eval<Ops>(lk.vals[v], PL, L)));
-    rlc = r;
+      for (int v = 0; v < lk.nvals; v++) lz.add(pb_pows[v + 1], vcol_eval<Ops>(lk.vals[v], PL, L));
+      rlc = kb::ef_add(lz.get(), kb::ef_add(pa, kb::ef_base(kb::to_mont_c(lk.kind))));
+    } else {
+      EF r = kb::ef_add(pa, kb::ef_base(kb::to_mont_c(lk.kind)));
+#pragma unroll
+      for (int v = 0; v < lk.nvals; v++)
+        r = kb::ef_add(r, Ops::mulE(pb_pows[v + 1], vcol_eval<Ops>(lk.vals[v], PL, L)));
+      rlc = r;
+    }
     const EF mm = Ops::toE(vcol_eval<Ops>(lk.mult, PL, L));
     mult = lk.send ? mm : kb::ef_neg(mm);
   }

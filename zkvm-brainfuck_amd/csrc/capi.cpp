@@ -237,6 +237,9 @@ void fill_timings(const bfz::StageTimes& st, bfz_timings* t) {
   t->ntt_kernel_ms = st.ntt_kernel_ms;
   t->ntt_kernel_bytes = st.ntt_kernel_bytes;
   t->ntt_kernel_launches = st.ntt_kernel_launches;
+  t->p2_kernel_ms = st.p2_kernel_ms;
+  t->p2_perms = st.p2_perms;
+  t->p2_launches = st.p2_launches;
 }
 struct ShardScope {  // installs the shard context for one proof
   explicit ShardScope(bfz::ShardCtx* c) { bfz::shard_ctx() = c; }

@@ -177,5 +177,8 @@ struct KernelProbe {
   }
 };
 KernelProbe& ntt_probe();  // NTT kernels: k_ntt_r16 (8 B/element), k_lde_mid (12 B/input element)
+// Throughput Poseidon2 kernels (k_hash_leaves, k_compress, k_hash_rows8); "bytes" counts
+// permutations.
+KernelProbe& p2_probe();
 
 }  // namespace bfz

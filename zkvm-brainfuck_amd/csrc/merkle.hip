@@ -256,9 +256,15 @@ static void launch_layer(MerkleTree& t, int L, size_t j0, size_t count,
   if (count <= LANE_LAYER_MAX)
     hipLaunchKernelGGL(k_compress_lanes, dim3(ceil_div(16 * count, 256)), dim3(256), 0, st, prev,
                        j0, count, t.layers[L].p, make_cols(grp));
-  else
+  else {
+    const ColList cl = make_cols(grp);
+    KernelProbe& probe = p2_probe();
+    hipEvent_t ev0 = probe.on ? probe.begin(st) : nullptr;
     hipLaunchKernelGGL(k_compress, dim3(ceil_div(count, 256)), dim3(256), 0, st, prev, j0, count,
-                       t.layers[L].p, make_cols(grp));
+                       t.layers[L].p, cl);
+    // one compression, plus the injected rows' sponge and one more compression if any
+    if (probe.on) probe.end(ev0, st, (double)count * (cl.n ? 2 + (cl.n + 7) / 8 : 1));
+  }
   KCHECK();
 }
 
@@ -362,9 +368,12 @@ void merkle_build(const std::vector<MatRef>& mats, MerkleTree& t, hipStream_t st
   t.layers[0].reset(8 * h0);
   const ColList cl = make_cols(grp);
   auto leaves = [&](size_t r0, size_t count) {
+    KernelProbe& probe = p2_probe();
+    hipEvent_t ev0 = probe.on ? probe.begin(st) : nullptr;
     hipLaunchKernelGGL(k_hash_leaves, dim3(ceil_div(count, 256)), dim3(256), 0, st, cl, r0,
                        count, t.layers[0].p);
     KCHECK();
+    if (probe.on) probe.end(ev0, st, (double)count * ((cl.n + 7) / 8));
   };
   if (shard_tree(h0)) {
     build_sharded(t, h0, sorted, next, leaves, st, true);
@@ -379,9 +388,13 @@ static void hash_rows8_range(const uint32_t* rows, size_t r0, size_t count, uint
   if (count <= LANE_LAYER_MAX)
     hipLaunchKernelGGL(k_hash_rows8_lanes, dim3(ceil_div(16 * count, 256)), dim3(256), 0, st, rows,
                        r0, count, digests);
-  else
+  else {
+    KernelProbe& probe = p2_probe();
+    hipEvent_t ev0 = probe.on ? probe.begin(st) : nullptr;
     hipLaunchKernelGGL(k_hash_rows8, dim3(ceil_div(count, 256)), dim3(256), 0, st, rows, r0, count,
                        digests);
+    if (probe.on) probe.end(ev0, st, (double)count);
+  }
   KCHECK();
 }
 

@@ -62,6 +62,9 @@ struct StageTimes {          // milliseconds, measured with HIP events on the pr
   double ntt_kernel_ms = 0;     // k_ntt_r16 launches, one event pair per launch
   double ntt_kernel_bytes = 0;  // 8 B per element per pass
   int ntt_kernel_launches = 0;
+  double p2_kernel_ms = 0;   // throughput Poseidon2 kernels (leaves, compress, FRI rows)
+  double p2_perms = 0;       // permutations they computed
+  int p2_launches = 0;
 };
 
 std::unique_ptr<ProvingKey> setup(const std::string& program_src);

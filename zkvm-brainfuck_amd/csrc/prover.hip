@@ -223,6 +223,8 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
   ev.on = opt.timing && times;
   ntt_probe().reset();
   ntt_probe().on = ev.on;
+  p2_probe().reset();
+  p2_probe().on = ev.on;
   std::vector<std::vector<EF>> keep;  // host buffers of async uploads live until the end
   const auto t_start = std::chrono::steady_clock::now();
   hipEvent_t e_total = ev.on ? ev.begin(st) : nullptr;
@@ -624,6 +626,12 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
     tms->ntt_kernel_ms = pr.ms;
     tms->ntt_kernel_bytes = pr.bytes;
     tms->ntt_kernel_launches = pr.launches;
+    KernelProbe& p2 = p2_probe();
+    p2.collect();
+    p2.on = false;
+    tms->p2_kernel_ms = p2.ms;
+    tms->p2_perms = p2.bytes;
+    tms->p2_launches = p2.launches;
   }
   (void)t_start;
   return std::move(w.b);

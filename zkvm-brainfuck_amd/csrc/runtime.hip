@@ -22,6 +22,11 @@ KernelProbe& ntt_probe() {
   return *k;
 }
 
+KernelProbe& p2_probe() {
+  static KernelProbe* k = new KernelProbe();
+  return *k;
+}
+
 Twiddles& twiddles() {
   static Twiddles* t = new Twiddles();
   return *t;
