@@ -109,6 +109,22 @@ int bfz_record_prove_sharded(const bfz_pk* pk, const bfz_record* rec, int rank, 
                              bfz_allgather_fn allgather, bfz_allreduce_u32_fn allreduce_sum,
                              void* ctx, uint8_t** proof, size_t* proof_len, bfz_timings* timings);
 
+/* Column-sharded PCS commit + FRI commit phase of a synthetic trace (BASELINE.json configs 4
+ * and 5).  Replaces, for one n x (world * w_local) trace, TwoAdicFriPcs::commit
+ * (crates/stark/src/prover.rs:209-236: coset LDE with shift GENERATOR, bit-reversed rows,
+ * MerkleTreeMmcs) followed by the FRI commit phase of fri::prover (prover.rs:460-470) on the
+ * batched column sum_c alpha^c col_c.  Rank r passes its columns [r w_local, (r+1) w_local) as a
+ * DEVICE buffer d_cols (column-major, bit-reversed rows, Montgomery form, n = 2^log_n) and two
+ * device exchange buffers of 2n * w_local words; alltoall(ctx) must exchange equal blocks of
+ * d_send into d_recv (block j to rank j, e.g. ncclAllToAll / torch all_to_all_single), and
+ * allgather is as above.  out receives [root (8) | FRI roots (8 per round) | final value (4)]
+ * (*nwords words, identical on every rank and to world = 1).  cap = capacity of out in words. */
+typedef int (*bfz_alltoall_fn)(void* ctx);
+int bfz_commit_fri_sharded(const uint32_t* d_cols, int log_n, size_t w_local, int rank, int world,
+                           uint32_t* d_send, uint32_t* d_recv, bfz_alltoall_fn alltoall,
+                           bfz_allgather_fn allgather, void* ctx, uint32_t* out, size_t cap,
+                           size_t* nwords);
+
 int bfz_set_num_queries(int num_queries); /* FRI_QUERIES (kb31_poseidon2.rs:59-62) */
 
 int bfz_coset_lde(const uint32_t* evals, size_t n, size_t w, uint32_t shift, uint32_t* lde_out);

@@ -35,6 +35,8 @@ class Timings(ctypes.Structure):
 # collective callbacks of bfz_record_prove_sharded (bfz_allgather_fn / bfz_allreduce_u32_fn)
 ALLGATHER_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_void_p, c_size_t, c_void_p)
 ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, c_void_p, POINTER(c_uint32), c_size_t)
+# bfz_alltoall_fn of bfz_commit_fri_sharded (the caller owns the device exchange buffers)
+ALLTOALL_FN = ctypes.CFUNCTYPE(c_int, c_void_p)
 
 # (name, restype, argtypes) for every symbol declared in include/bfz.h
 SIGNATURES = [
@@ -65,6 +67,9 @@ SIGNATURES = [
     ("bfz_record_prove_sharded", c_int, [c_void_p, c_void_p, c_int, c_int, ALLGATHER_FN,
                                          ALLREDUCE_FN, c_void_p, POINTER(POINTER(c_uint8)),
                                          POINTER(c_size_t), POINTER(Timings)]),
+    ("bfz_commit_fri_sharded", c_int, [c_void_p, c_int, c_size_t, c_int, c_int, c_void_p, c_void_p,
+                                       ALLTOALL_FN, ALLGATHER_FN, c_void_p, POINTER(c_uint32),
+                                       c_size_t, POINTER(c_size_t)]),
     ("bfz_set_num_queries", c_int, [c_int]),
     ("bfz_coset_lde", c_int, [POINTER(c_uint32), c_size_t, c_size_t, c_uint32, POINTER(c_uint32)]),
     ("bfz_commit", c_int, [POINTER(POINTER(c_uint32)), POINTER(c_size_t), POINTER(c_size_t),
@@ -82,6 +87,13 @@ def lib() -> ctypes.CDLL:
         if not os.path.exists(LIB_PATH):
             raise BfzError(f"{LIB_PATH} not built: run `make -C zkvm-brainfuck_amd` "
                            "(or __graft_entry__.build())")
+        # One HIP runtime per process: PyTorch ships its own libamdhip64, and a process that
+        # loads ROCm's copy first (through libbfz) cannot initialise torch.cuda afterwards.
+        # Importing torch first makes libbfz bind to the runtime torch already loaded.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
             fn = getattr(L, name)

@@ -28,6 +28,8 @@ class Collectives:
                     if "nccl" in backend else torch.device("cpu"))
         self.allgather = _lib.ALLGATHER_FN(self._allgather)
         self.allreduce = _lib.ALLREDUCE_FN(self._allreduce)
+        self.alltoall = _lib.ALLTOALL_FN(self._alltoall)
+        self.exchange = None  # (send, recv) device tensors of the pending all-to-all
 
     def _allgather(self, _ctx, send, nbytes, recv):
         try:
@@ -55,6 +57,62 @@ class Collectives:
         except Exception:  # noqa: BLE001
             traceback.print_exc()
             return 1
+
+
+    def _alltoall(self, _ctx):
+        """Equal-block all-to-all of the registered device tensors (RCCL with nccl; through
+        host memory with gloo)."""
+        try:
+            send, recv = self.exchange
+            if self.dev.type == "cuda":
+                self.dist.all_to_all_single(recv, send, group=self.group)
+                self.torch.cuda.synchronize(recv.device)
+            else:
+                r = self.torch.empty(send.shape, dtype=send.dtype)
+                self.dist.all_to_all_single(r, send.cpu(), group=self.group)
+                recv.copy_(r)
+                self.torch.cuda.synchronize(recv.device)
+            return 0
+        except Exception:  # noqa: BLE001
+            traceback.print_exc()
+            return 1
+
+
+def commit_fri_sharded(cols, log_n: int, coll: "Collectives | None", rank: int = 0):
+    """bfz_commit_fri_sharded on this rank's columns.
+
+    cols: int32 CUDA tensor of shape (w_local, 2^log_n): column-major, bit-reversed rows,
+    Montgomery form, columns [rank w_local, (rank+1) w_local) of the trace.  Returns
+    (root, fri_roots, final) as uint32 numpy arrays (identical on every rank)."""
+    import torch
+    L = _lib.lib()
+    w_local = cols.shape[0]
+    world = coll.world if coll else 1
+    n2 = 2 << log_n
+    send = recv = None
+    if world > 1:
+        send = torch.empty((w_local * n2,), dtype=torch.int32, device=cols.device)
+        recv = torch.empty_like(send)
+        coll.exchange = (send, recv)
+    torch.cuda.synchronize(cols.device)  # cols may still be in flight on torch's stream
+    cap = 8 + 8 * (log_n + 1) + 4
+    out = (ctypes.c_uint32 * cap)()
+    nw = ctypes.c_size_t()
+    empty_a2a = _lib.ALLTOALL_FN(0)
+    empty_ag = _lib.ALLGATHER_FN(0)
+    try:
+        _lib.check(L.bfz_commit_fri_sharded(
+            ctypes.c_void_p(cols.data_ptr()), log_n, w_local, rank, world,
+            ctypes.c_void_p(send.data_ptr() if send is not None else 0),
+            ctypes.c_void_p(recv.data_ptr() if recv is not None else 0),
+            coll.alltoall if coll else empty_a2a, coll.allgather if coll else empty_ag, None,
+            out, cap, ctypes.byref(nw)))
+    finally:
+        if coll:
+            coll.exchange = None
+    words = np.frombuffer(bytes(out), dtype=np.uint32)[: nw.value]
+    nfri = (nw.value - 12) // 8
+    return words[:8].copy(), words[8:8 + 8 * nfri].reshape(nfri, 8).copy(), words[-4:].copy()
 
 
 def prove_record_sharded(pk_handle, rec, coll: Collectives, rank: int, timings=None) -> bytes:

@@ -12,6 +12,8 @@
 #include "fri.h"
 #include "merkle.h"
 #include "ntt.h"
+#include "pcs_sharded.h"
+#include "pcs_sharded.h"
 #include "prover.h"
 #include "tracegen.h"
 #include "verifier.h"
@@ -283,6 +285,39 @@ int bfz_record_prove_sharded(const bfz_pk* pk, const bfz_record* rec, int rank, 
     auto v = bfz::prove_events(*pk->pk, rec->ev, o, &st);
     fill_timings(st, t);
     return emit(std::move(v), proof, len);
+  });
+}
+
+int bfz_commit_fri_sharded(const uint32_t* d_cols, int log_n, size_t w_local, int rank, int world,
+                           uint32_t* d_send, uint32_t* d_recv, bfz_alltoall_fn alltoall,
+                           bfz_allgather_fn allgather, void* ctx, uint32_t* out, size_t cap,
+                           size_t* nwords) {
+  return guarded([&] {
+    if (world < 1 || rank < 0 || rank >= world || (world & (world - 1)))
+      throw std::runtime_error("pcs: world must be a power of two, 0 <= rank < world");
+    if (log_n < 1 || log_n > 27) throw std::runtime_error("pcs: log_n out of range");
+    if (world > 1 && (!alltoall || !allgather)) throw std::runtime_error("pcs: collectives required");
+    if (!d_cols || !out || !nwords) throw std::runtime_error("pcs: null argument");
+    bfz::ShardCtx c;
+    c.rank = rank;
+    c.world = world;
+    c.allgather = [&](const void* send, size_t bytes, void* recv) {
+      if (allgather(ctx, send, bytes, recv)) throw std::runtime_error("allgather callback failed");
+    };
+    ShardScope scope(world > 1 ? &c : nullptr);
+    const bfz::PcsShardedResult r = bfz::commit_fri_sharded(
+        d_cols, log_n, (int)w_local, d_send, d_recv,
+        [&] {
+          if (alltoall(ctx)) throw std::runtime_error("alltoall callback failed");
+        },
+        bfz::stream());
+    const size_t need = 8 + 8 * r.fri_roots.size() + 4;
+    *nwords = need;
+    if (cap < need) throw std::runtime_error("pcs: output buffer too small");
+    std::memcpy(out, r.root, 32);
+    for (size_t i = 0; i < r.fri_roots.size(); i++) std::memcpy(out + 8 + 8 * i, r.fri_roots[i].data(), 32);
+    std::memcpy(out + 8 + 8 * r.fri_roots.size(), r.final_value.c, 16);
+    return 0;
   });
 }
 

@@ -44,6 +44,9 @@ void fri_challenge(uint32_t* state, const uint32_t* root, kb::EF* beta, hipStrea
 // Fold with beta read from device memory.
 void fri_fold_dev(const kb::EF* in, kb::EF* out, size_t h, const kb::EF* beta, const kb::EF* add,
                   hipStream_t st);
+// Outputs [i0, i0 + count) of the same fold; in, out and add hold only that range.
+void fri_fold_range(const kb::EF* in, kb::EF* out, size_t h, size_t i0, size_t count,
+                    const kb::EF* beta, const kb::EF* add, hipStream_t st);
 // Query openings: word k of segment s for query index I is
 //   base[((I >> shift) ^ xr) * unit + k * stride],  k < count
 // (matrix rows: unit 1, stride = height; Merkle siblings: unit 8; FRI siblings: unit 4).

@@ -221,16 +221,19 @@ __global__ __launch_bounds__(256) void k_fri_fold(const EF* __restrict__ in, EF*
   out[i] = r;
 }
 
+// Outputs [i0, i0 + count) of a fold of 2h values to h; in/out/add hold that range only
+// (in: 2 count values, from 2 i0).
 __global__ __launch_bounds__(256) void k_fri_fold_dev(const EF* __restrict__ in,
                                                       EF* __restrict__ out, size_t h, int logh,
+                                                      size_t i0, size_t count,
                                                       const EF* __restrict__ beta,
                                                       const uint32_t* __restrict__ twi,
                                                       const EF* __restrict__ add) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= h) return;
+  if (i >= count) return;
   const uint32_t halfv = to_mont_c((P + 1) / 2);
   const EF half_beta = ef_mul_base(*beta, halfv);
-  const uint32_t g = twi[h + dbitrev((uint32_t)i, logh)];
+  const uint32_t g = twi[h + dbitrev((uint32_t)(i0 + i), logh)];
   const EF p = ef_mul_base(half_beta, g);
   const EF lo = in[2 * i], hi = in[2 * i + 1];
   EF r = ef_add(ef_mul(ef_add_base(p, halfv), lo), ef_mul(ef_sub(ef_base(halfv), p), hi));
@@ -356,10 +359,15 @@ void fri_challenge(uint32_t* state, const uint32_t* root, EF* beta, hipStream_t 
 }
 
 void fri_fold_dev(const EF* in, EF* out, size_t h, const EF* beta, const EF* add, hipStream_t st) {
+  fri_fold_range(in, out, h, 0, h, beta, add, st);
+}
+
+void fri_fold_range(const EF* in, EF* out, size_t h, size_t i0, size_t count, const EF* beta,
+                    const EF* add, hipStream_t st) {
   const int logh = log2i(h);
   twiddles().ensure(logh + 1);
-  hipLaunchKernelGGL(k_fri_fold_dev, dim3(ceil_div(h, 256)), dim3(256), 0, st, in, out, h, logh,
-                     beta, (const uint32_t*)twiddles().inv.p, add);
+  hipLaunchKernelGGL(k_fri_fold_dev, dim3(ceil_div(count, 256)), dim3(256), 0, st, in, out, h,
+                     logh, i0, count, beta, (const uint32_t*)twiddles().inv.p, add);
   KCHECK();
 }
 
