@@ -107,22 +107,73 @@ def timed_steps(step, steps, dist=None, sync=lambda: None):
     return ms
 
 
+def run_pcs(args, rank, world, device, dist, coll):
+    """Column-sharded commit + FRI commit phase of a synthetic 2^log_n x cols trace (uniform
+    random Montgomery words, seeded per rank); one step = bfz_commit_fri_sharded on every rank:
+    LDE of the rank's columns, the all-to-all, the Merkle commit and the FRI rounds."""
+    import torch
+    from bfz import shard as bfz_shard
+    P = 0x7F000001
+    log_n, W = args.log_n, args.cols
+    if W % world:
+        raise SystemExit(f"--cols {W} is not divisible by {world} ranks")
+    wl = W // world
+    dev = torch.device("cuda", device)
+    torch.cuda.set_device(dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x5EED + rank)
+    cols = torch.randint(0, P, (wl, 1 << log_n), dtype=torch.int32, device=dev, generator=g)
+    send = recv = None
+    if world > 1:
+        send = torch.empty((wl * (2 << log_n),), dtype=torch.int32, device=dev)
+        recv = torch.empty_like(send)
+
+    def step():
+        return bfz_shard.commit_fri_sharded(cols, log_n, coll, rank, send, recv)
+
+    for _ in range(args.warmup):
+        root, fri, fin = step()
+    ms = timed_steps(step, args.steps, dist, sync=torch.cuda.synchronize)
+    if rank == 0:
+        n = 1 << log_n
+        lde_bytes = 12.0 * n * W  # coset LDE algorithmic bytes of the whole trace
+        line = {
+            "metric": f"column-sharded commit + FRI commit phase, synthetic 2^{log_n} x {W} trace",
+            "value": round(ms, 3), "unit": "ms", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": False,
+            "scaling": "strong", "vs_baseline": None, "dtype": "u32 (KoalaBear mod-p)",
+            "data": "synthetic: uniform random field words, seeded per rank",
+            "config": {"workload": f"trace 2^{log_n} rows x {W} columns, {wl} per rank; LDE x2, "
+                                   "Merkle commit, FRI fold to a constant",
+                       "parallelism": f"column shards x{world} -> all-to-all -> row shards"},
+            "trace_cells_per_s": round(n * W / (ms * 1e-3), 1),
+            "lde_equiv_gbs": round(lde_bytes / (ms * 1e-3) / 1e9, 1),
+            "fri_rounds": int(len(fri)),
+            "root": [int(x) for x in root],
+        }
+        print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", choices=("replicas", "sharded"), default="replicas",
+    ap.add_argument("--mode", choices=("replicas", "sharded", "pcs"), default="replicas",
                     help="replicas: one independent proof per rank (weak scaling, default); "
-                         "sharded: one proof split across all ranks (strong scaling)")
+                         "sharded: one proof split across all ranks (strong scaling); "
+                         "pcs: column-sharded commit + FRI of a synthetic trace (BASELINE "
+                         "configs 4/5, strong scaling)")
+    ap.add_argument("--log-n", type=int, default=24, help="pcs mode: trace rows = 2^log_n")
+    ap.add_argument("--cols", type=int, default=64, help="pcs mode: trace columns")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    sharded = args.mode == "sharded" and world > 1
+    sharded = args.mode in ("sharded", "pcs") and world > 1
     # gloo prints its connection banner on stdout during init: keep stdout for the JSON line
     sys.stdout.flush()
     saved_stdout = os.dup(1)
@@ -151,6 +202,12 @@ def main():
     # BFZ_DEVICE pins every rank to one GPU (rehearsing --mode sharded on a one-GPU box)
     device = int(os.environ.get("BFZ_DEVICE", local_rank))
     _lib.init(device)
+    if args.mode == "pcs":
+        run_pcs(args, rank, world, device, dist,
+                bfz_shard.Collectives(dist, device=device) if world > 1 else None)
+        if dist:
+            dist.destroy_process_group()
+        return
     L = _lib.lib()
     client = sdk.ProverClient(device=device)
     prog, stdin = guests.FIBO_X4, bytes([255])

@@ -78,22 +78,26 @@ class Collectives:
             return 1
 
 
-def commit_fri_sharded(cols, log_n: int, coll: "Collectives | None", rank: int = 0):
+def commit_fri_sharded(cols, log_n: int, coll: "Collectives | None", rank: int = 0, send=None,
+                       recv=None):
     """bfz_commit_fri_sharded on this rank's columns.
 
     cols: int32 CUDA tensor of shape (w_local, 2^log_n): column-major, bit-reversed rows,
-    Montgomery form, columns [rank w_local, (rank+1) w_local) of the trace.  Returns
+    Montgomery form, columns [rank w_local, (rank+1) w_local) of the trace.  send/recv:
+    optional preallocated int32 CUDA exchange buffers of 2^(log_n+1) * w_local words.  Returns
     (root, fri_roots, final) as uint32 numpy arrays (identical on every rank)."""
     import torch
     L = _lib.lib()
     w_local = cols.shape[0]
     world = coll.world if coll else 1
     n2 = 2 << log_n
-    send = recv = None
     if world > 1:
-        send = torch.empty((w_local * n2,), dtype=torch.int32, device=cols.device)
-        recv = torch.empty_like(send)
+        if send is None or recv is None:
+            send = torch.empty((w_local * n2,), dtype=torch.int32, device=cols.device)
+            recv = torch.empty_like(send)
         coll.exchange = (send, recv)
+    else:
+        send = recv = None
     torch.cuda.synchronize(cols.device)  # cols may still be in flight on torch's stream
     cap = 8 + 8 * (log_n + 1) + 4
     out = (ctypes.c_uint32 * cap)()

@@ -9,9 +9,10 @@
 namespace bfz {
 
 struct MatRef {           // column-major, bit-reversed rows
-  const uint32_t* base;   // column c at base + c * height
+  const uint32_t* base;   // column c at base + c * (stride ? stride : height)
   size_t height;
   int width;
+  size_t stride = 0;
 };
 
 struct MerkleTree {

@@ -13,17 +13,27 @@ namespace bfz {
 
 using namespace kb;
 
-constexpr int MAXCOLS = 160;
+// The columns hashed at one height: up to MAXSEG matrices ("segments"), segment s holding
+// columns [start[s], start[s+1]) at base[s] + (c - start[s]) * stride[s].
+constexpr int MAXSEG = 16;
 struct ColList {
-  const uint32_t* p[MAXCOLS];
+  const uint32_t* base[MAXSEG];
+  size_t stride[MAXSEG];
+  int start[MAXSEG + 1];
+  int nseg;
   int n;
+  __device__ __forceinline__ const uint32_t* col(int c) const {
+    int s = 0;
+    while (s + 1 < nseg && c >= start[s + 1]) s++;
+    return base[s] + (size_t)(c - start[s]) * stride[s];
+  }
 };
 
 __device__ __forceinline__ void sponge_cols(uint32_t st[16], const ColList& cl, size_t row) {
   for (int c0 = 0; c0 < cl.n; c0 += 8) {
 #pragma unroll
     for (int k = 0; k < 8; k++)
-      if (c0 + k < cl.n) st[k] = cl.p[c0 + k][row];
+      if (c0 + k < cl.n) st[k] = cl.col(c0 + k)[row];
     poseidon2_permute(st);
   }
 }
@@ -63,7 +73,7 @@ __device__ __forceinline__ void merkle_node(uint32_t st[16], const ColList& cl, 
       const int cb = c0 + 8 * (step - 1);
 #pragma unroll
       for (int k = 0; k < 8; k++)
-        if (cb + k < c1) st[k] = cl.p[cb + k][j];
+        if (cb + k < c1) st[k] = cl.col(cb + k)[j];
     }
     if (nchunks && step == nchunks + 1) {
 #pragma unroll
@@ -115,7 +125,7 @@ __device__ __forceinline__ uint32_t merkle_node_lane(uint32_t v, const ColList& 
     uint32_t h = 0;
     for (int k = 0; k < nchunks; k++) {  // PaddingFreeSponge, overwrite mode
       const int col = c0 + 8 * k + lane;
-      if (lane < 8 && col < c1) h = cl.p[col][j];
+      if (lane < 8 && col < c1) h = cl.col(col)[j];
       h = poseidon2_permute_lane(h, lane);
     }
     const uint32_t hs = dpp<DPP_ROR8>(h);  // lanes 8..15 <- h[0..7]
@@ -241,11 +251,16 @@ __global__ __launch_bounds__(256) void k_hash_rows8(const uint32_t* __restrict__
 static ColList make_cols(const std::vector<const MatRef*>& ms) {
   ColList cl{};
   cl.n = 0;
-  for (const MatRef* m : ms)
-    for (int c = 0; c < m->width; c++) {
-      if (cl.n >= MAXCOLS) throw std::runtime_error("merkle: too many columns at one height");
-      cl.p[cl.n++] = m->base + (size_t)c * m->height;
-    }
+  cl.nseg = 0;
+  for (const MatRef* m : ms) {
+    if (cl.nseg >= MAXSEG) throw std::runtime_error("merkle: too many matrices at one height");
+    cl.base[cl.nseg] = m->base;
+    cl.stride[cl.nseg] = m->stride ? m->stride : m->height;
+    cl.start[cl.nseg] = cl.n;
+    cl.nseg++;
+    cl.n += m->width;
+  }
+  cl.start[cl.nseg] = cl.n;
   return cl;
 }
 

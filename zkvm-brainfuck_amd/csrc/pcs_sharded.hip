@@ -46,7 +46,7 @@ PcsShardedResult commit_fri_sharded(const uint32_t* cols, int log_n, int w_local
   const ShardCtx* sc = shard_ctx();
   const int G = sc && sc->world > 1 ? sc->world : 1, k = G > 1 ? sc->rank : 0;
   const size_t n = (size_t)1 << log_n, H = 2 * n, blk = H / G;
-  if (w_local < 1 || (size_t)w_local * G > 128) throw std::runtime_error("pcs: 1..128 columns");
+  if (w_local < 1) throw std::runtime_error("pcs: no columns");
   if (G > 1 && blk < SHARD_MIN_LEAVES) throw std::runtime_error("pcs: 2n / world < 1024 rows");
   if (G > 1 && (!send || !recv)) throw std::runtime_error("pcs: exchange buffers missing");
 
@@ -68,13 +68,11 @@ PcsShardedResult commit_fri_sharded(const uint32_t* cols, int log_n, int w_local
   }
   const int W = w_local * G;
 
-  // 3. commit: one width-1 matrix per column; row r of column c sits at
-  //    rows[c * rstride + r - k * blk] (only the rank's rows are read)
+  // 3. commit: one matrix whose row r of column c sits at rows[c * rstride + r - k * blk]
+  //    (only the rank's rows are read)
   PcsShardedResult res;
   {
-    std::vector<MatRef> mats(W);
-    for (int c = 0; c < W; c++)
-      mats[c] = MatRef{rows + (size_t)c * rstride - (size_t)k * blk, H, 1};
+    std::vector<MatRef> mats{MatRef{rows - (size_t)k * blk, H, W, rstride}};
     MerkleTree tree;
     merkle_build(mats, tree, st);
     std::copy(tree.root, tree.root + 8, res.root);
