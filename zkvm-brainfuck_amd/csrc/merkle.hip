@@ -134,15 +134,15 @@ __device__ __forceinline__ uint32_t merkle_node_lane(uint32_t v, const ColList& 
   return v;
 }
 
-// All layers of <= TOP_NODES nodes in one workgroup: layer l reads the previous layer from
-// LDS (the first from HBM), writes its digests to HBM (query paths need every layer) and to
-// LDS for the next.  Layers of <= LANE_NODES nodes switch to lane mode (16 lanes per node):
-// there the permutation latency, not throughput, is the cost.  64 nodes fill the 1024-thread
-// block in one lane-mode pass; larger layers run as k_compress_lanes launches over many CUs
-// (one CU takes ~10 us for a 512-node layer even in single-lane mode, ~4 passes for 256).
-constexpr int TOP_NODES = 64;
-constexpr int LANE_NODES = 64;
-constexpr int MAXTOP = 24;
+// Subtree layers in lane mode (16 lanes per node: the permutation latency, not throughput,
+// is the cost here).  Block b owns TOP_NODES consecutive nodes of the first layer and
+// computes their subtree up to its root: up to TOP_LAYERS layers per launch, every layer but
+// the first read from LDS, every digest written to HBM (query paths need every layer).  A
+// 2^14-node layer takes three such launches (2^14 .. 2^8, 2^7 .. 2^1, 2^0) where one launch
+// per layer took eight; with fewer than TOP_NODES nodes a single block finishes the tree.
+constexpr int TOP_NODES = 64;  // fills a 1024-thread block in one lane-mode pass
+constexpr int TOP_LAYERS = 7;  // 64 nodes -> 1
+constexpr int MAXTOP = TOP_LAYERS;
 struct TopLayers {
   uint32_t* out[MAXTOP];
   int c0[MAXTOP], c1[MAXTOP];
@@ -151,37 +151,20 @@ struct TopLayers {
 
 __global__ __launch_bounds__(1024) void k_compress_top(const uint32_t* __restrict__ prev,
                                                        size_t nlen, ColList inj, TopLayers tl) {
-  __shared__ uint4 buf[2][TOP_NODES * 2];
-  for (int l = 0; l < tl.n; l++, nlen >>= 1) {
-    const uint32_t* src32 = l == 0 ? prev : reinterpret_cast<const uint32_t*>(buf[(l - 1) & 1]);
-    uint32_t* dst32 = reinterpret_cast<uint32_t*>(buf[l & 1]);
-    if (nlen <= (size_t)LANE_NODES) {
-      const int lane = threadIdx.x & 15;
-      for (size_t j = threadIdx.x >> 4; j < nlen; j += blockDim.x >> 4) {
-        // whole 16-lane rows are active together (DPP needs all of them)
-        const uint32_t v = merkle_node_lane(src32[16 * j + lane], inj, tl.c0[l], tl.c1[l], j, lane);
-        if (lane < 8) {
-          tl.out[l][8 * j + lane] = v;
-          dst32[8 * j + lane] = v;
-        }
-      }
-    } else {
-      for (size_t j = threadIdx.x; j < nlen; j += blockDim.x) {
-        uint32_t st[16];
-        if (l == 0) {
-          load16(st, prev + 16 * j);
-        } else {
-          const uint4* s4 = buf[(l - 1) & 1] + 4 * j;
-          const uint4 a = s4[0], b = s4[1], c = s4[2], d = s4[3];
-          st[0] = a.x; st[1] = a.y; st[2] = a.z; st[3] = a.w;
-          st[4] = b.x; st[5] = b.y; st[6] = b.z; st[7] = b.w;
-          st[8] = c.x; st[9] = c.y; st[10] = c.z; st[11] = c.w;
-          st[12] = d.x; st[13] = d.y; st[14] = d.z; st[15] = d.w;
-        }
-        merkle_node(st, inj, tl.c0[l], tl.c1[l], j);
-        store8(tl.out[l] + 8 * j, st);
-        buf[l & 1][2 * j] = make_uint4(st[0], st[1], st[2], st[3]);
-        buf[l & 1][2 * j + 1] = make_uint4(st[4], st[5], st[6], st[7]);
+  __shared__ uint32_t buf[2][TOP_NODES * 8];
+  const size_t per = nlen < (size_t)TOP_NODES ? nlen : (size_t)TOP_NODES;
+  const size_t g0 = (size_t)blockIdx.x * per;  // first-layer node of this block
+  const int lane = threadIdx.x & 15;
+  for (int l = 0; l < tl.n; l++) {
+    const size_t m = per >> l, g = g0 >> l;
+    const uint32_t* src = l == 0 ? prev + 16 * g : buf[(l - 1) & 1];
+    uint32_t* dst = buf[l & 1];
+    // whole 16-lane rows are active together (DPP needs all of them)
+    for (size_t j = threadIdx.x >> 4; j < m; j += blockDim.x >> 4) {
+      const uint32_t v = merkle_node_lane(src[16 * j + lane], inj, tl.c0[l], tl.c1[l], g + j, lane);
+      if (lane < 8) {
+        tl.out[l][8 * (g + j) + lane] = v;
+        dst[8 * j + lane] = v;
       }
     }
     __syncthreads();
@@ -290,7 +273,7 @@ static void build_layers(MerkleTree& t, int L0, size_t len, const std::vector<co
                          size_t next, hipStream_t st, bool fetch_root = true) {
   const int nl = (int)t.layers.size() - 1;
   int L = L0;
-  for (; L <= nl && (len >> 1) > (size_t)TOP_NODES; L++) {
+  for (; L <= nl && (len >> 1) > LANE_LAYER_MAX; L++) {  // throughput layers
     const size_t nlen = len >> 1;
     std::vector<const MatRef*> grp;
     while (next < sorted.size() && sorted[next]->height == nlen) grp.push_back(sorted[next++]);
@@ -298,12 +281,13 @@ static void build_layers(MerkleTree& t, int L0, size_t len, const std::vector<co
     launch_layer(t, L, 0, nlen, grp, st);
     len = nlen;
   }
-  if (L <= nl) {
+  while (L <= nl) {  // subtree launches of up to TOP_LAYERS layers each
+    const size_t first = len >> 1;
+    const int maxl = first > (size_t)TOP_NODES ? TOP_LAYERS : log2i(first) + 1;
     TopLayers tl{};
-    tl.n = nl - L + 1;
-    if (tl.n > MAXTOP) throw std::runtime_error("merkle: too many top layers");
+    tl.n = std::min(maxl, nl - L + 1);
     std::vector<const MatRef*> all;
-    size_t nlen = len >> 1;
+    size_t nlen = first;
     for (int l = 0; l < tl.n; l++, nlen >>= 1) {
       tl.c0[l] = 0;
       for (const MatRef* m : all) tl.c0[l] += m->width;
@@ -313,9 +297,12 @@ static void build_layers(MerkleTree& t, int L0, size_t len, const std::vector<co
       t.layers[L + l].reset(8 * nlen);
       tl.out[l] = t.layers[L + l].p;
     }
-    hipLaunchKernelGGL(k_compress_top, dim3(1), dim3(1024), 0, st,
-                       (const uint32_t*)t.layers[L - 1].p, len >> 1, make_cols(all), tl);
+    const unsigned blocks = first > (size_t)TOP_NODES ? (unsigned)(first / TOP_NODES) : 1u;
+    hipLaunchKernelGGL(k_compress_top, dim3(blocks), dim3(1024), 0, st,
+                       (const uint32_t*)t.layers[L - 1].p, first, make_cols(all), tl);
     KCHECK();
+    L += tl.n;
+    len = first >> (tl.n - 1);
   }
   if (next != sorted.size()) throw std::runtime_error("merkle: non power-of-two heights");
   if (!fetch_root) return;

@@ -99,6 +99,11 @@ constexpr SmallRoots make_small_roots() {
 constexpr SmallRoots SMALL = make_small_roots();
 
 constexpr int R16_TILE_LOG = 14;  // 16384 elements per tile, 1024 threads x 16
+// Second-pass tiles take 2^c adjacent columns (2^c * 4 B coalesced runs); c <= MID_CMAX.
+#ifndef BFZ_MID_CMAX
+#define BFZ_MID_CMAX 5
+#endif
+constexpr int MID_CMAX = BFZ_MID_CMAX;
 
 __device__ __forceinline__ int lds_pad(int idx, int c) { return c < 5 ? idx + (idx >> 4) : idx; }
 
@@ -305,8 +310,8 @@ template <int L>
 struct MidPlan {
   static constexpr int b1 = L - 4 < R16_TILE_LOG ? L - 4 : R16_TILE_LOG;
   static constexpr int b2 = L - b1;
-  static constexpr int c2 = b1 < R16_TILE_LOG - b2 ? (b1 < 6 ? b1 : 6)
-                                                  : (R16_TILE_LOG - b2 < 6 ? R16_TILE_LOG - b2 : 6);
+  static constexpr int c2 = b1 < R16_TILE_LOG - b2 ? (b1 < MID_CMAX ? b1 : MID_CMAX)
+                                                  : (R16_TILE_LOG - b2 < MID_CMAX ? R16_TILE_LOG - b2 : MID_CMAX);
 };
 
 template <int L>
@@ -473,7 +478,7 @@ struct R16Pass {
 static std::vector<R16Pass> r16_plan(int L) {
   if (L <= R16_TILE_LOG) return {{0, L, 0}};
   const int b1 = std::min(R16_TILE_LOG, L - 4), b2 = L - b1;
-  const int c2 = std::min({b1, R16_TILE_LOG - b2, 6});
+  const int c2 = std::min({b1, R16_TILE_LOG - b2, MID_CMAX});
   return {{0, b1, 0}, {b1, b2, c2}};
 }
 
