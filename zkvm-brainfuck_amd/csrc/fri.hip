@@ -186,12 +186,20 @@ __global__ __launch_bounds__(256) void k_reduce(const RedCol* __restrict__ cols,
       acc.init();
       const int end = rm.first + rm.count;
       int c = rm.first;
-      for (; c + 4 <= end; c += 4) {  // four column loads in flight per step
+      for (; c + 8 <= end; c += 8) {  // eight column loads in flight per step
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = cols[c + k].col[t];
+#pragma unroll
+        for (int k = 0; k < 8; k++) acc.add(cols[c + k].ca, v[k]);
+      }
+      if (c + 4 <= end) {
         uint32_t v[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) v[k] = cols[c + k].col[t];
 #pragma unroll
         for (int k = 0; k < 4; k++) acc.add(cols[c + k].ca, v[k]);
+        c += 4;
       }
       for (; c < end; c++) acc.add(cols[c].ca, cols[c].col[t]);
       const EF s = acc.get();

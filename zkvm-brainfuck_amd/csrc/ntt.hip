@@ -98,7 +98,10 @@ constexpr SmallRoots make_small_roots() {
 }
 constexpr SmallRoots SMALL = make_small_roots();
 
-constexpr int R16_TILE_LOG = 14;  // 16384 elements per tile, 1024 threads x 16
+#ifndef BFZ_TILE_LOG
+#define BFZ_TILE_LOG 14
+#endif
+constexpr int R16_TILE_LOG = BFZ_TILE_LOG;  // 2^14 elements per tile: 1024 threads x 16
 // Second-pass tiles take 2^c adjacent columns (2^c * 4 B coalesced runs); c <= MID_CMAX.
 #ifndef BFZ_MID_CMAX
 #define BFZ_MID_CMAX 5
@@ -490,16 +493,16 @@ static void r16_attrs() {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_r16<false>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-  const void* mids[] = {(const void*)&k_lde_mid<15>, (const void*)&k_lde_mid<16>,
+  const void* mids[] = {(const void*)&k_lde_mid<14>, (const void*)&k_lde_mid<15>, (const void*)&k_lde_mid<16>,
                         (const void*)&k_lde_mid<17>, (const void*)&k_lde_mid<18>,
                         (const void*)&k_lde_mid<19>, (const void*)&k_lde_mid<20>,
                         (const void*)&k_lde_mid<21>, (const void*)&k_lde_mid<22>,
                         (const void*)&k_lde_mid<23>};
   for (const void* f : mids)
     HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<true, 14>),
+  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<true, R16_TILE_LOG>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<false, 14>),
+  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<false, R16_TILE_LOG>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   done = true;
 }
@@ -522,7 +525,12 @@ static bool tile_dispatch(int b, dim3 grid, const uint32_t* in, size_t is, uint3
     case 11: tile_launch<DIF, 11>(grid, in, is, dst, ds, tw, st); return true;
     case 12: tile_launch<DIF, 12>(grid, in, is, dst, ds, tw, st); return true;
     case 13: tile_launch<DIF, 13>(grid, in, is, dst, ds, tw, st); return true;
-    case 14: tile_launch<DIF, 14>(grid, in, is, dst, ds, tw, st); return true;
+    case 14:
+      if constexpr (R16_TILE_LOG >= 14) {
+        tile_launch<DIF, 14>(grid, in, is, dst, ds, tw, st);
+        return true;
+      }
+      return false;
   }
   return false;
 }
@@ -661,7 +669,7 @@ void coset_lde(const uint32_t* evals, size_t n, int w, uint32_t shift, uint32_t*
                        n, lde, n, (const uint32_t*)T.inv.p, (const uint32_t*)T.fwd.p, pw, B, mp); \
     break;
     switch (L) {
-      BFZ_MID(15) BFZ_MID(16) BFZ_MID(17) BFZ_MID(18) BFZ_MID(19) BFZ_MID(20) BFZ_MID(21)
+      BFZ_MID(14) BFZ_MID(15) BFZ_MID(16) BFZ_MID(17) BFZ_MID(18) BFZ_MID(19) BFZ_MID(20) BFZ_MID(21)
       BFZ_MID(22) BFZ_MID(23)
       default: throw std::runtime_error("coset_lde: log height above 23");
     }
