@@ -201,3 +201,27 @@ def test_invalid_trace_rejected_by_verifiers(client):
     with pytest.raises(_lib.BfzError, match="OOD evaluation mismatch"):
         client.verify(pf, vk)
     assert not O.verify(prog, pf.proof)
+
+
+def test_cpu_2pow23_proves_but_verifier_bounds_degree(client):
+    """Largest provable size: 8 outer fibonacci loops (~7.5 M cycles) give a 2^23-row Cpu
+    trace, whose LDE (2^24 rows) is KoalaBear's full two-adic subgroup.  The prover handles it;
+    the verifier rejects Cpu log degree 23 > MAX_CPU_LOG_DEGREE = 22 exactly as
+    crates/prover/src/verify.rs:20-28 (CpuLogDegreeTooLarge)."""
+    prog = "++++++++[>" + guests.FIBO + "[-]<[-]<<-]"
+    pk, vk = client.setup(prog)
+    pf = client.prove(pk, [255]).run()
+    with pytest.raises(_lib.BfzError, match="Cpu log degree too large"):
+        client.verify(pf, vk)
+
+
+def test_trace_beyond_two_adicity_is_an_error(client):
+    """16 outer loops (~15 M cycles) need a 2^24-row Cpu trace and a 2^25-point LDE, beyond
+    the 2^24-element two-adic subgroup of KoalaBear (p - 1 = 127 * 2^24): a clean error, no
+    device fault, and the library keeps working afterwards."""
+    prog = "++++++++++++++++[>" + guests.FIBO + "[-]<[-]<<-]"
+    pk, vk = client.setup(prog)
+    with pytest.raises(_lib.BfzError):
+        client.prove(pk, [255]).run()
+    pk2, vk2 = client.setup(guests.FIBO)
+    client.verify(client.prove(pk2, [17]).run(), vk2)
