@@ -125,27 +125,21 @@ __global__ __launch_bounds__(256) void k_perm_rows(const uint32_t* __restrict__ 
   rowsum[t] = sum;
 }
 
-__global__ __launch_bounds__(256) void k_gather_bitrev_ef(const EF* __restrict__ in,
-                                                          EF* __restrict__ out, size_t n,
-                                                          int logn) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = in[dbitrev((uint32_t)i, logn)];
-}
-
-// perm last EF column (4 base columns starting at col0) <- phi_nat[bitrev(t)]
-__global__ __launch_bounds__(256) void k_write_phi(const EF* __restrict__ phi, size_t n, int logn,
-                                                   uint32_t* __restrict__ perm, int col0) {
-  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
-  const EF v = phi[dbitrev((uint32_t)t, logn)];
-#pragma unroll
-  for (int e = 0; e < 4; e++) perm[(size_t)(col0 + e) * n + t] = v.c[e];
-}
+// perm last EF column (4 base columns from col0) at storage position t <- phi(i), i = bitrev(t):
+// phi(i) = block-local inclusive sum + the prefix of the blocks before (scan of block sums).
+// The row t = n - 1 (= bitrev(n - 1)) also holds the cumulative sum.
+__global__ __launch_bounds__(256) void k_write_phi(const EF* __restrict__ local, size_t n, int logn,
+                                                   const EF* __restrict__ block_prefix,
+                                                   uint32_t* __restrict__ perm, int col0,
+                                                   EF* __restrict__ cumsum);
 
 // --------------------------------------------------------------------- EF prefix scan
 constexpr int SCAN_T = 256, SCAN_PER = 8, SCAN_BLOCK = SCAN_T * SCAN_PER;
 
-__global__ __launch_bounds__(SCAN_T) void k_scan_block(EF* __restrict__ data, size_t n,
+// Block-local inclusive scan of natural-order blocks of SCAN_BLOCK values.  With logn >= 0 the
+// input is read from bit-reversed storage (in[bitrev(i)]: the LogUp row sums), else in place.
+__global__ __launch_bounds__(SCAN_T) void k_scan_block(const EF* __restrict__ in, int logn,
+                                                       EF* __restrict__ data, size_t n,
                                                        EF* __restrict__ block_sums) {
   __shared__ EF sh[SCAN_T];
   const size_t base = (size_t)blockIdx.x * SCAN_BLOCK + (size_t)threadIdx.x * SCAN_PER;
@@ -153,7 +147,8 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_block(EF* __restrict__ data, si
   EF run = ef_zero();
 #pragma unroll
   for (int k = 0; k < SCAN_PER; k++) {
-    v[k] = base + k < n ? data[base + k] : ef_zero();
+    const size_t i = base + k;
+    v[k] = i < n ? in[logn >= 0 ? dbitrev((uint32_t)i, logn) : i] : ef_zero();
     run = ef_add(run, v[k]);
     v[k] = run;
   }
@@ -184,7 +179,8 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_add(EF* __restrict__ data, size
 void ef_inclusive_scan(EF* data, size_t n, hipStream_t st) {
   const size_t nb = (n + SCAN_BLOCK - 1) / SCAN_BLOCK;
   DBuf<EF> sums(nb);
-  hipLaunchKernelGGL(k_scan_block, dim3((unsigned)nb), dim3(SCAN_T), 0, st, data, n, sums.p);
+  hipLaunchKernelGGL(k_scan_block, dim3((unsigned)nb), dim3(SCAN_T), 0, st, (const EF*)data, -1,
+                     data, n, sums.p);
   KCHECK();
   if (nb > 1) {
     ef_inclusive_scan(sums.p, nb, st);
@@ -217,15 +213,34 @@ void perm_trace(int chip, const uint32_t* mainc, const uint32_t* prepc, size_t n
     case CHIP_IO: launch_rows<CHIP_IO>(mainc, prepc, n, ch, perm, rows.p, st); break;
     default: throw std::runtime_error("perm_trace: bad chip");
   }
-  hipLaunchKernelGGL(k_gather_bitrev_ef, dim3(ceil_div(n, 256)), dim3(256), 0, st,
-                     (const EF*)rows.p, nat.p, n, logn);
+  // running sum in natural row order: block-local scans read the bit-reversed row sums
+  // directly, the block sums are scanned, and k_write_phi adds each block's prefix while
+  // scattering phi back to bit-reversed storage
+  const size_t nb = (n + SCAN_BLOCK - 1) / SCAN_BLOCK;
+  DBuf<EF> sums(nb);
+  hipLaunchKernelGGL(k_scan_block, dim3((unsigned)nb), dim3(SCAN_T), 0, st, (const EF*)rows.p,
+                     logn, nat.p, n, sums.p);
   KCHECK();
-  ef_inclusive_scan(nat.p, n, st);
+  if (nb > 1) ef_inclusive_scan(sums.p, nb, st);
   const int col0 = 4 * (perm_width(chip) - 1);
   hipLaunchKernelGGL(k_write_phi, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const EF*)nat.p, n,
-                     logn, perm, col0);
+                     logn, nb > 1 ? (const EF*)sums.p : nullptr, perm, col0, cumsum_dev);
   KCHECK();
-  HIP_CHECK(hipMemcpyAsync(cumsum_dev, nat.p + (n - 1), sizeof(EF), hipMemcpyDeviceToDevice, st));
+}
+
+__global__ __launch_bounds__(256) void k_write_phi(const EF* __restrict__ local, size_t n, int logn,
+                                                   const EF* __restrict__ block_prefix,
+                                                   uint32_t* __restrict__ perm, int col0,
+                                                   EF* __restrict__ cumsum) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const size_t i = dbitrev((uint32_t)t, logn);
+  EF v = local[i];
+  const size_t b = i / SCAN_BLOCK;
+  if (block_prefix && b > 0) v = ef_add(v, block_prefix[b - 1]);
+#pragma unroll
+  for (int e = 0; e < 4; e++) perm[(size_t)(col0 + e) * n + t] = v.c[e];
+  if (t == n - 1) *cumsum = v;
 }
 
 }  // namespace bfz

@@ -66,6 +66,21 @@ bool Challenger::check_witness(int bits, uint32_t w) {
 }
 
 // ------------------------------------------------------------------------ timing
+constexpr int MAX_FRI_ROUNDS = 32;
+struct FriTail {
+  const uint32_t* root[MAX_FRI_ROUNDS];
+  int nroots;
+  const uint32_t* state;
+  const EF* fin;
+};
+// packed = [root 0 .. root MAX-1 (8 words each) | state (16) | final layer (2 EF)]
+__global__ void k_pack_fri_tail(FriTail t, uint32_t* __restrict__ packed) {
+  const int i = threadIdx.x;
+  if (i < 8 * t.nroots) packed[i] = t.root[i >> 3][i & 7];
+  if (i < 16) packed[8 * MAX_FRI_ROUNDS + i] = t.state[i];
+  if (i < 8) packed[8 * MAX_FRI_ROUNDS + 16 + i] = t.fin[i >> 2].c[i & 3];
+}
+
 namespace {
 struct EvTimer {
   bool on = false;
@@ -486,13 +501,26 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
     layers.push_back(std::move(next));
     len = h;
   }
-  for (MerkleTree& t : trees)
-    HIP_CHECK(hipMemcpyAsync(t.root, t.layers.back().p, 32, hipMemcpyDeviceToHost, st));
-  uint32_t st_after[16];
-  HIP_CHECK(hipMemcpyAsync(st_after, dstate.p, 64, hipMemcpyDeviceToHost, st));
-  EF fin[2];
-  HIP_CHECK(hipMemcpyAsync(fin, layers.back().p, 2 * sizeof(EF), hipMemcpyDeviceToHost, st));
+  // one device-to-host copy for the commit-phase roots, the transcript state and the final
+  // layer (small copies each cost a copy-kernel launch)
+  const int nt = (int)trees.size();
+  if (nt > MAX_FRI_ROUNDS) throw std::runtime_error("FRI: too many rounds");
+  FriTail tail{};
+  for (int i = 0; i < nt; i++) tail.root[i] = trees[i].layers.back().p;
+  tail.nroots = nt;
+  tail.state = dstate.p;
+  tail.fin = layers.back().p;
+  DBuf<uint32_t> packed(8 * MAX_FRI_ROUNDS + 16 + 8);
+  hipLaunchKernelGGL(k_pack_fri_tail, dim3(1), dim3(256), 0, st, tail, packed.p);
+  KCHECK();
+  std::vector<uint32_t> hp(packed.n);
+  HIP_CHECK(hipMemcpyAsync(hp.data(), packed.p, packed.n * 4, hipMemcpyDeviceToHost, st));
   HIP_CHECK(hipStreamSynchronize(st));
+  for (int i = 0; i < nt; i++) std::memcpy(trees[i].root, &hp[8 * i], 32);
+  uint32_t st_after[16];
+  std::memcpy(st_after, &hp[8 * MAX_FRI_ROUNDS], 64);
+  EF fin[2];
+  std::memcpy(fin, &hp[8 * MAX_FRI_ROUNDS + 16], sizeof(fin));
   if (!trees.empty()) {  // host challenger = state after the last round's duplex, 4 outputs left
     for (int i = 0; i < 16; i++) ch.st[i] = st_after[i];
     for (int i = 0; i < 8; i++) ch.out[i] = st_after[i];
