@@ -107,6 +107,10 @@ constexpr int R16_TILE_LOG = BFZ_TILE_LOG;  // 2^14 elements per tile: 1024 thre
 #define BFZ_MID_CMAX 5
 #endif
 constexpr int MID_CMAX = BFZ_MID_CMAX;
+#ifndef BFZ_MID_TW_LOAD
+#define BFZ_MID_TW_LOAD 1
+#endif
+constexpr bool MID_TW_LOAD = BFZ_MID_TW_LOAD;
 
 __device__ __forceinline__ int lds_pad(int idx, int c) { return c < 5 ? idx + (idx >> 4) : idx; }
 
@@ -133,11 +137,11 @@ __device__ __forceinline__ void r16_window(uint32_t (&x)[16], int g0, int kk_lo,
 #pragma unroll
       for (int l = 0; l < 8; l++)
         if (l < (1 << kk)) tws[l] = DIF ? SMALL.f[(1 << kk) + l] : SMALL.i[(1 << kk) + l];
-    } else if (TW_LOAD) {
-      const uint32_t* tt = tw + (1u << (g0 + kk)) + m_low;
+    } else if (TW_LOAD) {  // one table load per twiddle instead of a load and a multiply
+      const uint32_t* tt = tw + (1u << (s0 + g0 + kk)) + ((size_t)m_low << s0) + lo_g;
 #pragma unroll
       for (int l = 0; l < 8; l++)
-        if (l < (1 << kk)) tws[l] = tt[l << g0];
+        if (l < (1 << kk)) tws[l] = tt[(size_t)l << (g0 + s0)];
     } else {
       const int t = g0 + kk;
       const uint32_t wb = tw[(1u << (s0 + t)) + (m_low << s0) + lo_g];
@@ -353,7 +357,7 @@ __global__ __launch_bounds__(1 << (MidPlan<L>::b2 + MidPlan<L>::c2 - 4)) void k_
     }
     const int kk_lo = max(0, done_lo - g0);
     done_lo = g0 + 4;
-    r16_window<false, false>(x, g0, kk_lo, 4, s0, m_low, lo_g, tw_inv);
+    r16_window<false, false, MID_TW_LOAD>(x, g0, kk_lo, 4, s0, m_low, lo_g, tw_inv);
     if (w < nwin - 1) {
 #pragma unroll
       for (int i = 0; i < 16; i++)
@@ -390,7 +394,7 @@ __global__ __launch_bounds__(1 << (MidPlan<L>::b2 + MidPlan<L>::c2 - 4)) void k_
         }
         const int kk_hi = min(4, done_hi - gg);
         done_hi = gg;
-        r16_window<true, false>(x, gg, 0, kk_hi, s0, m_low, lo_g, tw_fwd);
+        r16_window<true, false, MID_TW_LOAD>(x, gg, 0, kk_hi, s0, m_low, lo_g, tw_fwd);
         if (w == nwin - 1) {
 #pragma unroll
           for (int i = 0; i < 16; i++) Dh[(uint32_t)((mb | ((uint32_t)i << gg)) << s0) + lo] = x[i];
