@@ -46,10 +46,18 @@ void poseidon2_batch(uint32_t* states, size_t n, hipStream_t st);
 // Same, latency-optimised (16 lanes per state; for few states).
 void poseidon2_batch_small(uint32_t* states, size_t n, hipStream_t st);
 
-// Tree over h rows of 8 elements (FRI commit-phase leaves: pairs of EF values, one
+// FRI transcript step fused into the launch that finishes a root: with state != nullptr the
+// device DuplexChallenger state observes the root, duplexes, and beta receives the 4 outputs a
+// sample_ef pops (see k_fri_challenge).
+struct RootChallenge {
+  uint32_t* state = nullptr;
+  kb::EF* beta = nullptr;
+};
+
+// Tree over h >= 2 rows of 8 elements (FRI commit-phase leaves: pairs of EF values, one
 // permutation each).  With fetch_root = false the root stays on the device
 // (tree.layers.back()) and tree.root is not filled.
 void merkle_from_rows8(MerkleTree& tree, const uint32_t* rows, size_t h, hipStream_t st,
-                       bool fetch_root = true);
+                       bool fetch_root = true, RootChallenge rc = {});
 
 }  // namespace bfz

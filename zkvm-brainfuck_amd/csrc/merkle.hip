@@ -150,7 +150,8 @@ struct TopLayers {
 };
 
 __global__ __launch_bounds__(1024) void k_compress_top(const uint32_t* __restrict__ prev,
-                                                       size_t nlen, ColList inj, TopLayers tl) {
+                                                       size_t nlen, ColList inj, TopLayers tl,
+                                                       RootChallenge rc) {
   __shared__ uint32_t buf[2][TOP_NODES * 8];
   const size_t per = nlen < (size_t)TOP_NODES ? nlen : (size_t)TOP_NODES;
   const size_t g0 = (size_t)blockIdx.x * per;  // first-layer node of this block
@@ -168,6 +169,17 @@ __global__ __launch_bounds__(1024) void k_compress_top(const uint32_t* __restric
       }
     }
     __syncthreads();
+  }
+  // FRI transcript step on the finished root (the root's block only): observe the root,
+  // duplex, beta = the last 4 outputs popped in reverse (as k_fri_challenge)
+  if (rc.state && threadIdx.x < 64) {
+    const uint32_t* root = buf[(tl.n - 1) & 1];
+    uint32_t v = lane < 8 ? root[lane] : rc.state[lane];
+    v = poseidon2_permute_lane(v, lane);
+    if (threadIdx.x < 16) {
+      rc.state[lane] = v;
+      if (lane >= 4 && lane < 8) rc.beta->c[7 - lane] = v;
+    }
   }
 }
 
@@ -270,7 +282,8 @@ static void launch_layer(MerkleTree& t, int L, size_t j0, size_t count,
 // still to inject (heights descending).  Big layers get one launch each; the rest go to
 // k_compress_top in one launch.
 static void build_layers(MerkleTree& t, int L0, size_t len, const std::vector<const MatRef*>& sorted,
-                         size_t next, hipStream_t st, bool fetch_root = true) {
+                         size_t next, hipStream_t st, bool fetch_root = true,
+                         RootChallenge rc = {}) {
   const int nl = (int)t.layers.size() - 1;
   int L = L0;
   for (; L <= nl && (len >> 1) > LANE_LAYER_MAX; L++) {  // throughput layers
@@ -298,8 +311,10 @@ static void build_layers(MerkleTree& t, int L0, size_t len, const std::vector<co
       tl.out[l] = t.layers[L + l].p;
     }
     const unsigned blocks = first > (size_t)TOP_NODES ? (unsigned)(first / TOP_NODES) : 1u;
+    const bool root_launch = L + tl.n > nl;
     hipLaunchKernelGGL(k_compress_top, dim3(blocks), dim3(1024), 0, st,
-                       (const uint32_t*)t.layers[L - 1].p, first, make_cols(all), tl);
+                       (const uint32_t*)t.layers[L - 1].p, first, make_cols(all), tl,
+                       root_launch ? rc : RootChallenge{});
     KCHECK();
     L += tl.n;
     len = first >> (tl.n - 1);
@@ -326,7 +341,8 @@ static bool shard_tree(size_t h0) {
 // it are built redundantly by every rank.  leaves(r0, count) hashes the rank's own rows.
 template <class Leaves>
 static void build_sharded(MerkleTree& t, size_t h0, const std::vector<const MatRef*>& sorted,
-                          size_t next, Leaves leaves, hipStream_t st, bool fetch_root) {
+                          size_t next, Leaves leaves, hipStream_t st, bool fetch_root,
+                          RootChallenge rc = {}) {
   const ShardCtx& c = *shard_ctx();
   const size_t G = (size_t)c.world, k = (size_t)c.rank;
   const int nl = log2i(h0), lg = log2i(G);
@@ -350,7 +366,7 @@ static void build_sharded(MerkleTree& t, size_t h0, const std::vector<const MatR
   c.allgather(mine, 32, all.data());
   HIP_CHECK(hipMemcpyAsync(lay.p, all.data(), all.size() * 4, hipMemcpyHostToDevice, st));
   HIP_CHECK(hipStreamSynchronize(st));  // `all` goes out of scope
-  build_layers(t, nl - lg + 1, G, sorted, next, st, fetch_root);
+  build_layers(t, nl - lg + 1, G, sorted, next, st, fetch_root, rc);
 }
 
 void merkle_build(const std::vector<MatRef>& mats, MerkleTree& t, hipStream_t st) {
@@ -401,7 +417,7 @@ static void hash_rows8_range(const uint32_t* rows, size_t r0, size_t count, uint
 }
 
 void merkle_from_rows8(MerkleTree& t, const uint32_t* rows, size_t h, hipStream_t st,
-                       bool fetch_root) {
+                       bool fetch_root, RootChallenge rc) {
   t.mats = {MatRef{rows, h, 8}};
   t.layers.clear();
   t.layers.resize(log2i(h) + 1);
@@ -410,12 +426,13 @@ void merkle_from_rows8(MerkleTree& t, const uint32_t* rows, size_t h, hipStream_
   auto leaves = [&](size_t r0, size_t count) {
     hash_rows8_range(rows, r0, count, t.layers[0].p, st);
   };
+  if (h < 2) throw std::runtime_error("merkle: rows8 tree needs two leaves");
   if (shard_tree(h)) {
-    build_sharded(t, h, {}, 0, leaves, st, fetch_root);
+    build_sharded(t, h, {}, 0, leaves, st, fetch_root, rc);
     return;
   }
   leaves(0, h);
-  build_layers(t, 1, h, {}, 0, st, fetch_root);
+  build_layers(t, 1, h, {}, 0, st, fetch_root, rc);
 }
 
 void poseidon2_batch(uint32_t* states, size_t n, hipStream_t st) {

@@ -115,8 +115,8 @@ PcsShardedResult commit_fri_sharded(const uint32_t* cols, int log_n, int w_local
     const size_t i0 = local ? (size_t)k * (h / G) : 0, cnt = local ? h / G : h;
     trees.emplace_back();
     MerkleTree& t = trees.back();
-    merkle_from_rows8(t, reinterpret_cast<const uint32_t*>(cur.p) - 8 * i0, h, st, false);
-    fri_challenge(dstate.p, t.layers.back().p, betas.p + rd, st);
+    merkle_from_rows8(t, reinterpret_cast<const uint32_t*>(cur.p) - 8 * i0, h, st, false,
+                      RootChallenge{dstate.p, betas.p + rd});
     DBuf<EF> next(cnt);
     fri_fold_range(cur.p, next.p, h, i0, cnt, betas.p + rd, nullptr, st);
     cur = std::move(next);

@@ -492,8 +492,8 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
     const size_t h = len / 2;
     trees.emplace_back();
     MerkleTree& t = trees.back();
-    merkle_from_rows8(t, (const uint32_t*)layers.back().p, h, st, /*fetch_root=*/false);
-    fri_challenge(dstate.p, t.layers.back().p, betas.p + rd, st);
+    merkle_from_rows8(t, (const uint32_t*)layers.back().p, h, st, /*fetch_root=*/false,
+                      RootChallenge{dstate.p, betas.p + rd});
     DBuf<EF> next(h);
     const int lgh = log2i(h);
     const EF* add = ro.count(lgh) ? ro.at(lgh).p : nullptr;
