@@ -1,0 +1,46 @@
+// NTT tile-pass rate with the data L2/MALL-resident vs streamed from HBM, to separate the
+// kernel's compute ceiling from its memory overlap.  Links against libbfz.so (bfz::ntt_passes).
+// Build: hipcc --offload-arch=gfx950 -O2 -I zkvm-brainfuck_amd/csrc scripts/ubench_ntt.cpp \
+//          -L zkvm-brainfuck_amd -lbfz -Wl,-rpath,$PWD/zkvm-brainfuck_amd -o /tmp/ubench_ntt
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <vector>
+
+#include "ntt.h"
+
+#define CHK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s\n", hipGetErrorString(e)); return 1; } } while (0)
+
+int main() {
+  const int L = 14;
+  const size_t n = (size_t)1 << L;
+  hipStream_t st = bfz::stream();
+  for (int w : {16, 64, 256, 4096}) {
+    const size_t words = n * (size_t)w;
+    uint32_t *a, *b;
+    CHK(hipMalloc(&a, words * 4));
+    CHK(hipMalloc(&b, words * 4));
+    std::vector<uint32_t> h(words);
+    for (size_t i = 0; i < words; i++) h[i] = (uint32_t)((i * 2654435761u) % 0x7f000001u);
+    CHK(hipMemcpy(a, h.data(), words * 4, hipMemcpyHostToDevice));
+    for (int dif = 0; dif < 2; dif++) {
+      bfz::ntt_passes(a, b, n, n, w, L, dif, st);
+      CHK(hipStreamSynchronize(st));
+      hipEvent_t e0, e1;
+      CHK(hipEventCreate(&e0));
+      CHK(hipEventCreate(&e1));
+      const int reps = w >= 4096 ? 20 : 400;
+      CHK(hipEventRecord(e0, st));
+      for (int r = 0; r < reps; r++) bfz::ntt_passes(a, b, n, n, w, L, dif, st);
+      CHK(hipEventRecord(e1, st));
+      CHK(hipEventSynchronize(e1));
+      float ms;
+      CHK(hipEventElapsedTime(&ms, e0, e1));
+      const double s = ms * 1e-3 / reps;
+      printf("L=%d w=%5d (%7.1f MB) %s: %8.2f us/pass  %7.1f G elem/s  %7.0f GB/s (8 B/elem)\n", L, w,
+             words * 4 / 1e6, dif ? "DIF" : "DIT", s * 1e6, words / s / 1e9, 8.0 * words / s / 1e9);
+    }
+    CHK(hipFree(a));
+    CHK(hipFree(b));
+  }
+  return 0;
+}
