@@ -49,3 +49,48 @@ def test_timed_steps_two_gloo_ranks_take_max():
     assert n0 == n1 == 3            # exactly K steps on every rank
     assert ms0 == ms1               # every rank reports the same (max) value
     assert ms0 >= 40.0              # ... which is the slow rank's pace
+
+
+def _coll_rank(rank, world, port, q):
+    """The host side of the sharded prover's two exchanges (bfz/shard.py Collectives), driven
+    through the same ctypes callback objects libbfz calls, on a gloo group (no GPU)."""
+    import ctypes
+
+    import numpy as np
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(ROOT, "zkvm-brainfuck_amd"))
+    from bfz import shard
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    coll = shard.Collectives(dist)
+    # all-gather of 32-byte subtree roots: rank r sends its own digest
+    send = np.arange(1, 9, dtype=np.uint32) + 1000 * rank
+    recv = np.zeros(8 * world, dtype=np.uint32)
+    rc_ag = coll.allgather(None, send.ctypes.data, send.nbytes, recv.ctypes.data)
+    # owner-masked all-reduce: word i is owned by rank i % world (others contribute 0)
+    n = 37
+    words = np.array([(0x7F000000 - i) if i % world == rank else 0 for i in range(n)],
+                     dtype=np.uint32)
+    rc_ar = coll.allreduce(None, words.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), n)
+    q.put((rank, rc_ag, recv.tolist(), rc_ar, words.tolist()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_shard_collectives_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_coll_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    gathered = [v + 1000 * r for r in range(world) for v in range(1, 9)]
+    reduced = [0x7F000000 - i for i in range(37)]  # exact: one owner per word, values < 2^31
+    for rank, rc_ag, recv, rc_ar, words in res:
+        assert rc_ag == 0 and rc_ar == 0
+        assert recv == gathered, f"rank {rank}: all-gather out of rank order"
+        assert words == reduced, f"rank {rank}: owner-masked all-reduce"

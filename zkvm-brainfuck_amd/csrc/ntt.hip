@@ -269,6 +269,13 @@ __global__ __launch_bounds__(1 << (B - 4)) void k_ntt_tile(const uint32_t* __res
 #pragma unroll
   for (int i = 0; i < 16; i++) lds[i * (T + T / 16) + tpad] = S[i * T + tid];
   uint32_t x[16];
+  // BFZ_NTT_REPS (diagnostic builds only, scripts/ubench_ntt.cpp): 0 = data movement alone,
+  // 2 = the stages twice, to split a pass's time into its memory and compute parts.
+#ifndef BFZ_NTT_REPS
+#define BFZ_NTT_REPS 1
+#endif
+#pragma nounroll
+  for (int rep = 0; rep < BFZ_NTT_REPS; rep++) {
   int done_lo = 0, done_hi = B;
 #pragma unroll
   for (int w = 0; w < NW; w++) {
@@ -293,6 +300,7 @@ __global__ __launch_bounds__(1 << (B - 4)) void k_ntt_tile(const uint32_t* __res
       r16_window<DIF, false, true>(x, g0, kk_lo, kk_hi, 0, m_low, 0, tw);
 #pragma unroll
     for (int i = 0; i < 16; i++) lds[pb + (i << g0) + ((i << g0) >> 4)] = x[i];
+  }
   }
   __syncthreads();
 #pragma unroll
