@@ -46,13 +46,23 @@ KB_HD uint32_t mreduce(uint64_t t) {
   if (r >= P) r -= P;
   return r;
 }
-// a, b < p: t < p^2 so hi < p/2 and r = hi - mh lies in (-p, p/2); min() folds the sign fix.
+// Any a < 2^32, b < p: with m = -t p^-1 mod 2^32, t + m p is a multiple of 2^32 below
+// 2^32 p + 2^32 p < 2^64, so r = (t + m p) / 2^32 lies in [0, 2p) (one v_mad_u64_u32 forms
+// t + m p: mad, mul_lo, mad, sub, min -- five instructions).
+constexpr uint32_t MU_NEG = 0u - MU;
 KB_HD uint32_t mmul(uint32_t a, uint32_t b) {
-  uint64_t t = (uint64_t)a * b;
-  uint32_t lo = (uint32_t)t, hi = (uint32_t)(t >> 32);
-  uint32_t m = mont_m(lo);
-  uint32_t mh = (uint32_t)(((uint64_t)m * P) >> 32);
-  uint32_t r = hi - mh;
+  const uint64_t t = (uint64_t)a * b;
+  const uint32_t m = (uint32_t)t * MU_NEG;
+  const uint32_t r = (uint32_t)(((uint64_t)m * P + t) >> 32);
+  return umin(r, r - P);
+}
+// Signed a in (-p, p), b < p: t = a b and the signed factor m give |t + m p| < 2^63 and
+// r = (t + m p) / 2^32 in (-p, p); one min() folds the sign.  Used for the DIF difference
+// (u - v) w, which then needs no + p before the product.
+KB_HD uint32_t mmul_s(int32_t a, uint32_t b) {
+  const int64_t t = (int64_t)a * (int64_t)(int32_t)b;
+  const int32_t m = (int32_t)((uint32_t)t * MU_NEG);
+  const uint32_t r = (uint32_t)(((int64_t)m * (int64_t)P + t) >> 32);
   return umin(r, r + P);
 }
 KB_HD uint32_t madd(uint32_t a, uint32_t b) {

@@ -102,13 +102,13 @@ __global__ __launch_bounds__(256) void k_perm_rows(const uint32_t* __restrict__ 
     const uint64_t w0 = (uint64_t)D.c[1] * cj[q].c[3] + (uint64_t)D.c[2] * cj[q].c[2] +
                         (uint64_t)D.c[3] * cj[q].c[1];
     nrm[q] = madd(mreduce((uint64_t)D.c[0] * cj[q].c[0]), mul3(mreduce(w0)));
-    pre[q] = q ? mmul(pre[q - 1], nrm[q]) : nrm[q];
+    pre[q] = q ? mmul(pre[q ? q - 1 : 0], nrm[q]) : nrm[q];
   });
   uint32_t inv = minv(pre[NP - 1]);
   EF sum = ef_zero();
   static_for<0, NP>([&](auto P) {
     constexpr int q = NP - 1 - decltype(P)::value, BA = 2 * q, BB = BA + 1;
-    const uint32_t inv_n = q ? mmul(inv, pre[q - 1]) : inv;  // 1 / N(D_q)
+    const uint32_t inv_n = q ? mmul(inv, pre[q ? q - 1 : 0]) : inv;  // 1 / N(D_q)
     if (q) inv = mmul(inv, nrm[q]);
     const EF invD = ef_mul_base(cj[q], inv_n);
     const EF va = ef_mul(xa[q], invD);

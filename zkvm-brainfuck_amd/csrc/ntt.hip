@@ -51,7 +51,7 @@ __global__ __launch_bounds__(256) void k_ntt_pass(const uint32_t* __restrict__ s
       const uint32_t u = tile[i1], v = tile[i2];
       if (DIF) {
         tile[i1] = madd(u, v);
-        tile[i2] = mmul(msub(u, v), w);
+        tile[i2] = mmul_s((int32_t)(u - v), w);
       } else {
         const uint32_t vw = mmul(v, w);
         tile[i1] = madd(u, vw);
@@ -160,7 +160,7 @@ __device__ __forceinline__ void r16_window(uint32_t (&x)[16], int g0, int kk_lo,
       const uint32_t u = x[i], v = x[j];
       if (DIF) {
         x[i] = madd(u, v);
-        x[j] = unit ? msub(u, v) : mmul(u - v + P, w);
+        x[j] = unit ? msub(u, v) : mmul_s((int32_t)(u - v), w);
       } else {
         const uint32_t vw = unit ? umin(v, v - P) : mmul(v, w);
         const bool lazy = kk < 3 && ((i >> (kk + 1)) & 1);
