@@ -36,16 +36,10 @@ KB_HD uint32_t opaque(uint32_t x) {
   return x;
 }
 
-// Montgomery reduction of t < 2^64 with hi(t) < 2p: result in [0, p).
-KB_HD uint32_t mreduce(uint64_t t) {
-  uint32_t lo = (uint32_t)t, hi = (uint32_t)(t >> 32);
-  uint32_t m = mont_m(lo);
-  uint32_t mh = (uint32_t)(((uint64_t)m * P) >> 32);
-  uint32_t r = hi - mh;
-  if (hi < mh) r += P;
-  if (r >= P) r -= P;
-  return r;
-}
+KB_HD uint32_t mred_lt_p(uint64_t y);
+KB_HD uint64_t fold32(uint64_t x);
+// Montgomery reduction of any t < 2^64: result in [0, p) (fold to < 2^57, then mred_lt_p).
+KB_HD uint32_t mreduce(uint64_t t) { return mred_lt_p(fold32(t)); }
 // Any a < 2^32, b < p: with m = -t p^-1 mod 2^32, t + m p is a multiple of 2^32 below
 // 2^32 p + 2^32 p < 2^64, so r = (t + m p) / 2^32 lies in [0, 2p) (one v_mad_u64_u32 forms
 // t + m p: mad, mul_lo, mad, sub, min -- five instructions).
@@ -144,11 +138,12 @@ KB_HD EF ef_add_base(EF a, uint32_t b) {
 KB_HD uint32_t mul3(uint32_t x) { return madd(madd(x, x), x); }
 // x mod p as a smaller 64-bit value: hi * (2^32 mod p) + lo  (< 2^57 for any x)
 KB_HD uint64_t fold32(uint64_t x) { return (uint64_t)(uint32_t)(x >> 32) * ((1u << 25) - 2) + (uint32_t)x; }
-// Montgomery reduction of y with hi(y) < p: result in [0, p)
+// Montgomery reduction of y with hi(y) < p: result in [0, p).  y + m p (m = -y p^-1 mod
+// 2^32) < 2^63 + 2^63 is a multiple of 2^32 whose high word lies in [0, 2p).
 KB_HD uint32_t mred_lt_p(uint64_t y) {
-  const uint32_t m = mont_m((uint32_t)y);
-  const uint32_t r = (uint32_t)(y >> 32) - (uint32_t)(((uint64_t)m * P) >> 32);
-  return umin(r, r + P);
+  const uint32_t m = (uint32_t)y * MU_NEG;
+  const uint32_t r = (uint32_t)(((uint64_t)m * P + y) >> 32);
+  return umin(r, r - P);
 }
 KB_HD EF ef_mul(const EF& a, const EF& b) {
   // Coefficient k = d_k + 3 w_k (x^4 = 3).  Each d_k, w_k is a sum of <= 4 raw products
@@ -245,7 +240,7 @@ struct LazyEF {
     fold();
     EF r;
 #pragma unroll
-    for (int e = 0; e < 4; e++) r.c[e] = mreduce(acc[e]);
+    for (int e = 0; e < 4; e++) r.c[e] = mred_lt_p(acc[e]);  // folded: < 2^57
     return r;
   }
 };

@@ -163,10 +163,12 @@ KB_HD int64_t opaque64(int64_t x) {
 #endif
   return x;
 }
+// With m = -y p^-1 (mod 2^32, signed), y + m p is a multiple of 2^32 and the reduction is
+// its high word: v_mul_lo_u32 + one v_mad_i64_i32 (y the 64-bit addend).  |m p| < 2^62 and
+// every caller keeps |y| < 2^62, so the sum stays inside int64.
 KB_HD int32_t mred_s(int64_t y) {
-  const int32_t m = (int32_t)((uint32_t)y * MU);
-  const uint32_t mh = (uint32_t)(((int64_t)m * (int64_t)P) >> 32);
-  return (int32_t)(opaque((uint32_t)((uint64_t)y >> 32)) - mh);
+  const int32_t m = (int32_t)((uint32_t)y * MU_NEG);
+  return (int32_t)(((int64_t)m * (int64_t)P + y) >> 32);
 }
 // a = x R, |a| < p  ->  x^3 R^2 (mod p), |.| < p^2
 KB_HD int64_t cube_s(int32_t a) {

@@ -57,7 +57,7 @@ struct PowAcc {
     fold();
     EF r;
 #pragma unroll
-    for (int e = 0; e < 4; e++) r.c[e] = mreduce(a64[e]);
+    for (int e = 0; e < 4; e++) r.c[e] = mred_lt_p(a64[e]);  // folded: < 2^57
     return r;
   }
 };
