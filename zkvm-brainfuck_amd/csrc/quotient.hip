@@ -12,6 +12,8 @@
 // 3 w_2n^k H_n (split_evals / split_domains), ready for the chunk LDE.
 #include "quotient.h"
 
+#include <map>
+
 #include "air.h"
 
 namespace bfz {
@@ -62,11 +64,32 @@ struct PowAcc {
   }
 };
 
+// x_i = 3 w_N^i, the natural point i of the quotient domain 3 H_N (twf[N/2 + j] = w_N^j).
+__device__ __forceinline__ uint32_t quot_point(uint32_t i, uint32_t half, uint32_t shift,
+                                               const uint32_t* __restrict__ twf) {
+  const uint32_t w = i < half ? twf[half + i] : mneg(twf[i]);  // twf[half + (i - half)]
+  return mmul(shift, w);
+}
+
+// 1 / ((x - 1)(x - w_n^-1)) at every point of 3 H_N, stored by LDE position t (point
+// bitrev(t)): the selector denominators depend on the domain alone, so one table per log N
+// serves every chip of that height in every proof (built once, cached).
+__global__ __launch_bounds__(256) void k_sel_inv(int logN, uint32_t shift, uint32_t wn_inv,
+                                                 const uint32_t* __restrict__ twf,
+                                                 uint32_t* __restrict__ out) {
+  const size_t N = (size_t)1 << logN;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N) return;
+  const uint32_t x = quot_point(dbitrev((uint32_t)t, logN), (uint32_t)(N >> 1), shift, twf);
+  out[t] = minv(mmul(msub(x, ONE), msub(x, wn_inv)));
+}
+
 template <int CHIP>
 __global__ __launch_bounds__(256, 3) void k_quotient(const uint32_t* __restrict__ mainc,
                                                   const uint32_t* __restrict__ prepc,
                                                   const uint32_t* __restrict__ permc, int logN,
                                                   QuotParams qp, const uint32_t* __restrict__ twf,
+                                                  const uint32_t* __restrict__ sel_inv,
                                                   uint32_t* __restrict__ qout) {
   constexpr int MW = QMAIN_W[CHIP];
   constexpr int PWD = QPREP_W[CHIP] > 0 ? QPREP_W[CHIP] : 1;
@@ -98,14 +121,11 @@ __global__ __launch_bounds__(256, 3) void k_quotient(const uint32_t* __restrict_
       pn[e].c[k] = permc[(size_t)(4 * e + k) * N + tn];
     }
 
-  // x = 3 * w_N^i
-  const uint32_t half = (uint32_t)n;
-  const uint32_t w = i < half ? twf[half + i] : mneg(twf[i]);  // twf[half + (i - half)]
-  const uint32_t x = mmul(qp.shift, w);
+  const uint32_t x = quot_point(i, (uint32_t)n, qp.shift, twf);
   const uint32_t zh = (i & 1) ? qp.zh_odd : qp.zh_even;
   const uint32_t zh_inv = (i & 1) ? qp.zh_odd_inv : qp.zh_even_inv;
   const uint32_t a = msub(x, ONE), b = msub(x, qp.wn_inv);
-  const uint32_t inv_ab = minv(mmul(a, b));
+  const uint32_t inv_ab = sel_inv[t];  // 1 / (a b)
   const uint32_t zi = mmul(zh, inv_ab);
   const uint32_t is_first = mmul(zi, b), is_last = mmul(zi, a), is_trans = b;
 
@@ -122,25 +142,42 @@ __global__ __launch_bounds__(256, 3) void k_quotient(const uint32_t* __restrict_
 
 template <int CHIP>
 static void launch_q(const uint32_t* mainc, const uint32_t* prepc, const uint32_t* permc, int logN,
-                     const QuotParams& qp, uint32_t* qout, hipStream_t st) {
+                     const QuotParams& qp, const uint32_t* sel, uint32_t* qout, hipStream_t st) {
   const size_t N = (size_t)1 << logN;
   hipLaunchKernelGGL(k_quotient<CHIP>, dim3(ceil_div(N, 256)), dim3(256), 0, st, mainc, prepc,
-                     permc, logN, qp, (const uint32_t*)twiddles().fwd.p, qout);
+                     permc, logN, qp, (const uint32_t*)twiddles().fwd.p, sel, qout);
   KCHECK();
+}
+
+// The selector-denominator table of 3 H_N (k_sel_inv), built on first use per log N.  It is
+// written on the prover stream, so every later reader on that stream sees it complete.
+static const uint32_t* sel_inv_table(int logN, const QuotParams& qp, hipStream_t st) {
+  static auto* cache = new std::map<int, DBuf<uint32_t>>();
+  auto it = cache->find(logN);
+  if (it != cache->end()) return it->second.p;
+  const size_t N = (size_t)1 << logN;
+  DBuf<uint32_t> d(N);
+  hipLaunchKernelGGL(k_sel_inv, dim3(ceil_div(N, 256)), dim3(256), 0, st, logN, qp.shift,
+                     qp.wn_inv, (const uint32_t*)twiddles().fwd.p, d.p);
+  KCHECK();
+  const uint32_t* p = d.p;
+  cache->emplace(logN, std::move(d));
+  return p;
 }
 
 void quotient(int chip, const uint32_t* mainc, const uint32_t* prepc, const uint32_t* permc,
               int logN, const QuotParams& qp, uint32_t* qout, hipStream_t st) {
   twiddles().ensure(logN);
+  const uint32_t* sel = sel_inv_table(logN, qp, st);
   switch (chip) {
-    case CHIP_CPU: launch_q<CHIP_CPU>(mainc, prepc, permc, logN, qp, qout, st); break;
-    case CHIP_PROGRAM: launch_q<CHIP_PROGRAM>(mainc, prepc, permc, logN, qp, qout, st); break;
-    case CHIP_ADDSUB: launch_q<CHIP_ADDSUB>(mainc, prepc, permc, logN, qp, qout, st); break;
-    case CHIP_JUMP: launch_q<CHIP_JUMP>(mainc, prepc, permc, logN, qp, qout, st); break;
-    case CHIP_MEMORY: launch_q<CHIP_MEMORY>(mainc, prepc, permc, logN, qp, qout, st); break;
-    case CHIP_BYTE: launch_q<CHIP_BYTE>(mainc, prepc, permc, logN, qp, qout, st); break;
-    case CHIP_MEMINSTRS: launch_q<CHIP_MEMINSTRS>(mainc, prepc, permc, logN, qp, qout, st); break;
-    case CHIP_IO: launch_q<CHIP_IO>(mainc, prepc, permc, logN, qp, qout, st); break;
+    case CHIP_CPU: launch_q<CHIP_CPU>(mainc, prepc, permc, logN, qp, sel, qout, st); break;
+    case CHIP_PROGRAM: launch_q<CHIP_PROGRAM>(mainc, prepc, permc, logN, qp, sel, qout, st); break;
+    case CHIP_ADDSUB: launch_q<CHIP_ADDSUB>(mainc, prepc, permc, logN, qp, sel, qout, st); break;
+    case CHIP_JUMP: launch_q<CHIP_JUMP>(mainc, prepc, permc, logN, qp, sel, qout, st); break;
+    case CHIP_MEMORY: launch_q<CHIP_MEMORY>(mainc, prepc, permc, logN, qp, sel, qout, st); break;
+    case CHIP_BYTE: launch_q<CHIP_BYTE>(mainc, prepc, permc, logN, qp, sel, qout, st); break;
+    case CHIP_MEMINSTRS: launch_q<CHIP_MEMINSTRS>(mainc, prepc, permc, logN, qp, sel, qout, st); break;
+    case CHIP_IO: launch_q<CHIP_IO>(mainc, prepc, permc, logN, qp, sel, qout, st); break;
     default: throw std::runtime_error("quotient: bad chip");
   }
 }
