@@ -283,7 +283,7 @@ def main():
             "poseidon2": poseidon2_roofline(tm),
             "proof_bytes": len(proof),
         }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the CPU baseline is timed at N=1 only
             try:
                 line["cpu_baseline"] = cpu_baseline()
             except Exception as e:  # keep the GPU line even if the baseline fails
