@@ -30,10 +30,10 @@ void open_matrix(const uint32_t* mat, size_t height, int w, const kb::EF* invd_a
                  const kb::EF& scale_a, kb::EF* out_a, const kb::EF* invd_b,
                  const kb::EF& scale_b, kb::EF* out_b, hipStream_t st);
 // ro[t] += (sum_c ca_c v_c[t] - ya) invd_a[t] + (sum_m kb_m sum_(c in m) ca_c v_c[t] - yb) invd_b[t]
-void reduce_height(const std::vector<RedCol>& cols, const std::vector<RedMat>& mats, size_t H,
-                   const kb::EF* invd_a,
-                   const kb::EF* invd_b, const kb::EF& ya, const kb::EF& yb, bool has_b,
-                   kb::EF* ro, hipStream_t st);
+// cols / mats: device descriptor arrays of one height (RedMat::first indexes cols).
+void reduce_height(const RedCol* cols, const RedMat* mats, int nmats, size_t H,
+                   const kb::EF* invd_a, const kb::EF* invd_b, const kb::EF& ya, const kb::EF& yb,
+                   bool has_b, kb::EF* ro, hipStream_t st);
 void fri_fold(const kb::EF* in, kb::EF* out, size_t h, const kb::EF& beta, const kb::EF* add,
               hipStream_t st);
 uint32_t grind(const GrindState& gs, int bits, hipStream_t st);

@@ -208,7 +208,7 @@ __global__ __launch_bounds__(256) void k_reduce(const RedCol* __restrict__ cols,
     }
     EF r = ef_mul(ef_sub(sa, ya), invd_a[t]);
     if (has_b) r = ef_add(r, ef_mul(ef_sub(sb, yb), invd_b[t]));
-    ro[t] = ef_add(ro[t], r);
+    ro[t] = r;  // one launch covers every matrix of the height
   }
 }
 
@@ -336,19 +336,12 @@ void open_matrix(const uint32_t* mat, size_t height, int w, const EF* invd_a, co
   KCHECK();
 }
 
-void reduce_height(const std::vector<RedCol>& cols, const std::vector<RedMat>& mats, size_t H,
-                   const EF* invd_a, const EF* invd_b, const EF& ya, const EF& yb, bool has_b,
-                   EF* ro, hipStream_t st) {
-  DBuf<RedCol> d(cols.size());
-  DBuf<RedMat> dm(mats.size());
-  HIP_CHECK(hipMemcpyAsync(d.p, cols.data(), cols.size() * sizeof(RedCol), hipMemcpyHostToDevice, st));
-  HIP_CHECK(hipMemcpyAsync(dm.p, mats.data(), mats.size() * sizeof(RedMat), hipMemcpyHostToDevice,
-                           st));
-  HIP_CHECK(hipStreamSynchronize(st));  // host vectors may go away
+void reduce_height(const RedCol* cols, const RedMat* mats, int nmats, size_t H, const EF* invd_a,
+                   const EF* invd_b, const EF& ya, const EF& yb, bool has_b, EF* ro,
+                   hipStream_t st) {
   const unsigned grid = std::min<unsigned>(ceil_div(H, 256), 8192);
-  hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(256), 0, st, (const RedCol*)d.p,
-                     (const RedMat*)dm.p, (int)mats.size(), H, invd_a, invd_b, ya, yb,
-                     has_b ? 1 : 0, ro);
+  hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(256), 0, st, cols, mats, nmats, H, invd_a, invd_b,
+                     ya, yb, has_b ? 1 : 0, ro);
   KCHECK();
 }
 
@@ -385,8 +378,7 @@ uint32_t grind(const GrindState& gs, int bits, hipStream_t st) {
   // 1 - e^-4, and chunks are scanned in order so the first hit is the smallest witness.
   const uint32_t chunk = 1u << std::min(22, std::max(16, bits + 2));
   for (uint64_t start = 0; start < P; start += chunk) {
-    const uint32_t init = 0xffffffffu;
-    HIP_CHECK(hipMemcpyAsync(best.p, &init, 4, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipMemsetAsync(best.p, 0xff, 4, st));  // no candidate yet
     hipLaunchKernelGGL(k_grind, dim3(chunk / 256), dim3(256), 0, st, gs, (uint32_t)start,
                        (uint32_t)bits, best.p);
     KCHECK();
@@ -410,10 +402,9 @@ void gather_queries(const std::vector<GatherSeg>& segs, const std::vector<uint32
   if (out.empty()) return;
   DBuf<GatherSeg> dseg(segs.size());
   DBuf<uint32_t> doff(off.size()), dq(qidx.size()), dout(out.size());
-  HIP_CHECK(hipMemcpyAsync(dseg.p, segs.data(), segs.size() * sizeof(GatherSeg),
-                           hipMemcpyHostToDevice, st));
-  HIP_CHECK(hipMemcpyAsync(doff.p, off.data(), off.size() * 4, hipMemcpyHostToDevice, st));
-  HIP_CHECK(hipMemcpyAsync(dq.p, qidx.data(), qidx.size() * 4, hipMemcpyHostToDevice, st));
+  upload_async(dseg.p, segs.data(), segs.size() * sizeof(GatherSeg), st);
+  upload_async(doff.p, off.data(), off.size() * 4, st);
+  upload_async(dq.p, qidx.data(), qidx.size() * 4, st);
   const size_t nthreads = segs.size() * qidx.size();
   hipLaunchKernelGGL(k_gather_segs, dim3(ceil_div(nthreads, 256)), dim3(256), 0, st,
                      (const GatherSeg*)dseg.p, (int)segs.size(), (const uint32_t*)doff.p, wpq,

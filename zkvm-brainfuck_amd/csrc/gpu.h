@@ -132,6 +132,10 @@ struct Twiddles {
 Twiddles& twiddles();
 
 hipStream_t stream();
+// Small host -> device copies inside a proof through a pinned arena (runtime.hip): no host
+// stall.  staging_reset() once no earlier copy can be pending (after a stream synchronize).
+void upload_async(void* dst, const void* src, size_t bytes, hipStream_t st);
+void staging_reset();
 
 // Per-launch HIP-event timing of one kernel family (the roofline kernel of bench.py):
 // when `on`, callers bracket each launch with begin()/end(bytes); collect() resolves the

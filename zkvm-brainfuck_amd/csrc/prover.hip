@@ -118,11 +118,12 @@ void to_canon_digest(const uint32_t* d, uint32_t* o) {
   for (int i = 0; i < 8; i++) o[i] = from_mont(d[i]);
 }
 
-struct Writer {
+struct Writer {  // appends into a buffer sized up front (reserve): a memcpy per word
   std::vector<uint8_t> b;
   void u32(uint32_t v) {
-    const uint8_t* p = reinterpret_cast<const uint8_t*>(&v);
-    b.insert(b.end(), p, p + 4);
+    const size_t n = b.size();
+    b.resize(n + 4);
+    std::memcpy(b.data() + n, &v, 4);
   }
   void fp(uint32_t mont) { u32(from_mont(mont)); }
   void ef(const EF& e) {
@@ -241,6 +242,12 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
   p2_probe().reset();
   p2_probe().on = ev.on;
   std::vector<std::vector<EF>> keep;  // host buffers of async uploads live until the end
+  struct StagingScope {  // the pinned upload arena is rewound when the proof is done
+    ~StagingScope() {
+      (void)hipStreamSynchronize(stream());
+      staging_reset();
+    }
+  } staging_scope;
   const auto t_start = std::chrono::steady_clock::now();
   hipEvent_t e_total = ev.on ? ev.begin(st) : nullptr;
 
@@ -320,7 +327,7 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
       p = ef_mul(p, alpha);
     }
     apows[k].reset(K);
-    HIP_CHECK(hipMemcpyAsync(apows[k].p, ap.data(), K * sizeof(EF), hipMemcpyHostToDevice, st));
+    upload_async(apows[k].p, ap.data(), K * sizeof(EF), st);
     QuotParams qp;
     qp.perm_alpha = perm_alpha;
     for (int j = 0; j < 8; j++) qp.beta_pows[j] = pc.beta_pows[j];
@@ -419,8 +426,18 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
           ch.observe_ef(opened[mp[r][i].off[j] + c]);
   const EF fri_alpha = ch.sample_ef();
 
-  // ---- reduced openings per LDE height
+  // ---- reduced openings per LDE height: every height's column descriptors go up in one copy
   std::map<int, DBuf<EF>> ro;
+  struct RedJob {
+    int lh;
+    size_t col0, mat0;
+    int nmats;
+    EF ya, yb;
+    bool has_b;
+  };
+  std::vector<RedCol> red_cols;
+  std::vector<RedMat> red_mats;
+  std::vector<RedJob> red_jobs;
   for (int lh = Lmax; lh >= 1; lh--) {
     std::vector<RedCol> cols;
     std::vector<RedMat> rmats;
@@ -465,11 +482,19 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
         rmats.push_back(rm);
       }
     if (cols.empty()) continue;
-    DBuf<EF> r((size_t)1 << lh);
-    HIP_CHECK(hipMemsetAsync(r.p, 0, ((size_t)1 << lh) * sizeof(EF), st));
-    reduce_height(cols, rmats, (size_t)1 << lh, invd_zeta.p, has_b ? invd_next.at(lh).p : nullptr, ya, yb,
-                  has_b, r.p, st);
-    ro.emplace(lh, std::move(r));
+    red_jobs.push_back({lh, red_cols.size(), red_mats.size(), (int)rmats.size(), ya, yb, has_b});
+    red_cols.insert(red_cols.end(), cols.begin(), cols.end());
+    red_mats.insert(red_mats.end(), rmats.begin(), rmats.end());
+  }
+  DBuf<RedCol> red_cols_d(std::max<size_t>(red_cols.size(), 1));
+  DBuf<RedMat> red_mats_d(std::max<size_t>(red_mats.size(), 1));
+  upload_async(red_cols_d.p, red_cols.data(), red_cols.size() * sizeof(RedCol), st);
+  upload_async(red_mats_d.p, red_mats.data(), red_mats.size() * sizeof(RedMat), st);
+  for (const RedJob& j : red_jobs) {
+    DBuf<EF> r((size_t)1 << j.lh);
+    reduce_height(red_cols_d.p + j.col0, red_mats_d.p + j.mat0, j.nmats, (size_t)1 << j.lh,
+                  invd_zeta.p, j.has_b ? invd_next.at(j.lh).p : nullptr, j.ya, j.yb, j.has_b, r.p, st);
+    ro.emplace(j.lh, std::move(r));
   }
   if (ev.on) ev.end(e3, st, &tms->open);
 
@@ -484,7 +509,7 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
   // beta = 4 pops, and no host round trip is needed until the final polynomial.
   if (ch.nin != 0) throw std::runtime_error("FRI: unexpected pending challenger input");
   DBuf<uint32_t> dstate(16);
-  HIP_CHECK(hipMemcpyAsync(dstate.p, ch.st, 64, hipMemcpyHostToDevice, st));
+  upload_async(dstate.p, ch.st, 64, st);
   const int nrounds = Lmax - LOG_BLOWUP;
   DBuf<EF> betas(std::max(nrounds, 1));
   size_t len = (size_t)1 << Lmax;
@@ -575,6 +600,7 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
 
   // ---- serialize (BFZ1 normal form)
   Writer w;
+  w.b.reserve(4 * words.size() + ((size_t)64 << 10));
   w.u32(0x315a4642u);
   w.u32((uint32_t)nc);
   for (int k = 0; k < nc; k++) {

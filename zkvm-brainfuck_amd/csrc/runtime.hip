@@ -1,6 +1,8 @@
 // Process-wide device state: allocator pool, stream, twiddle tables.
 #include "gpu.h"
 
+#include <cstring>
+
 namespace bfz {
 
 DevicePool& pool() {
@@ -25,6 +27,44 @@ KernelProbe& ntt_probe() {
 KernelProbe& p2_probe() {
   static KernelProbe* k = new KernelProbe();
   return *k;
+}
+
+// Pinned staging for the small host -> device uploads inside a proof.  A copy from pageable
+// memory is staged synchronously by the runtime and leaves the GPU idle until the host catches
+// up; from pinned memory it is a plain stream-ordered DMA.  The arena is rewound when a proof
+// ends (after its stream synchronize), so a slot is never rewritten while its copy may still
+// be pending.
+namespace {
+struct Staging {
+  uint8_t* base = nullptr;
+  size_t cap = 0, off = 0;
+};
+Staging& staging() {
+  static Staging* s = [] {
+    auto* st = new Staging();
+    st->cap = (size_t)8 << 20;
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&st->base), st->cap, hipHostMallocDefault));
+    return st;
+  }();
+  return *s;
+}
+}  // namespace
+
+void staging_reset() { staging().off = 0; }
+
+void upload_async(void* dst, const void* src, size_t bytes, hipStream_t st) {
+  if (!bytes) return;
+  Staging& s = staging();
+  const size_t need = (bytes + 255) & ~(size_t)255;
+  if (s.off + need > s.cap) {  // arena full: a synchronous copy is always safe
+    HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    return;
+  }
+  uint8_t* slot = s.base + s.off;
+  s.off += need;
+  std::memcpy(slot, src, bytes);
+  HIP_CHECK(hipMemcpyAsync(dst, slot, bytes, hipMemcpyHostToDevice, st));
 }
 
 Twiddles& twiddles() {
