@@ -299,7 +299,9 @@ __global__ __launch_bounds__(256) void k_gather_segs(const GatherSeg* __restrict
   const int owner = g.own_shift >= 0 ? (int)(e >> g.own_shift) : 0;
   const uint64_t pos = (uint64_t)e * g.unit;
   uint32_t* o = out + (size_t)q * words_per_q + seg_off[s];
-  for (uint32_t k = 0; k < g.count; k++) o[k] = owner == rank ? g.base[pos + k * g.stride] : 0u;
+  // canonical form here, so the host copies the words straight into the proof
+  for (uint32_t k = 0; k < g.count; k++)
+    o[k] = owner == rank ? from_mont(g.base[pos + k * g.stride]) : 0u;
 }
 
 // ================================================================== host wrappers

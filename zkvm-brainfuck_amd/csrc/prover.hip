@@ -126,6 +126,11 @@ struct Writer {  // appends into a buffer sized up front (reserve): a memcpy per
     std::memcpy(b.data() + n, &v, 4);
   }
   void fp(uint32_t mont) { u32(from_mont(mont)); }
+  void raw(const uint32_t* w, size_t n) {  // words already canonical
+    const size_t o = b.size();
+    b.resize(o + 4 * n);
+    std::memcpy(b.data() + o, w, 4 * n);
+  }
   void ef(const EF& e) {
     for (int i = 0; i < 4; i++) fp(e.c[i]);
   }
@@ -646,8 +651,11 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
   w.u32((uint32_t)ncommit);
   for (int i = 0; i < ncommit; i++) w.digest(trees[i].root);
   w.u32((uint32_t)nq);
-  size_t pos = 0;
-  auto take = [&]() { return words[pos++]; };
+  size_t pos = 0;  // the gathered words arrive canonical (k_gather_segs)
+  auto take = [&](size_t n) {
+    w.raw(words.data() + pos, n);
+    pos += n;
+  };
   for (int q = 0; q < nq; q++) {
     w.u32(4);
     for (int r = 0; r < 4; r++) {
@@ -656,17 +664,17 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
       w.u32((uint32_t)R.mats.size());
       for (const CMat& m : R.mats) {
         w.u32((uint32_t)m.lde.width);
-        for (int c = 0; c < m.lde.width; c++) w.fp(take());
+        take(m.lde.width);
       }
       w.u32((uint32_t)lrm);
-      for (int L = 0; L < lrm * 8; L++) w.fp(take());
+      take((size_t)lrm * 8);
     }
     w.u32((uint32_t)ncommit);
     for (int i = 0; i < ncommit; i++) {
-      for (int e = 0; e < 4; e++) w.fp(take());
+      take(4);
       const int lm = (int)trees[i].layers.size() - 1;
       w.u32((uint32_t)lm);
-      for (int L = 0; L < lm * 8; L++) w.fp(take());
+      take((size_t)lm * 8);
     }
   }
   w.ef(fin[0]);
