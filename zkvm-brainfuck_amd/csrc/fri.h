@@ -29,7 +29,7 @@ void inv_denoms(const kb::EF& z, int logH, kb::EF* out, hipStream_t st);
 void open_matrix(const uint32_t* mat, size_t height, int w, const kb::EF* invd_a,
                  const kb::EF& scale_a, kb::EF* out_a, const kb::EF* invd_b,
                  const kb::EF& scale_b, kb::EF* out_b, hipStream_t st);
-// ro[t] += (sum_c ca_c v_c[t] - ya) invd_a[t] + (sum_m kb_m sum_(c in m) ca_c v_c[t] - yb) invd_b[t]
+// ro[t] = (sum_c ca_c v_c[t] - ya) invd_a[t] + (sum_m kb_m sum_(c in m) ca_c v_c[t] - yb) invd_b[t]
 // cols / mats: device descriptor arrays of one height (RedMat::first indexes cols).
 void reduce_height(const RedCol* cols, const RedMat* mats, int nmats, size_t H,
                    const kb::EF* invd_a, const kb::EF* invd_b, const kb::EF& ya, const kb::EF& yb,
@@ -62,7 +62,9 @@ struct GatherSeg {
 };
 // out[q * words_per_query + ...] = the segments' words for qidx[q], segments in order
 // (this rank's share when rank/world describe a sharded proof).
-void gather_queries(const std::vector<GatherSeg>& segs, const std::vector<uint32_t>& qidx,
-                    std::vector<uint32_t>& out, int rank, hipStream_t st);
+// Returns the nwords gathered words (canonical form) in a pinned host buffer that stays valid
+// until the next call.
+uint32_t* gather_queries(const std::vector<GatherSeg>& segs, const std::vector<uint32_t>& qidx,
+                         size_t& nwords, int rank, hipStream_t st);
 
 }  // namespace bfz

@@ -392,18 +392,27 @@ uint32_t grind(const GrindState& gs, int bits, hipStream_t st) {
   throw std::runtime_error("grind: no witness");
 }
 
-void gather_queries(const std::vector<GatherSeg>& segs, const std::vector<uint32_t>& qidx,
-                    std::vector<uint32_t>& out, int rank, hipStream_t st) {
+// The gathered words land in a pinned host buffer (grown on demand, reused by every proof):
+// the device-to-host copy is a plain DMA instead of a runtime staging through pageable memory.
+uint32_t* gather_queries(const std::vector<GatherSeg>& segs, const std::vector<uint32_t>& qidx,
+                         size_t& nwords, int rank, hipStream_t st) {
   std::vector<uint32_t> off(segs.size());
   uint32_t wpq = 0;
   for (size_t s = 0; s < segs.size(); s++) {
     off[s] = wpq;
     wpq += segs[s].count;
   }
-  out.assign((size_t)wpq * qidx.size(), 0);
-  if (out.empty()) return;
+  nwords = (size_t)wpq * qidx.size();
+  if (!nwords) return nullptr;
+  static uint32_t* host = nullptr;
+  static size_t cap = 0;
+  if (nwords > cap) {  // no copy into it is pending: every proof ends with a synchronize
+    if (host) HIP_CHECK(hipHostFree(host));
+    cap = nwords + nwords / 4;
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host), cap * 4, hipHostMallocDefault));
+  }
   DBuf<GatherSeg> dseg(segs.size());
-  DBuf<uint32_t> doff(off.size()), dq(qidx.size()), dout(out.size());
+  DBuf<uint32_t> doff(off.size()), dq(qidx.size()), dout(nwords);
   upload_async(dseg.p, segs.data(), segs.size() * sizeof(GatherSeg), st);
   upload_async(doff.p, off.data(), off.size() * 4, st);
   upload_async(dq.p, qidx.data(), qidx.size() * 4, st);
@@ -412,8 +421,9 @@ void gather_queries(const std::vector<GatherSeg>& segs, const std::vector<uint32
                      (const GatherSeg*)dseg.p, (int)segs.size(), (const uint32_t*)doff.p, wpq,
                      (const uint32_t*)dq.p, (int)qidx.size(), rank, dout.p);
   KCHECK();
-  HIP_CHECK(hipMemcpyAsync(out.data(), dout.p, out.size() * 4, hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipMemcpyAsync(host, dout.p, nwords * 4, hipMemcpyDeviceToHost, st));
   HIP_CHECK(hipStreamSynchronize(st));
+  return host;
 }
 
 }  // namespace bfz

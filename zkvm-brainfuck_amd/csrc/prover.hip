@@ -597,15 +597,15 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
       segs.push_back({trees[i].layers[L].p, 1, (uint32_t)(i + 1 + L), 1, 8, 8,
                       owner_shift(trees[i], L), 0});
   }
-  std::vector<uint32_t> words;
+  size_t nwords = 0;
   const ShardCtx* shard = shard_ctx();
-  gather_queries(segs, qidx, words, shard ? shard->rank : 0, st);
-  if (shard && shard->world > 1) shard->allreduce_sum_u32(words.data(), words.size());
+  uint32_t* words = gather_queries(segs, qidx, nwords, shard ? shard->rank : 0, st);
+  if (shard && shard->world > 1) shard->allreduce_sum_u32(words, nwords);
   if (ev.on) ev.end(e4, st, &tms->fri);
 
   // ---- serialize (BFZ1 normal form)
   Writer w;
-  w.b.reserve(4 * words.size() + ((size_t)64 << 10));
+  w.b.reserve(4 * nwords + ((size_t)64 << 10));
   w.u32(0x315a4642u);
   w.u32((uint32_t)nc);
   for (int k = 0; k < nc; k++) {
@@ -653,7 +653,7 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
   w.u32((uint32_t)nq);
   size_t pos = 0;  // the gathered words arrive canonical (k_gather_segs)
   auto take = [&](size_t n) {
-    w.raw(words.data() + pos, n);
+    w.raw(words + pos, n);
     pos += n;
   };
   for (int q = 0; q < nq; q++) {
