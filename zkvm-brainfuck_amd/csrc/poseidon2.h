@@ -175,8 +175,9 @@ KB_HD int32_t mred_s(int64_t y) {
   uint64_t carry;  // VOP3b carry-out, unused
   asm("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(carry) : "v"(m), "s"(P), "v"(y));
   return (int32_t)(r >> 32);
-#else
-  return (int32_t)(((int64_t)m * (int64_t)P + y) >> 32);
+#else  // host (transcript, verifier): the same residue as hi(y) - hi(m' p), m' = -m
+  const uint32_t mh = (uint32_t)(((int64_t)(int32_t)(0u - (uint32_t)m) * (int64_t)P) >> 32);
+  return (int32_t)((uint32_t)((uint64_t)y >> 32) - mh);
 #endif
 }
 // a = x R, |a| < p  ->  x^3 R^2 (mod p), |.| < p^2
