@@ -117,8 +117,8 @@ __global__ __launch_bounds__(256) void k_compress(const uint32_t* __restrict__ p
 // Merkle node j in lane mode (see poseidon2_permute_lane): lane l of the node's 16-lane row
 // holds word l of the state; the digest ends up in lanes 0..7.
 __device__ __forceinline__ uint32_t merkle_node_lane(uint32_t v, const ColList& cl, int c0, int c1,
-                                                     size_t j, int lane) {
-  v = poseidon2_permute_lane(v, lane);
+                                                     size_t j, int lane, const LaneConsts& kc) {
+  v = poseidon2_permute_lane(v, lane, kc);
   const int nchunks = (c1 - c0 + 7) >> 3;
   if (nchunks) {
     const uint32_t d = v;
@@ -126,10 +126,10 @@ __device__ __forceinline__ uint32_t merkle_node_lane(uint32_t v, const ColList& 
     for (int k = 0; k < nchunks; k++) {  // PaddingFreeSponge, overwrite mode
       const int col = c0 + 8 * k + lane;
       if (lane < 8 && col < c1) h = cl.col(col)[j];
-      h = poseidon2_permute_lane(h, lane);
+      h = poseidon2_permute_lane(h, lane, kc);
     }
     const uint32_t hs = dpp<DPP_ROR8>(h);  // lanes 8..15 <- h[0..7]
-    v = poseidon2_permute_lane(lane < 8 ? d : hs, lane);
+    v = poseidon2_permute_lane(lane < 8 ? d : hs, lane, kc);
   }
   return v;
 }
@@ -156,13 +156,14 @@ __global__ __launch_bounds__(1024) void k_compress_top(const uint32_t* __restric
   const size_t per = nlen < (size_t)TOP_NODES ? nlen : (size_t)TOP_NODES;
   const size_t g0 = (size_t)blockIdx.x * per;  // first-layer node of this block
   const int lane = threadIdx.x & 15;
+  const LaneConsts kc = lane_consts(lane);
   for (int l = 0; l < tl.n; l++) {
     const size_t m = per >> l, g = g0 >> l;
     const uint32_t* src = l == 0 ? prev + 16 * g : buf[(l - 1) & 1];
     uint32_t* dst = buf[l & 1];
     // whole 16-lane rows are active together (DPP needs all of them)
     for (size_t j = threadIdx.x >> 4; j < m; j += blockDim.x >> 4) {
-      const uint32_t v = merkle_node_lane(src[16 * j + lane], inj, tl.c0[l], tl.c1[l], g + j, lane);
+      const uint32_t v = merkle_node_lane(src[16 * j + lane], inj, tl.c0[l], tl.c1[l], g + j, lane, kc);
       if (lane < 8) {
         tl.out[l][8 * (g + j) + lane] = v;
         dst[8 * j + lane] = v;
@@ -175,7 +176,7 @@ __global__ __launch_bounds__(1024) void k_compress_top(const uint32_t* __restric
   if (rc.state && threadIdx.x < 64) {
     const uint32_t* root = buf[(tl.n - 1) & 1];
     uint32_t v = lane < 8 ? root[lane] : rc.state[lane];
-    v = poseidon2_permute_lane(v, lane);
+    v = poseidon2_permute_lane(v, lane, kc);
     if (threadIdx.x < 16) {
       rc.state[lane] = v;
       if (lane >= 4 && lane < 8) rc.beta->c[7 - lane] = v;
@@ -193,7 +194,7 @@ __global__ __launch_bounds__(256) void k_compress_lanes(const uint32_t* __restri
   const int lane = threadIdx.x & 15;
   if (i >= count) return;
   const size_t j = j0 + i;
-  const uint32_t v = merkle_node_lane(prev[16 * j + lane], inj, 0, inj.n, j, lane);
+  const uint32_t v = merkle_node_lane(prev[16 * j + lane], inj, 0, inj.n, j, lane, lane_consts(lane));
   if (lane < 8) out[8 * j + lane] = v;
 }
 

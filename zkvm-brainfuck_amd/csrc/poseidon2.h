@@ -272,14 +272,27 @@ __device__ __forceinline__ uint32_t sum_lanes16(uint32_t v) {
   return madd(v, dpp<DPP_ROR8>(v));
 }
 
-__device__ __forceinline__ uint32_t poseidon2_permute_lane(uint32_t v, int lane) {
+// The lane's round constants, loaded once per kernel by callers that permute in a loop (the
+// loads are a memory round trip on a latency-bound chain).
+struct LaneConsts {
   uint32_t rce[8];
+  uint32_t dg;
+};
+__device__ __forceinline__ LaneConsts lane_consts(int lane) {
+  LaneConsts k;
 #pragma unroll
   for (int r = 0; r < 4; r++) {
-    rce[r] = P2.ext_init[r][lane];
-    rce[4 + r] = P2.ext_term[r][lane];
+    k.rce[r] = P2.ext_init[r][lane];
+    k.rce[4 + r] = P2.ext_term[r][lane];
   }
-  const uint32_t dg = P2.diag[lane];
+  k.dg = P2.diag[lane];
+  return k;
+}
+
+__device__ __forceinline__ uint32_t poseidon2_permute_lane(uint32_t v, int lane,
+                                                           const LaneConsts& kc) {
+  const uint32_t* rce = kc.rce;
+  const uint32_t dg = kc.dg;
   v = mds_light_lane(v);
 #pragma unroll
   for (int r = 0; r < 4; r++) v = mds_light_lane(cube(madd(v, rce[r])));
@@ -292,6 +305,9 @@ __device__ __forceinline__ uint32_t poseidon2_permute_lane(uint32_t v, int lane)
 #pragma unroll
   for (int r = 0; r < 4; r++) v = mds_light_lane(cube(madd(v, rce[4 + r])));
   return v;
+}
+__device__ __forceinline__ uint32_t poseidon2_permute_lane(uint32_t v, int lane) {
+  return poseidon2_permute_lane(v, lane, lane_consts(lane));
 }
 
 }  // namespace kb
