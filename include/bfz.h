@@ -26,7 +26,11 @@
  * byte-identical to a Rust `[KoalaBear]` slice; matrices are row-major.  Every function
  * returns 0 on success and a negative status on failure (bfz_last_error() describes it);
  * the Rust wrapper panics on a non-zero status, matching the reference (which unwraps).
- * Calls are serialized internally; one process-wide context drives one GPU.
+ * Calls are serialized internally (one mutex); one process drives ONE GPU: bfz_init binds
+ * the device on first use and fails if a later call names another one.  The stream,
+ * allocator pool, twiddle/selector caches and pinned staging are process-wide, so ranks are
+ * separate processes (one per GPU), never threads of one process -- the sharded entry points
+ * hold the mutex while they run the caller's collective callbacks.
  * Proofs are byte strings in the BFZ1 normal form described in DESIGN.md.
  */
 #ifndef BFZ_H
@@ -53,6 +57,9 @@ typedef struct {
 
 int bfz_init(int device);
 const char* bfz_last_error(void);
+/* Hash of the sources the library was built from (bfz/srchash.py); bfz/_lib.py refuses a
+ * library whose hash differs from the sources beside it. */
+const char* bfz_build_id(void);
 int bfz_device_name(char* buf, size_t cap);
 void bfz_free(void* p);
 int bfz_synchronize(void); /* hipDeviceSynchronize on the bound device */
@@ -125,7 +132,28 @@ int bfz_commit_fri_sharded(const uint32_t* d_cols, int log_n, size_t w_local, in
                            bfz_allgather_fn allgather, void* ctx, uint32_t* out, size_t cap,
                            size_t* nwords);
 
-int bfz_set_num_queries(int num_queries); /* FRI_QUERIES (kb31_poseidon2.rs:59-62) */
+/* FRI_QUERIES (kb31_poseidon2.rs:59-62): 1..4096, or 0 = environment FRI_QUERIES / 84. */
+int bfz_set_num_queries(int num_queries);
+
+/* PCS transcript variant, decision D1 of DESIGN.md §2 ([p3-recalled] TwoAdicFriPcs::open at
+ * zkMIPS/Plonky3 93967fce): 1 = every opened value is observed before the FRI batching
+ * challenge alpha is sampled (default), 0 = alpha is sampled first; -1 = environment
+ * BFZ_OBSERVE_OPENINGS.  Applies to bfz_prove*, bfz_verify*, identically in the oracle. */
+int bfz_set_pcs_variant(int observe_openings);
+
+/* Proof wire format.  bfz_prove* return the BFZ1 normal form; bfz_proof_to_bincode turns it
+ * into the reference's bytes: bincode::serialize(&MachineProof<KoalaBearPoseidon2>)
+ * (crates/core/machine/src/utils/prove.rs:46), i.e. ShardProof (crates/stark/src/types.rs:66-73)
+ * with bincode 1.x default options, chip_ordering entries in proof order.  field_repr selects
+ * how a KoalaBear word is serialized: 0 = Montgomery word (p3 MontyField31 serde, default,
+ * [p3-recalled]), 1 = canonical value.  bfz_proof_from_bincode is the inverse;
+ * bfz_verify_bincode verifies the bincode bytes directly.  *out is malloc'd (bfz_free). */
+int bfz_proof_to_bincode(const uint8_t* proof, size_t len, int field_repr, uint8_t** out,
+                         size_t* out_len);
+int bfz_proof_from_bincode(const uint8_t* bytes, size_t len, int field_repr, uint8_t** out,
+                           size_t* out_len);
+int bfz_verify_bincode(const char* elf, const uint32_t vk_commit[8], const uint8_t* bytes,
+                       size_t len, int field_repr);
 
 int bfz_coset_lde(const uint32_t* evals, size_t n, size_t w, uint32_t shift, uint32_t* lde_out);
 int bfz_commit(const uint32_t* const* mats, const size_t* heights, const size_t* widths,

@@ -11,6 +11,7 @@ int or_prove_record(const or_program* prog, or_record* rec, uint8_t** out, size_
                     or_timing* tm);
 int or_verify_proof(const or_program* prog, const uint8_t* proof, size_t len);
 void or_set_num_queries(int q);
+void or_set_pcs_variant(int observe_openings);
 void or_setup_root(const or_program* p, uint32_t root[8]);
 int or_api_setup_root(const char* program, uint32_t root[8]);
 

@@ -28,6 +28,10 @@
 
 static int g_num_queries = 84;
 void or_set_num_queries(int q) { g_num_queries = q; }
+/* Decision D1 ([p3-recalled] TwoAdicFriPcs::open): 1 = every opened value is
+ * observed before the FRI batching challenge is sampled; 0 = the challenge is sampled first. */
+static int g_observe_openings = 1;
+void or_set_pcs_variant(int observe_openings) { g_observe_openings = observe_openings != 0; }
 
 /* ------------------------------------------------------------------ byte buffer */
 typedef struct { uint8_t* p; size_t n, cap; } buf;
@@ -450,7 +454,8 @@ int or_prove_record(const or_program* prog, or_record* rec, uint8_t** out, size_
       for (int p = 0; p < orr[r].npts[i]; p++) {
         orr[r].vals[i][p] = malloc(sizeof(ef) * c->w);
         or_eval_columns_at(c->evals, c->n, c->w, c->shift, orr[r].pts[i][p], orr[r].vals[i][p]);
-        for (size_t k = 0; k < c->w; k++) or_ch_observe_ef(&ch, orr[r].vals[i][p][k]);
+        if (g_observe_openings)
+          for (size_t k = 0; k < c->w; k++) or_ch_observe_ef(&ch, orr[r].vals[i][p][k]);
       }
     }
   }
@@ -657,8 +662,8 @@ int or_verify_proof(const or_program* prog, const uint8_t* proof, size_t len) {
       m->pt[0] = zeta; m->v[0] = k ? q1[i] : q0[i];
     }
   }
-  /* PCS verify: observe openings, sample alpha */
-  for (int rr_ = 0; rr_ < 4; rr_++)
+  /* PCS verify: observe openings (decision D1), sample alpha */
+  if (g_observe_openings) for (int rr_ = 0; rr_ < 4; rr_++)
     for (int i = 0; i < vn[rr_]; i++)
       for (int p = 0; p < vm[rr_][i].np; p++)
         for (size_t k = 0; k < vm[rr_][i].w; k++) or_ch_observe_ef(&ch, vm[rr_][i].v[p][k]);

@@ -43,6 +43,7 @@ def lib():
         L.or_api_challenger.argtypes = [P32, ctypes.c_size_t, P32, ctypes.c_size_t]
         L.or_api_setup_root.argtypes = [ctypes.c_char_p, P32]
         L.or_set_num_queries.argtypes = [ctypes.c_int]
+        L.or_set_pcs_variant.argtypes = [ctypes.c_int]
         _L = L
     return _L
 
@@ -62,9 +63,10 @@ def execute(prog: str, stdin):
     return {"output": bytes(out[: n.value]), "cycles": cyc.value, "pc": pc.value, "mp": mp.value}
 
 
-def prove(prog: str, stdin, num_queries: int = 84) -> bytes:
+def prove(prog: str, stdin, num_queries: int = 84, observe_openings: bool = True) -> bytes:
     L = lib()
     L.or_set_num_queries(num_queries)
+    L.or_set_pcs_variant(int(observe_openings))
     p = ctypes.POINTER(ctypes.c_uint8)()
     n = ctypes.c_size_t()
     inb = bytes(stdin)
@@ -76,9 +78,10 @@ def prove(prog: str, stdin, num_queries: int = 84) -> bytes:
     return b
 
 
-def verify(prog: str, proof: bytes, num_queries: int = 84) -> bool:
+def verify(prog: str, proof: bytes, num_queries: int = 84, observe_openings: bool = True) -> bool:
     L = lib()
     L.or_set_num_queries(num_queries)
+    L.or_set_pcs_variant(int(observe_openings))
     return L.or_api_verify(prog.encode(), proof, len(proof)) == 0
 
 

@@ -64,3 +64,118 @@ def test_host_verifier_rejects_tampering_and_wrong_vk():
     wrong.elf = prog
     with pytest.raises(_lib.BfzError):
         c.verify(sdk.BfProofWithPublicValues(proof=pf, stdin=b""), wrong)
+
+
+# ---------------------------------------------------------------- proof byte forms (bincode)
+import struct  # noqa: E402
+
+import bincode_ref as BR  # noqa: E402
+
+
+@pytest.mark.parametrize("name,prog,stdin", guests.REFERENCE_PROGRAMS[:4] +
+                         [("hello", guests.HELLO, [])])
+def test_bincode_encoder_matches_independent_model(name, prog, stdin):
+    """csrc/proof.cpp's bincode ShardProof == the separately written Python model, in both
+    field representations; bincode -> BFZ1 is the exact inverse; the decoded model re-encodes
+    to the same BFZ1 bytes."""
+    pf = O.prove(prog, stdin)
+    model = BR.parse_bfz1(pf)
+    assert BR.encode_bfz1(model) == pf
+    for repr_, mont in ((sdk.FIELD_MONTGOMERY, True), (sdk.FIELD_CANONICAL, False)):
+        bc = sdk.proof_to_bincode(pf, repr_)
+        assert bc == BR.encode_bincode(model, montgomery=mont)
+        assert sdk.proof_from_bincode(bc, repr_) == pf
+
+
+def test_bincode_layout_landmarks():
+    """Spot-check the serde layout: 3 digests, then u64 chip count, chip_ordering at the end
+    as (u64 len, name, u64 index) in proof order."""
+    pf = O.prove(guests.HELLO, [])
+    model = BR.parse_bfz1(pf)
+    bc = sdk.proof_to_bincode(pf, sdk.FIELD_CANONICAL)
+    assert list(struct.unpack_from("<8I", bc, 0)) == model["roots"][0]
+    assert struct.unpack_from("<Q", bc, 96)[0] == len(model["chips"])
+    tail = b"".join(struct.pack("<Q", len(BR.CHIPS[c])) + BR.CHIPS[c].encode() + struct.pack("<Q", i)
+                    for i, c in enumerate(model["chips"]))
+    assert bc.endswith(struct.pack("<Q", len(model["chips"])) + tail)
+
+
+def test_verify_bincode_and_proof_with_public_values():
+    prog = guests.FIBO
+    pf = O.prove(prog, [17])
+    vk = _vk(prog)
+    c = sdk.ProverClient()
+    bc = sdk.proof_to_bincode(pf)
+    c.verify_bincode(bc, vk)
+    c.verify_bincode(sdk.proof_to_bincode(pf, sdk.FIELD_CANONICAL), vk, sdk.FIELD_CANONICAL)
+    with pytest.raises(_lib.BfzError, match="verification failed"):  # wrong representation
+        c.verify_bincode(bc, vk, sdk.FIELD_CANONICAL)
+    bad = bytearray(bc)
+    bad[len(bad) // 2] ^= 1
+    with pytest.raises(_lib.BfzError, match="verification failed"):
+        c.verify_bincode(bytes(bad), vk)
+    wp = sdk.BfProofWithPublicValues(proof=pf, stdin=bytes([17]))
+    ser = wp.to_bincode()
+    assert ser == bc + struct.pack("<Q", 1) + bytes([17])
+    back = sdk.BfProofWithPublicValues.from_bincode(ser)
+    assert back.proof == pf and back.stdin == bytes([17])
+
+
+def _tampered(pf, fn):
+    m = BR.parse_bfz1(pf)
+    fn(m)
+    return BR.encode_bfz1(m)
+
+
+def test_verifier_rejects_out_of_range_log_degree_and_round_count():
+    """a log degree word >= 2^31 (a negative int) or 0, and a commit phase shorter
+    than the tallest matrix, are rejected before any shift by them."""
+    prog = guests.HELLO
+    pf = O.prove(prog, [])
+    vk = _vk(prog)
+    c = sdk.ProverClient()
+
+    def set_logdeg(v):
+        return lambda m: m["opened"][0].__setitem__("log_degree", v)
+
+    for v in (0x80000000, 0xFFFFFFFF, 0, 24):
+        with pytest.raises(_lib.BfzError, match="log degree out of range"):
+            c.verify(sdk.BfProofWithPublicValues(proof=_tampered(pf, set_logdeg(v)), stdin=b""), vk)
+
+    def short_commit(m):
+        m["commit_roots"].pop()
+        for q in m["queries"]:
+            q["steps"].pop()
+
+    with pytest.raises(_lib.BfzError, match="FRI round count"):
+        c.verify(sdk.BfProofWithPublicValues(proof=_tampered(pf, short_commit), stdin=b""), vk)
+
+
+def test_pcs_variant_switch_is_consistent():
+    """Decision D1: with the opened values kept out of the transcript, the
+    oracle's proof differs, and each verifier accepts exactly the proofs of its own variant."""
+    prog = guests.LOOP if hasattr(guests, "LOOP") else guests.HELLO
+    a = O.prove(prog, [], observe_openings=True)
+    b = O.prove(prog, [], observe_openings=False)
+    assert a != b
+    vk = _vk(prog)
+    c = sdk.ProverClient()
+    try:
+        sdk.set_pcs_variant(0)
+        c.verify(sdk.BfProofWithPublicValues(proof=b, stdin=b""), vk)
+        with pytest.raises(_lib.BfzError, match="verification failed"):
+            c.verify(sdk.BfProofWithPublicValues(proof=a, stdin=b""), vk)
+        assert O.verify(prog, b, observe_openings=False)
+        assert not O.verify(prog, a, observe_openings=False)
+    finally:
+        sdk.set_pcs_variant(-1)
+    c.verify(sdk.BfProofWithPublicValues(proof=a, stdin=b""), vk)
+    with pytest.raises(_lib.BfzError, match="verification failed"):
+        c.verify(sdk.BfProofWithPublicValues(proof=b, stdin=b""), vk)
+
+
+def test_query_count_validation():
+    """FRI_QUERIES-style overrides must be positive."""
+    with pytest.raises(_lib.BfzError, match="num_queries"):
+        sdk.set_num_queries(-3)
+    sdk.set_num_queries(0)

@@ -155,6 +155,12 @@ def test_prove_traces_rejects_bad_shapes(client):
         sdk.CoreProver().prove(pk, [(c, name, t[:-1])] + traces[1:])
     with pytest.raises(_lib.BfzError, match="repeated"):
         sdk.CoreProver().prove(pk, traces + traces[:1])
+    bad = t.copy()
+    bad[3, 0] = P  # a Montgomery word >= p
+    with pytest.raises(_lib.BfzError, match="non-canonical"):
+        sdk.CoreProver().prove(pk, [(c, name, bad)] + traces[1:])
+    with pytest.raises(_lib.BfzError, match="power of two"):  # height 1
+        sdk.CoreProver().prove(pk, [(c, name, t[:1])] + traces[1:])
 
 
 def test_fibo17_end_to_end_sdk(client):
@@ -174,19 +180,40 @@ def test_fibo255_2pow20_parity(client):
 
 
 @pytest.mark.slow
-def test_fibo_x4_2pow22_properties(client):
-    """Headline size (2^22 Cpu rows): size-independent properties — host verifier and oracle
-    verifier accept, the proof is deterministic, tampering is rejected."""
+def test_fibo_x4_2pow22_bytes_match_oracle(client):
+    """Headline workload (BASELINE.json metric: Cpu trace 2^22 rows, FIBO_X4 stdin [255],
+    3,767,729 cycles): the GPU proof is byte-identical to the oracle's, both verifiers accept
+    it, proving is deterministic, the bincode form round-trips, and tampering is rejected."""
     pk, vk = client.setup(guests.FIBO_X4)
     a = client.prove(pk, [255]).run()
     client.verify(a, vk)
-    assert O.verify(guests.FIBO_X4, a.proof)
     b = client.prove(pk, [255]).run()
     assert a.proof == b.proof
+    ref = O.prove(guests.FIBO_X4, [255])
+    assert a.proof == ref, "headline proof differs from the oracle"
+    assert O.verify(guests.FIBO_X4, a.proof)
+    bc = sdk.proof_to_bincode(a.proof)
+    client.verify_bincode(bc, vk)
+    assert sdk.proof_from_bincode(bc) == a.proof
     bad = bytearray(a.proof)
     bad[len(bad) // 3] ^= 4
     with pytest.raises(_lib.BfzError):
         client.verify(sdk.BfProofWithPublicValues(proof=bytes(bad), stdin=b"\xff"), vk)
+
+
+def test_pcs_variant_parity(client):
+    """Decision D1 switched off: GPU and oracle still agree bit for bit, and the
+    proof differs from the default variant's."""
+    prog = guests.FIBO
+    pk, vk = client.setup(prog)
+    try:
+        sdk.set_pcs_variant(0)
+        pf = client.prove(pk, [17]).run()
+        client.verify(pf, vk)
+        assert pf.proof == O.prove(prog, [17], observe_openings=False)
+    finally:
+        sdk.set_pcs_variant(-1)
+    assert pf.proof != client.prove(pk, [17]).run().proof
 
 
 def test_invalid_trace_rejected_by_verifiers(client):

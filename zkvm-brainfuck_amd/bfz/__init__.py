@@ -5,8 +5,10 @@ this package is the host-side mirror of the reference's SDK (crates/sdk) over th
 """
 from ._lib import BfzError, LIB_PATH, init
 from .sdk import (BfProofWithPublicValues, BfProvingKey, BfVerifyingKey, Execute, Prove,
-                  ProverClient, set_num_queries)
+                  ProverClient, proof_from_bincode, proof_to_bincode, set_num_queries,
+                  set_pcs_variant)
 from . import guests
 
 __all__ = ["ProverClient", "BfProvingKey", "BfVerifyingKey", "BfProofWithPublicValues",
-           "Execute", "Prove", "BfzError", "LIB_PATH", "init", "set_num_queries", "guests"]
+           "Execute", "Prove", "BfzError", "LIB_PATH", "init", "set_num_queries", "set_pcs_variant", "proof_to_bincode",
+           "proof_from_bincode", "guests"]

@@ -42,6 +42,7 @@ ALLTOALL_FN = ctypes.CFUNCTYPE(c_int, c_void_p)
 SIGNATURES = [
     ("bfz_init", c_int, [c_int]),
     ("bfz_last_error", c_char_p, []),
+    ("bfz_build_id", c_char_p, []),
     ("bfz_device_name", c_int, [c_char_p, c_size_t]),
     ("bfz_free", None, [c_void_p]),
     ("bfz_synchronize", c_int, []),
@@ -71,6 +72,12 @@ SIGNATURES = [
                                        ALLTOALL_FN, ALLGATHER_FN, c_void_p, POINTER(c_uint32),
                                        c_size_t, POINTER(c_size_t)]),
     ("bfz_set_num_queries", c_int, [c_int]),
+    ("bfz_set_pcs_variant", c_int, [c_int]),
+    ("bfz_proof_to_bincode", c_int, [POINTER(c_uint8), c_size_t, c_int, POINTER(POINTER(c_uint8)),
+                                     POINTER(c_size_t)]),
+    ("bfz_proof_from_bincode", c_int, [POINTER(c_uint8), c_size_t, c_int,
+                                       POINTER(POINTER(c_uint8)), POINTER(c_size_t)]),
+    ("bfz_verify_bincode", c_int, [c_char_p, POINTER(c_uint32), POINTER(c_uint8), c_size_t, c_int]),
     ("bfz_coset_lde", c_int, [POINTER(c_uint32), c_size_t, c_size_t, c_uint32, POINTER(c_uint32)]),
     ("bfz_commit", c_int, [POINTER(POINTER(c_uint32)), POINTER(c_size_t), POINTER(c_size_t),
                            c_size_t, POINTER(c_uint32)]),
@@ -99,6 +106,12 @@ def lib() -> ctypes.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        built = L.bfz_build_id().decode()
+        from . import srchash
+        want = srchash.source_hash()
+        if built != want:
+            raise BfzError(f"{LIB_PATH} was built from other sources (build id {built}, sources "
+                           f"{want}): rebuild with `make -C zkvm-brainfuck_amd`")
         _lib = L
     return _lib
 

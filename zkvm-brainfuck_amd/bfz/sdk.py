@@ -49,13 +49,63 @@ class BfProvingKey:
             pass
 
 
+# KoalaBear word representation inside bincode (bfz_proof_to_bincode): the p3 MontyField31
+# serde writes the Montgomery word [p3-recalled]; CANONICAL is the alternative.
+FIELD_MONTGOMERY, FIELD_CANONICAL = 0, 1
+
+
+def proof_to_bincode(proof: bytes, field_repr: int = FIELD_MONTGOMERY) -> bytes:
+    """BFZ1 normal form -> bincode::serialize(&ShardProof<KoalaBearPoseidon2>) bytes
+    (crates/stark/src/types.rs:66-73, crates/core/machine/src/utils/prove.rs:46)."""
+    buf, n = u8buf(proof)
+    ptr = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    check(lib().bfz_proof_to_bincode(buf, n, int(field_repr), ctypes.byref(ptr), ctypes.byref(olen)))
+    return take_bytes(ptr, olen.value)
+
+
+def proof_from_bincode(data: bytes, field_repr: int = FIELD_MONTGOMERY) -> bytes:
+    """bincode ShardProof bytes -> BFZ1 normal form (chip_ordering applied)."""
+    buf, n = u8buf(data)
+    ptr = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    check(lib().bfz_proof_from_bincode(buf, n, int(field_repr), ctypes.byref(ptr),
+                                       ctypes.byref(olen)))
+    return take_bytes(ptr, olen.value)
+
+
 @dataclass
 class BfProofWithPublicValues:
-    """crates/sdk/src/proof.rs:10-13 — the proof (BFZ1 normal-form bytes) and stdin."""
+    """crates/sdk/src/proof.rs:10-13 — the proof (BFZ1 normal-form bytes) and stdin.
+
+    `to_bincode()` gives the reference's serialized form of this struct, bincode of
+    { proof: ShardProof<CoreSC>, stdin: Vec<u8> }; `from_bincode()` reads it back."""
     proof: bytes
     stdin: bytes
     public_values: bytes = b""
     cycles: int = 0
+
+    def to_bincode(self, field_repr: int = FIELD_MONTGOMERY) -> bytes:
+        import struct
+        return (proof_to_bincode(self.proof, field_repr) + struct.pack("<Q", len(self.stdin))
+                + bytes(self.stdin))
+
+    @staticmethod
+    def from_bincode(data: bytes, field_repr: int = FIELD_MONTGOMERY) -> "BfProofWithPublicValues":
+        import struct
+        # the ShardProof is everything before the trailing Vec<u8> stdin; its length is found by
+        # trying the stdin lengths the tail can hold (the u64 prefix sits right before stdin)
+        for k in range(0, len(data) - 7):
+            cut = len(data) - k - 8
+            if cut < 0:
+                break
+            if struct.unpack_from("<Q", data, cut)[0] == k:
+                try:
+                    pf = proof_from_bincode(data[:cut], field_repr)
+                except BfzError:
+                    continue
+                return BfProofWithPublicValues(proof=pf, stdin=bytes(data[cut + 8:]))
+        raise BfzError("not a bincode BfProofWithPublicValues")
 
 
 class Execute:
@@ -121,6 +171,13 @@ class ProverClient:
         commit = (ctypes.c_uint32 * 8)(*vk.commit)
         check(lib().bfz_verify(vk.elf.encode(), commit, buf, n))
 
+    def verify_bincode(self, shard_proof: bytes, vk: BfVerifyingKey,
+                       field_repr: int = FIELD_MONTGOMERY) -> None:
+        """StarkMachine::verify on the reference's bincode ShardProof bytes."""
+        buf, n = u8buf(shard_proof)
+        commit = (ctypes.c_uint32 * 8)(*vk.commit)
+        check(lib().bfz_verify_bincode(vk.elf.encode(), commit, buf, n, int(field_repr)))
+
 
 # BfAir::chips() order (crates/core/machine/src/brainfuck/mod.rs:53-81) = chip index in the ABI
 CHIPS = ("Cpu", "Program", "AddSub", "Jump", "Memory", "Byte", "MemoryInstrs", "IO")
@@ -169,5 +226,11 @@ class CoreProver:
 
 
 def set_num_queries(q: int) -> None:
-    """FRI_QUERIES override (crates/stark/src/kb31_poseidon2.rs:59-62)."""
+    """FRI_QUERIES override (crates/stark/src/kb31_poseidon2.rs:59-62); 0 = environment/84."""
     check(lib().bfz_set_num_queries(int(q)))
+
+
+def set_pcs_variant(observe_openings: int) -> None:
+    """Decision D1: 1 = opened values observed before FRI alpha (default),
+    0 = alpha sampled first, -1 = environment BFZ_OBSERVE_OPENINGS."""
+    check(lib().bfz_set_pcs_variant(int(observe_openings)))

@@ -13,7 +13,7 @@
 #include "merkle.h"
 #include "ntt.h"
 #include "pcs_sharded.h"
-#include "pcs_sharded.h"
+#include "proof.h"
 #include "prover.h"
 #include "tracegen.h"
 #include "verifier.h"
@@ -30,6 +30,7 @@ namespace {
 std::mutex g_mu;
 thread_local std::string g_err;
 int g_num_queries = -1;
+int g_observe_openings = -1;  // -1: BFZ_OBSERVE_OPENINGS / default
 
 int fail(const std::exception& e, int code = -1) {
   g_err = e.what();
@@ -38,6 +39,7 @@ int fail(const std::exception& e, int code = -1) {
 bfz::ProveOptions opts() {
   bfz::ProveOptions o;
   o.num_queries = g_num_queries > 0 ? g_num_queries : bfz::num_queries_from_env();
+  o.observe_openings = g_observe_openings >= 0 ? g_observe_openings != 0 : bfz::observe_openings_from_env();
   return o;
 }
 template <class F>
@@ -55,18 +57,31 @@ int guarded(F&& f) {
 
 extern "C" {
 
+// One process drives one device: the stream, the allocator pool, the twiddle and selector
+// caches and the pinned staging arena are process-wide and belong to the first device bound.
 int bfz_init(int device) {
   return guarded([&] {
+    static int bound = -1;
     int n = 0;
     HIP_CHECK(hipGetDeviceCount(&n));
     if (n <= 0) throw std::runtime_error("no HIP device");
+    if (device < 0 || device >= n) throw std::runtime_error("bfz_init: device index out of range");
+    if (bound >= 0 && bound != device)
+      throw std::runtime_error("bfz_init: this process is already bound to device " +
+                               std::to_string(bound) + " (one process per GPU)");
     HIP_CHECK(hipSetDevice(device));
     (void)bfz::stream();
+    bound = device;
     return 0;
   });
 }
 
 const char* bfz_last_error(void) { return g_err.c_str(); }
+
+#ifndef BFZ_SRC_HASH
+#error "BFZ_SRC_HASH must be defined by the Makefile (bfz/srchash.py)"
+#endif
+const char* bfz_build_id(void) { return BFZ_SRC_HASH; }
 
 int bfz_device_name(char* buf, size_t cap) {
   return guarded([&] {
@@ -200,8 +215,11 @@ int bfz_prove_traces(const bfz_pk* pk, const int* chips, const uint32_t* const* 
 int bfz_verify(const char* elf, const uint32_t vk_commit[8], const uint8_t* proof, size_t len) {
   return guarded([&] {
     std::string why;
-    const int nq = g_num_queries > 0 ? g_num_queries : bfz::num_queries_from_env();
-    if (!bfz::verify_proof(elf, vk_commit, proof, len, nq, &why)) {
+    const bfz::ProveOptions o = opts();
+    bfz::VerifyOptions vo;
+    vo.num_queries = o.num_queries;
+    vo.observe_openings = o.observe_openings;
+    if (!bfz::verify_proof(elf, vk_commit, proof, len, vo, &why)) {
       g_err = "verification failed: " + why;
       return -3;
     }
@@ -323,9 +341,63 @@ int bfz_commit_fri_sharded(const uint32_t* d_cols, int log_n, size_t w_local, in
 
 void bfz_record_free(bfz_record* rec) { delete rec; }
 
+int bfz_set_pcs_variant(int observe_openings) {
+  return guarded([&] {
+    if (observe_openings < -1 || observe_openings > 1)
+      throw std::runtime_error("observe_openings must be -1 (environment), 0 or 1");
+    g_observe_openings = observe_openings;
+    return 0;
+  });
+}
+
+int bfz_proof_to_bincode(const uint8_t* proof, size_t len, int field_repr, uint8_t** out,
+                         size_t* out_len) {
+  return guarded([&] {
+    if (field_repr != 0 && field_repr != 1) throw std::runtime_error("field_repr must be 0 or 1");
+    const bfz::ShardProof pf = bfz::decode_bfz1(proof, len);
+    return emit(bfz::encode_bincode(pf, (bfz::FieldRepr)field_repr), out, out_len);
+  });
+}
+
+int bfz_proof_from_bincode(const uint8_t* bytes, size_t len, int field_repr, uint8_t** out,
+                           size_t* out_len) {
+  return guarded([&] {
+    if (field_repr != 0 && field_repr != 1) throw std::runtime_error("field_repr must be 0 or 1");
+    const bfz::ShardProof pf = bfz::decode_bincode(bytes, len, (bfz::FieldRepr)field_repr);
+    return emit(bfz::encode_bfz1(pf), out, out_len);
+  });
+}
+
+int bfz_verify_bincode(const char* elf, const uint32_t vk_commit[8], const uint8_t* bytes,
+                       size_t len, int field_repr) {
+  return guarded([&] {
+    if (field_repr != 0 && field_repr != 1) throw std::runtime_error("field_repr must be 0 or 1");
+    std::string why;
+    const bfz::ProveOptions o = opts();
+    bfz::VerifyOptions vo;
+    vo.num_queries = o.num_queries;
+    vo.observe_openings = o.observe_openings;
+    bfz::ShardProof pf;
+    try {
+      pf = bfz::decode_bincode(bytes, len, (bfz::FieldRepr)field_repr);
+    } catch (const std::exception& e) {
+      g_err = std::string("verification failed: ") + e.what();
+      return -3;
+    }
+    if (!bfz::verify_shard(elf, vk_commit, pf, vo, &why)) {
+      g_err = "verification failed: " + why;
+      return -3;
+    }
+    return 0;
+  });
+}
+
 int bfz_set_num_queries(int q) {
-  g_num_queries = q;
-  return 0;
+  return guarded([&] {
+    if (q < 0 || q > 4096) throw std::runtime_error("num_queries must be in [1, 4096] (0 = FRI_QUERIES/84)");
+    g_num_queries = q;
+    return 0;
+  });
 }
 
 int bfz_coset_lde(const uint32_t* evals, size_t n, size_t w, uint32_t shift, uint32_t* out) {

@@ -136,6 +136,9 @@ hipStream_t stream();
 // stall.  staging_reset() once no earlier copy can be pending (after a stream synchronize).
 void upload_async(void* dst, const void* src, size_t bytes, hipStream_t st);
 void staging_reset();
+// Large pageable host -> device copy through double-buffered pinned chunks (runtime.hip);
+// returns when the data has arrived.
+void upload_bulk(void* dst, const void* src, size_t bytes, hipStream_t st);
 
 // Per-launch HIP-event timing of one kernel family (the roofline kernel of bench.py):
 // when `on`, callers bracket each launch with begin()/end(bytes); collect() resolves the

@@ -26,6 +26,9 @@ void coset_lde(const uint32_t* evals, size_t n, int w, uint32_t shift, uint32_t*
 void transpose_bitrev(const uint32_t* rowmajor, size_t n, int w, uint32_t* colmajor,
                       hipStream_t st);
 
+// Number of waves that saw a word >= p in d[0..n) (0 iff every word is canonical); syncs st.
+size_t count_noncanonical(const uint32_t* d, size_t n, hipStream_t st);
+
 // Column-major (H x w) -> row-major, row order unchanged.
 void transpose_to_rowmajor(const uint32_t* colmajor, size_t H, int w, uint32_t* rowmajor,
                            hipStream_t st);

@@ -709,6 +709,29 @@ void transpose_to_rowmajor(const uint32_t* colmajor, size_t H, int w, uint32_t* 
   KCHECK();
 }
 
+// Counts words >= p (non-canonical Montgomery words) into *count (atomic, wave-aggregated).
+__global__ __launch_bounds__(256) void k_count_noncanonical(const uint32_t* __restrict__ a,
+                                                            size_t n, unsigned* count) {
+  unsigned bad = 0;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    bad += a[i] >= kb::P;
+  const unsigned long long any = __ballot(bad != 0);
+  if (any && (threadIdx.x & 63) == 0) atomicAdd(count, 1u);
+}
+
+size_t count_noncanonical(const uint32_t* d, size_t n, hipStream_t st) {
+  DBuf<unsigned> c(1);
+  HIP_CHECK(hipMemsetAsync(c.p, 0, sizeof(unsigned), st));
+  hipLaunchKernelGGL(k_count_noncanonical, dim3(std::min<size_t>(ceil_div(n, 256), 4096)),
+                     dim3(256), 0, st, d, n, c.p);
+  KCHECK();
+  unsigned h = 0;
+  HIP_CHECK(hipMemcpyAsync(&h, c.p, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+  return h;
+}
+
 void transpose_bitrev(const uint32_t* rowmajor, size_t n, int w, uint32_t* colmajor,
                       hipStream_t st) {
   hipLaunchKernelGGL(k_transpose_bitrev, dim3(ceil_div(n, 64)), dim3(256), 0, st, rowmajor,

@@ -76,6 +76,9 @@ void commit_lde(CMat& cm, const uint32_t* evals, size_t n, int w, uint32_t domai
 struct ProveOptions {
   int num_queries = 84;
   bool timing = false;
+  // Decision D1 ([p3-recalled]): TwoAdicFriPcs::open observes every opened
+  // value before sampling the FRI batching challenge alpha (true), or samples alpha first (false)
+  bool observe_openings = true;
 };
 
 // Full core proof of (program, stdin) in the BFZ1 normal form.
@@ -98,5 +101,6 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
                                   StageTimes* times);
 
 int num_queries_from_env();
+bool observe_openings_from_env();  // BFZ_OBSERVE_OPENINGS = 1 (default) | 0
 
 }  // namespace bfz

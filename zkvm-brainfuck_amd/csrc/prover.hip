@@ -8,6 +8,7 @@
 #include "prover.h"
 
 #include <algorithm>
+#include <cerrno>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -26,9 +27,25 @@ using namespace kb;
 static constexpr int LOG_BLOWUP = 1;
 static constexpr int POW_BITS = 16;
 
+// kb31_poseidon2.rs:59-62: `value.parse().unwrap()` into a usize -- anything but a whole
+// positive decimal number is an error (the reference panics), never a silent 0 or default.
 int num_queries_from_env() {
-  const char* s = std::getenv("FRI_QUERIES");  // kb31_poseidon2.rs:59-62
-  return s ? std::atoi(s) : 84;
+  const char* s = std::getenv("FRI_QUERIES");
+  if (!s) return 84;
+  char* end = nullptr;
+  errno = 0;
+  const long v = std::strtol(s, &end, 10);
+  if (errno || end == s || *end != '\0' || v <= 0 || v > 4096)
+    throw std::runtime_error(std::string("FRI_QUERIES is not a positive query count: '") + s + "'");
+  return (int)v;
+}
+
+bool observe_openings_from_env() {
+  const char* s = std::getenv("BFZ_OBSERVE_OPENINGS");
+  if (!s) return true;
+  if (!std::strcmp(s, "1")) return true;
+  if (!std::strcmp(s, "0")) return false;
+  throw std::runtime_error(std::string("BFZ_OBSERVE_OPENINGS must be 0 or 1, not '") + s + "'");
 }
 
 // ------------------------------------------------------------------------ challenger
@@ -219,14 +236,18 @@ void upload_host_traces(const int* chips, const uint32_t* const* mats, const siz
     const int w = CHIP_INFO[c].main_w;
     if ((size_t)w != widths[i])
       throw std::runtime_error(std::string("traces: width mismatch for ") + CHIP_INFO[c].name);
-    if (h == 0 || (h & (h - 1)) || h > ((size_t)1 << 23))
-      throw std::runtime_error(std::string("traces: height not a power of two <= 2^23 for ") +
+    // height >= 2: a 1-row trace has a 2-row LDE that the FRI commit phase never folds into
+    if (h < 2 || (h & (h - 1)) || h > ((size_t)1 << 23))
+      throw std::runtime_error(std::string("traces: height not a power of two in [2, 2^23] for ") +
                                CHIP_INFO[c].name);
     DBuf<uint32_t> rm(h * w);
-    HIP_CHECK(hipMemcpyAsync(rm.p, mats[i], h * w * 4, hipMemcpyHostToDevice, st));
+    upload_bulk(rm.p, mats[i], h * w * 4, st);
+    // KoalaBear words are Montgomery residues < p; a larger word breaks mmul's b < p bound
+    if (count_noncanonical(rm.p, h * w, st))
+      throw std::runtime_error(std::string("traces: non-canonical field word (>= p) in ") +
+                               CHIP_INFO[c].name);
     DBuf<uint32_t> ev(h * w);
     transpose_bitrev(rm.p, h, w, ev.p, st);
-    HIP_CHECK(hipStreamSynchronize(st));
     dt.chips.push_back(c);
     dt.evals.push_back(std::move(ev));
     dt.heights.push_back(h);
@@ -424,11 +445,12 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
   std::vector<EF> opened(nvals);
   HIP_CHECK(hipMemcpyAsync(opened.data(), opened_d.p, nvals * sizeof(EF), hipMemcpyDeviceToHost, st));
   HIP_CHECK(hipStreamSynchronize(st));
-  for (int r = 0; r < 4; r++)
-    for (size_t i = 0; i < rounds[r]->mats.size(); i++)
-      for (int j = 0; j < mp[r][i].npts; j++)
-        for (int c = 0; c < rounds[r]->mats[i].lde.width; c++)
-          ch.observe_ef(opened[mp[r][i].off[j] + c]);
+  if (opt.observe_openings)  // decision D1: opened values enter the transcript
+    for (int r = 0; r < 4; r++)
+      for (size_t i = 0; i < rounds[r]->mats.size(); i++)
+        for (int j = 0; j < mp[r][i].npts; j++)
+          for (int c = 0; c < rounds[r]->mats[i].lde.width; c++)
+            ch.observe_ef(opened[mp[r][i].off[j] + c]);
   const EF fri_alpha = ch.sample_ef();
 
   // ---- reduced openings per LDE height: every height's column descriptors go up in one copy

@@ -1,7 +1,10 @@
 // Process-wide device state: allocator pool, stream, twiddle tables.
 #include "gpu.h"
 
+#include <algorithm>
 #include <cstring>
+#include <thread>
+#include <vector>
 
 namespace bfz {
 
@@ -65,6 +68,57 @@ void upload_async(void* dst, const void* src, size_t bytes, hipStream_t st) {
   s.off += need;
   std::memcpy(slot, src, bytes);
   HIP_CHECK(hipMemcpyAsync(dst, slot, bytes, hipMemcpyHostToDevice, st));
+}
+
+// Bulk host -> device copy of a pageable buffer (host traces, executor events): chunks go
+// through two pinned buffers, each filled by several host threads while the DMA of the other
+// is in flight, so the copy runs near the PCIe rate instead of the runtime's synchronous
+// pageable path.  Returns when the data is on the device.
+void upload_bulk(void* dst, const void* src, size_t bytes, hipStream_t st) {
+  if (!bytes) return;
+  constexpr size_t CHUNK = (size_t)32 << 20;
+  constexpr int NTHR = 8;
+  struct Bulk {
+    uint8_t* buf[2] = {nullptr, nullptr};
+    hipEvent_t done[2];
+  };
+  static Bulk* b = [] {
+    auto* x = new Bulk();
+    for (int i = 0; i < 2; i++) {
+      HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&x->buf[i]), CHUNK, hipHostMallocDefault));
+      HIP_CHECK(hipEventCreateWithFlags(&x->done[i], hipEventDisableTiming));
+    }
+    return x;
+  }();
+  if (bytes <= ((size_t)1 << 20)) {  // small: one staged copy
+    const uint8_t* s = static_cast<const uint8_t*>(src);
+    HIP_CHECK(hipEventSynchronize(b->done[0]));
+    std::memcpy(b->buf[0], s, bytes);
+    HIP_CHECK(hipMemcpyAsync(dst, b->buf[0], bytes, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipEventRecord(b->done[0], st));
+    HIP_CHECK(hipEventSynchronize(b->done[0]));
+    return;
+  }
+  const uint8_t* s = static_cast<const uint8_t*>(src);
+  uint8_t* d = static_cast<uint8_t*>(dst);
+  int k = 0;
+  for (size_t off = 0; off < bytes; off += CHUNK, k ^= 1) {
+    const size_t n = std::min(CHUNK, bytes - off);
+    HIP_CHECK(hipEventSynchronize(b->done[k]));  // buffer k's previous DMA has finished
+    std::vector<std::thread> th;
+    const size_t per = (n + NTHR - 1) / NTHR;
+    for (int t = 0; t < NTHR; t++) {
+      const size_t a = t * per;
+      if (a >= n) break;
+      const size_t len = std::min(per, n - a);
+      th.emplace_back([=] { std::memcpy(b->buf[k] + a, s + off + a, len); });
+    }
+    for (auto& t : th) t.join();
+    HIP_CHECK(hipMemcpyAsync(d + off, b->buf[k], n, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipEventRecord(b->done[k], st));
+  }
+  HIP_CHECK(hipEventSynchronize(b->done[0]));
+  HIP_CHECK(hipEventSynchronize(b->done[1]));
 }
 
 Twiddles& twiddles() {

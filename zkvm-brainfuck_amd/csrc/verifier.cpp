@@ -26,38 +26,6 @@ namespace {
 
 constexpr int LOG_BLOWUP = 1, POW_BITS = 16, MAX_CPU_LOG_DEGREE = 22;
 
-struct Reader {
-  const uint8_t* p;
-  size_t n, off = 0;
-  uint32_t u32() {
-    if (off + 4 > n) throw std::runtime_error("truncated proof");
-    uint32_t v;
-    std::memcpy(&v, p + off, 4);
-    off += 4;
-    return v;
-  }
-  uint32_t fp() {
-    const uint32_t v = u32();
-    if (v >= P) throw std::runtime_error("non-canonical field element");
-    return to_mont(v);
-  }
-  EF ef() {
-    EF e;
-    for (int i = 0; i < 4; i++) e.c[i] = fp();
-    return e;
-  }
-  void digest(uint32_t* d) {
-    for (int i = 0; i < 8; i++) d[i] = fp();
-  }
-  std::vector<EF> efs(size_t maxn = 4096) {
-    const uint32_t k = u32();
-    if (k > maxn) throw std::runtime_error("bad vector length");
-    std::vector<EF> v(k);
-    for (auto& e : v) e = ef();
-    return v;
-  }
-};
-
 struct HornerAcc {
   EF acc = ef_zero();
   EF alpha;
@@ -179,7 +147,19 @@ int sent_byte_lookups(int chip) { return chip == CHIP_CPU ? 7 : chip == CHIP_ADD
 }  // namespace
 
 bool verify_proof(const std::string& src, const uint32_t vk_commit[8], const uint8_t* proof,
-                  size_t len, int num_queries, std::string* why) {
+                  size_t len, const VerifyOptions& opt, std::string* why) {
+  ShardProof pf;
+  try {
+    pf = decode_bfz1(proof, len);
+  } catch (const std::exception& e) {
+    if (why) *why = e.what();
+    return false;
+  }
+  return verify_shard(src, vk_commit, pf, opt, why);
+}
+
+bool verify_shard(const std::string& src, const uint32_t vk_commit[8], const ShardProof& pf,
+                  const VerifyOptions& opt, std::string* why) {
   try {
     Program prog = Program::parse(src);
     // vk.chip_information: prep matrices sorted by (Reverse(height), name)
@@ -194,46 +174,34 @@ bool verify_proof(const std::string& src, const uint32_t vk_commit[8], const uin
         (prep[1].log_n == prep[0].log_n && std::strcmp("Byte", "Program") < 0))
       std::swap(prep[0], prep[1]);
 
-    Reader r{proof, len};
-    if (r.u32() != 0x315a4642u) throw std::runtime_error("bad magic");
-    const uint32_t nc = r.u32();
-    if (nc == 0 || nc > NUM_CHIPS) throw std::runtime_error("bad chip count");
-    std::vector<int> chip(nc);
-    std::vector<bool> seen(NUM_CHIPS, false);
-    for (uint32_t i = 0; i < nc; i++) {
-      chip[i] = (int)r.u32();
-      if (chip[i] < 0 || chip[i] >= NUM_CHIPS || seen[chip[i]]) throw std::runtime_error("bad chip id");
-      seen[chip[i]] = true;
-      const uint32_t l = r.u32();
-      if (l != std::strlen(CHIP_INFO[chip[i]].name) || r.off + l > len ||
-          std::memcmp(proof + r.off, CHIP_INFO[chip[i]].name, l) != 0)
-        throw std::runtime_error("chip name mismatch");
-      r.off += l;
+    const uint32_t nc = (uint32_t)pf.chips.size();
+    if (nc == 0 || nc > NUM_CHIPS || pf.opened.size() != nc) throw std::runtime_error("bad chip count");
+    const std::vector<int>& chip = pf.chips;
+    {
+      std::vector<bool> seen(NUM_CHIPS, false);
+      for (int c : chip) {
+        if (c < 0 || c >= NUM_CHIPS || seen[c]) throw std::runtime_error("bad chip id");
+        seen[c] = true;
+      }
     }
-    uint32_t main_root[8], perm_root[8], quot_root[8];
-    r.digest(main_root);
-    r.digest(perm_root);
-    r.digest(quot_root);
+    const uint32_t* main_root = pf.main_root.data();
+    const uint32_t* perm_root = pf.perm_root.data();
+    const uint32_t* quot_root = pf.quot_root.data();
     struct ChipOpen {
       int log_n;
-      std::vector<EF> pl, pn, ml, mn, perml, permn, q[2];
+      const std::vector<EF> &pl, &pn, &ml, &mn, &perml, &permn;
+      const std::vector<EF>* q;
       EF cumsum;
     };
-    std::vector<ChipOpen> co(nc);
+    std::vector<ChipOpen> co;
+    co.reserve(nc);
     for (uint32_t i = 0; i < nc; i++) {
-      ChipOpen& c = co[i];
-      c.log_n = (int)r.u32();
-      if (c.log_n > 23) throw std::runtime_error("log degree too large");
-      c.pl = r.efs();
-      c.pn = r.efs();
-      c.ml = r.efs();
-      c.mn = r.efs();
-      c.perml = r.efs();
-      c.permn = r.efs();
-      if (r.u32() != 2) throw std::runtime_error("bad quotient chunk count");
-      c.q[0] = r.efs();
-      c.q[1] = r.efs();
-      c.cumsum = r.ef();
+      const ChipOpened& o = pf.opened[i];
+      // unsigned: a huge word must not become a negative shift count below
+      if (o.log_degree < 1 || o.log_degree > 23) throw std::runtime_error("log degree out of range");
+      co.push_back(ChipOpen{(int)o.log_degree, o.prep_local, o.prep_next, o.main_local, o.main_next,
+                            o.perm_local, o.perm_next, o.quotient, o.cumsum});
+      const ChipOpen& c = co.back();
       const int ch = chip[i];
       const size_t pw = CHIP_INFO[ch].prep_w;
       if (c.ml.size() != (size_t)CHIP_INFO[ch].main_w || c.mn.size() != c.ml.size() ||
@@ -289,72 +257,57 @@ bool verify_proof(const std::string& src, const uint32_t vk_commit[8], const uin
         rounds[3].push_back(VMat{c.log_n, mmul(to_mont(3), k ? w2n : ONE), 4, 1, {zeta, zeta},
                                  {&c.q[k], &c.q[k]}});
     }
-    for (int rr = 0; rr < 4; rr++)
-      for (const VMat& m : rounds[rr])
-        for (int p = 0; p < m.np; p++)
-          for (int c = 0; c < m.w; c++) ch.observe_ef((*m.v[p])[c]);
+    if (opt.observe_openings)  // decision D1: opened values enter the transcript
+      for (int rr = 0; rr < 4; rr++)
+        for (const VMat& m : rounds[rr])
+          for (int p = 0; p < m.np; p++)
+            for (int c = 0; c < m.w; c++) ch.observe_ef((*m.v[p])[c]);
     const EF fri_alpha = ch.sample_ef();
-    const uint32_t ncommit = r.u32();
+    const uint32_t ncommit = (uint32_t)pf.commit_roots.size();
     if (ncommit > 30) throw std::runtime_error("too many FRI rounds");
-    std::vector<std::array<uint32_t, 8>> croots(ncommit);
+    const int log_max = (int)ncommit + LOG_BLOWUP;
+    {  // the commit phase folds the tallest LDE down to 2^LOG_BLOWUP: every height must fit
+      int lh_max = 0;
+      for (int rr = 0; rr < 4; rr++)
+        for (const VMat& m : rounds[rr]) lh_max = std::max(lh_max, m.log_n + LOG_BLOWUP);
+      if (lh_max != log_max) throw std::runtime_error("FRI round count does not match the tallest matrix");
+    }
     std::vector<EF> betas(ncommit);
     for (uint32_t i = 0; i < ncommit; i++) {
-      r.digest(croots[i].data());
-      ch.observe_digest(croots[i].data());
+      ch.observe_digest(pf.commit_roots[i].data());
       betas[i] = ch.sample_ef();
     }
-    const uint32_t nq = r.u32();
-    if ((int)nq != num_queries) throw std::runtime_error("wrong number of queries");
-    const size_t qstart = r.off;
-    // skip to final poly / witness
-    for (uint32_t q = 0; q < nq; q++) {
-      const uint32_t nr = r.u32();
-      for (uint32_t x = 0; x < nr; x++) {
-        const uint32_t nm = r.u32();
-        for (uint32_t i = 0; i < nm; i++) r.off += 4 * (size_t)r.u32();
-        r.off += 32 * (size_t)r.u32();
-      }
-      const uint32_t ns = r.u32();
-      for (uint32_t s = 0; s < ns; s++) {
-        r.off += 16;
-        r.off += 32 * (size_t)r.u32();
-      }
-      if (r.off > len) throw std::runtime_error("truncated proof");
-    }
-    const EF final_poly = r.ef();
-    const uint32_t witness = r.u32();
-    if (r.off != len) throw std::runtime_error("trailing bytes");
+    const uint32_t nq = (uint32_t)pf.queries.size();
+    if ((int)nq != opt.num_queries) throw std::runtime_error("wrong number of queries");
+    const EF final_poly = pf.final_poly;
     ch.observe_ef(final_poly);
-    if (witness >= P || !ch.check_witness(POW_BITS, witness)) throw std::runtime_error("bad PoW witness");
-    const int log_max = (int)ncommit + LOG_BLOWUP;
-    r.off = qstart;
+    if (!ch.check_witness(POW_BITS, from_mont(pf.pow_witness))) throw std::runtime_error("bad PoW witness");
     const uint32_t* roots[4] = {vk_commit, main_root, perm_root, quot_root};
     const uint32_t half = to_mont_c((P + 1) / 2);
     (void)half;
     for (uint32_t q = 0; q < nq; q++) {
+      const QueryProof& qp = pf.queries[q];
       const size_t index = ch.sample_bits(log_max);
-      if (r.u32() != 4) throw std::runtime_error("bad round count");
+      if (qp.inputs.size() != 4) throw std::runtime_error("bad round count");
       std::map<int, std::pair<EF, EF>> ro;  // log height -> (alpha_pow, ro)
       for (int rr = 0; rr < 4; rr++) {
-        const uint32_t nm = r.u32();
+        const BatchOpening& bo = qp.inputs[rr];
+        const size_t nm = bo.rows.size();
         if (nm != rounds[rr].size()) throw std::runtime_error("bad matrix count");
-        std::vector<std::vector<uint32_t>> rows(nm);
+        const std::vector<std::vector<uint32_t>>& rows = bo.rows;
         std::vector<size_t> heights(nm);
         std::vector<int> widths(nm);
         int lbmax = 0;
-        for (uint32_t i = 0; i < nm; i++) {
-          const uint32_t w = r.u32();
+        for (size_t i = 0; i < nm; i++) {
+          const size_t w = rows[i].size();
           if ((int)w != rounds[rr][i].w) throw std::runtime_error("bad row width");
-          rows[i].resize(w);
-          for (uint32_t c = 0; c < w; c++) rows[i][c] = r.fp();
           heights[i] = (size_t)1 << (rounds[rr][i].log_n + LOG_BLOWUP);
           widths[i] = (int)w;
           lbmax = std::max(lbmax, rounds[rr][i].log_n + LOG_BLOWUP);
         }
-        const uint32_t pl = r.u32();
-        if ((int)pl != lbmax) throw std::runtime_error("bad path length");
-        std::vector<uint32_t> path(8 * pl);
-        for (auto& x : path) x = r.fp();
+        if ((int)bo.path.size() != lbmax) throw std::runtime_error("bad path length");
+        std::vector<uint32_t> path(8 * bo.path.size());
+        for (size_t L = 0; L < bo.path.size(); L++) std::memcpy(&path[8 * L], bo.path[L].data(), 32);
         const size_t ridx = index >> (log_max - lbmax);
         if (!verify_batch(roots[rr], heights, widths, ridx, rows, path))
           throw std::runtime_error("input Merkle opening rejected");
@@ -376,7 +329,7 @@ bool verify_proof(const std::string& src, const uint32_t vk_commit[8], const uin
         }
       }
       // verify_query
-      if (r.u32() != ncommit) throw std::runtime_error("bad step count");
+      if (qp.steps.size() != ncommit) throw std::runtime_error("bad step count");
       EF folded = ef_zero();
       size_t idx = index;
       for (uint32_t s = 0; s < ncommit; s++) {
@@ -386,18 +339,18 @@ bool verify_proof(const std::string& src, const uint32_t vk_commit[8], const uin
           folded = ef_add(folded, it->second.second);
           ro.erase(it);
         }
-        const EF sib = r.ef();
-        const uint32_t pl = r.u32();
-        if ((int)pl != lfh) throw std::runtime_error("bad FRI path length");
-        std::vector<uint32_t> path(8 * pl);
-        for (auto& x : path) x = r.fp();
+        const CommitPhaseStep& stp = qp.steps[s];
+        const EF sib = stp.sibling;
+        if ((int)stp.path.size() != lfh) throw std::runtime_error("bad FRI path length");
+        std::vector<uint32_t> path(8 * stp.path.size());
+        for (size_t L = 0; L < stp.path.size(); L++) std::memcpy(&path[8 * L], stp.path[L].data(), 32);
         EF ev[2];
         ev[idx & 1] = folded;
         ev[(idx & 1) ^ 1] = sib;
         std::vector<std::vector<uint32_t>> row(1, std::vector<uint32_t>(8));
         std::memcpy(row[0].data(), ev[0].c, 16);
         std::memcpy(row[0].data() + 4, ev[1].c, 16);
-        if (!verify_batch(croots[s].data(), {(size_t)1 << lfh}, {8}, idx >> 1, row, path))
+        if (!verify_batch(pf.commit_roots[s].data(), {(size_t)1 << lfh}, {8}, idx >> 1, row, path))
           throw std::runtime_error("FRI commit-phase opening rejected");
         idx >>= 1;
         const uint32_t x0 = mpow(two_adic_gen(lfh + 1), bitrev32((uint32_t)idx, lfh));

@@ -1,14 +1,26 @@
-// Host verifier for BFZ1 proofs: Verifier::verify_shard (crates/stark/src/verifier.rs:27-329)
+// Host verifier: Verifier::verify_shard (crates/stark/src/verifier.rs:27-329)
 // + TwoAdicFriPcs::verify / fri::verifier [p3-recalled] + BfProver::verify's CPU-degree cap
-// (crates/prover/src/verify.rs:10-36).
+// (crates/prover/src/verify.rs:10-36), over a decoded ShardProof (proof.h) -- so the same checks
+// run on the BFZ1 normal form and on the reference's bincode bytes.
 #pragma once
 #include <cstddef>
 #include <cstdint>
 #include <string>
 
+#include "proof.h"
+
 namespace bfz {
 
+struct VerifyOptions {
+  int num_queries = 84;
+  bool observe_openings = true;  // PCS transcript variant (decision D1)
+};
+
+bool verify_shard(const std::string& program_src, const uint32_t vk_commit[8], const ShardProof& pf,
+                  const VerifyOptions& opt, std::string* why);
+
+// BFZ1 bytes (decode_bfz1 + verify_shard)
 bool verify_proof(const std::string& program_src, const uint32_t vk_commit[8], const uint8_t* proof,
-                  size_t len, int num_queries, std::string* why);
+                  size_t len, const VerifyOptions& opt, std::string* why);
 
 }  // namespace bfz
