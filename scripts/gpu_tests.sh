@@ -1,7 +1,10 @@
-# GPU parity tests + smoke (run on the GPU box from the repo root)
+# GPU parity tests + smoke (run on the GPU box from the repo root).  Each step has its own
+# time limit and the chain stops at the first failure.
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
-timeout -k 10 1200 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
-echo "exit $?"
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
+timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+echo "exit $rc"
+exit $rc
