@@ -10,8 +10,10 @@ quotient, FRI open and proof assembly.  The executor and the event upload run be
 timed region.  Every rank proves its own replica (no data-path collective: replicas only), so
 the job is weak-scaled; `value` is the wall time of one step (max over ranks).
 
-Also reported: roofline of the coset-LDE (NTT) kernels, measured live with HIP events on
-the prover's stream, and the oracle (CPU restatement) timed on a bounded sample.
+Also reported: the HBM roofline of the coset-LDE (NTT) kernels on SURVEY 8(d)'s basis
+(12*n*w B per LDE / NTT kernel time, per-launch HIP events on the prover's stream), their
+VALU-issue fraction, the Poseidon2 kernels' VALU fraction, and the oracle (CPU restatement)
+proving the same headline workload on the host cores.
 """
 import argparse
 import json
@@ -35,9 +37,17 @@ P2_UNITS_PER_PERM = 5548
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01", "pmc_summary.json")
 
 
+# VALU units (full-rate lane-ops) per radix-2 element-stage of a 2^22 coset LDE, from the gfx950
+# ISA of k_ntt_tile<false,14> + k_lde_mid<22> + k_ntt_tile<true,14> (scripts/ntt_isa.py ->
+# profiles/r02/ntt_isa_mix.txt).  Smaller chips' LDEs use the same kernels' shapes within ~5%.
+NTT_UNITS_PER_ELEM_STAGE = 7.064
+
+
 def ntt_traffic():
-    """HBM bytes per k_ntt_r16 launch from the committed rocprofv3 PMC passes
-    (scripts/gpu_pmc.sh: FETCH_SIZE x2 per MI355X_MICROARCH.md + WRITE_SIZE, separate runs)."""
+    """(HBM bytes per NTT launch, traffic / per-pass algorithmic bytes) from the committed
+    rocprofv3 PMC passes (scripts/gpu_pmc.sh: FETCH_SIZE x2 per MI355X_MICROARCH.md +
+    WRITE_SIZE, separate runs); per-pass algorithmic = 8 B per element per tile pass, 12 B per
+    input element per k_lde_mid launch."""
     try:
         k = json.load(open(PMC_SUMMARY))["kernels"]
         rows = [v for n, v in k.items() if any(x in n for x in ("k_ntt_r16", "k_ntt_tile", "k_lde_mid"))]
@@ -47,6 +57,58 @@ def ntt_traffic():
         return traffic / launches, traffic / alg
     except (OSError, KeyError, ValueError, ZeroDivisionError):
         return None, None
+
+
+def ntt_roofline(tm):
+    """HBM roofline of the NTT kernels on SURVEY §8(d)'s basis: 12*n*w algorithmic bytes per
+    coset LDE of an n x w matrix (read n, write 2n), summed over the proof, divided by the
+    summed per-launch HIP-event time of the NTT kernels (k_ntt_tile, k_lde_mid, k_ntt_r16; one
+    LDE = 3 launches = 3 HBM passes).  The per-pass figure (each launch's own read + write) is
+    kept as a secondary field."""
+    if tm.ntt_kernel_ms <= 0:
+        return None
+    launches = max(tm.ntt_kernel_launches, 1)
+    achieved = tm.lde_bytes / (tm.ntt_kernel_ms * 1e-3) / 1e9
+    per_pass = tm.ntt_kernel_bytes / (tm.ntt_kernel_ms * 1e-3) / 1e9
+    alg_per_launch = tm.lde_bytes / launches
+    _, ratio_pass = ntt_traffic()
+    traffic = None
+    if ratio_pass:  # PMC bytes per launch, scaled to this proof's per-pass byte count
+        traffic = ratio_pass * tm.ntt_kernel_bytes / launches
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": round(traffic) if traffic else None,
+            "algorithmic_per_launch": round(alg_per_launch),
+            "traffic_over_algorithmic": round(traffic / alg_per_launch, 3) if traffic else None,
+            "traffic_source": "profiles/r01/pmc_summary.json (FETCH_SIZE x2 + WRITE_SIZE per "
+                              "launch, scaled to this proof's launches)",
+            "basis": "SURVEY 8(d): 12*n*w B per coset LDE (read n, write 2n) / NTT kernel time",
+            "kernel": "coset LDE = k_ntt_tile<false,14> (iDFT stages 0-13) + k_lde_mid<L> (iDFT "
+                      "stages 14.., coset scale, DFT of both halves) + k_ntt_tile<true,14> (DFT "
+                      "stages 13-0 of the 2n outputs)",
+            "launches": tm.ntt_kernel_launches,
+            "avg_launch_us": round(tm.ntt_kernel_ms * 1e3 / launches, 2),
+            "kernel_ms": round(tm.ntt_kernel_ms, 3),
+            "per_pass_gbs": round(per_pass, 1),
+            "per_pass_frac": round(per_pass / HBM_PEAK_GBS, 4),
+            "per_pass_note": "each launch's own read + write (8 B/elem tile pass, 12 B/input "
+                             "elem middle): 3 HBM passes per LDE"}
+
+
+def ntt_valu(tm):
+    """VALU-issue roofline of the same NTT kernels: units per element-stage (ISA) x the proof's
+    element-stages (3*n*log2(n)*w per LDE) / NTT kernel time, against 78.6 T units/s."""
+    if tm.ntt_kernel_ms <= 0 or tm.lde_elem_stages <= 0:
+        return None
+    tops = NTT_UNITS_PER_ELEM_STAGE * tm.lde_elem_stages / (tm.ntt_kernel_ms * 1e-3) / 1e12
+    return {"bound": "valu", "units_per_element_stage": NTT_UNITS_PER_ELEM_STAGE,
+            "element_stages_per_proof": int(tm.lde_elem_stages), "achieved": round(tops, 1),
+            "peak": round(VALU_PEAK_TOPS, 1), "unit": "T full-rate VALU lane-ops/s",
+            "frac": round(tops / VALU_PEAK_TOPS, 4),
+            # 2^22 LDE at 100% VALU issue: 66 element-stages and 12 B per input element
+            "hbm_frac_at_valu_peak": round(12.0 * VALU_PEAK_TOPS * 1e12
+                                           / (NTT_UNITS_PER_ELEM_STAGE * 66) / (HBM_PEAK_GBS * 1e9), 4),
+            "source": "profiles/r02/ntt_isa_mix.txt (scripts/ntt_isa.py 22)"}
 
 
 def poseidon2_roofline(tm):
@@ -64,24 +126,42 @@ def poseidon2_roofline(tm):
             "frac": round(tops / VALU_PEAK_TOPS, 4)}
 
 
-def cpu_baseline(sample_stdin=200):
-    """Oracle (C restatement, OpenMP) proving the fibonacci guest with stdin [200]
-    (722,833 cycles, Cpu 2^20 rows) on the host cores; scaled x4 (trace cells) to the 2^22
-    workload.  Runs in a child process so its OpenMP pool does not perturb the GPU process."""
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline():
+    """The oracle (C restatement of the reference prover, OpenMP) proving the headline workload
+    itself -- FIBO_X4 with stdin [255], Cpu trace 2^22 rows, executor included as in the
+    reference's utils/prove.rs:23-66 -- on the host cores this process may use (its CPU
+    affinity, capped by OMP_NUM_THREADS: the GPU box gives a one-GPU job a 16-core share).
+    Runs in a child process so its OpenMP pool does not perturb the GPU process."""
     code = (
         "import sys,time; sys.path.insert(0,%r); sys.path.insert(0,%r);"
         "import oracle_lib as O; from bfz import guests;"
-        "t=time.time(); O.prove(guests.FIBO,[%d]); print(time.time()-t)"
-    ) % (os.path.join(ROOT, "tests"), os.path.join(ROOT, "zkvm-brainfuck_amd"), sample_stdin)
-    threads = int(os.environ.get("OMP_NUM_THREADS", "16"))
+        "t=time.time(); O.prove(guests.FIBO_X4,[255]); print(time.time()-t)"
+    ) % (os.path.join(ROOT, "tests"), os.path.join(ROOT, "zkvm-brainfuck_amd"))
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    threads = min(avail, int(os.environ.get("OMP_NUM_THREADS") or avail))
     env = dict(os.environ, OMP_NUM_THREADS=str(threads))
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
                          timeout=900)
     secs = float(out.stdout.strip().splitlines()[-1])
-    return {"value": round(secs * 1000.0 * 4.0, 1), "unit": "ms per 2^22-row core proof (x4 scaled)",
+    return {"value": round(secs * 1000.0, 1), "unit": "ms per 2^22-row core proof",
             "cores": threads, "kind": "port",
-            "sample": f"oracle prove of fibonacci guest stdin [{sample_stdin}] (2^20 Cpu rows) "
-                      f"= {secs:.2f} s, scaled x4 by trace cells"}
+            "nproc": os.cpu_count(), "affinity_cpus": avail, "cpu_model": cpu_model(),
+            "sample": f"whole headline workload: oracle prove of FIBO_X4 stdin [255] (3,767,729 "
+                      f"cycles, Cpu 2^22 rows, executor included) = {secs:.2f} s on {threads} "
+                      f"OpenMP threads"}
 
 
 def timed_steps(step, steps, dist=None, sync=lambda: None):
@@ -240,10 +320,6 @@ def main():
 
     if rank == 0:
         lde_gbs = tm.lde_bytes / (tm.lde_ms * 1e-3) / 1e9 if tm.lde_ms > 0 else 0.0
-        ntt_gbs = (tm.ntt_kernel_bytes / (tm.ntt_kernel_ms * 1e-3) / 1e9
-                   if tm.ntt_kernel_ms > 0 else 0.0)
-        ntt_avg_us = tm.ntt_kernel_ms * 1e3 / max(tm.ntt_kernel_launches, 1)
-        traffic_b, traffic_ratio = ntt_traffic()
         # whole job: replicas finish `world` proofs every `ms`; sharded ranks finish one
         job_ms = ms if sharded else ms / world
         line = {
@@ -268,18 +344,8 @@ def main():
             "aggregate_proofs_per_s": round((1 if sharded else world) * 1000.0 / ms, 4),
             "ntt_hbm_gbs": round(lde_gbs, 1),
             "stages_ms": {k: round(v, 3) for k, v in tm.as_dict().items() if k.endswith("_ms")},
-            "roofline": {"bound": "hbm", "achieved": round(ntt_gbs, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(ntt_gbs / HBM_PEAK_GBS, 4),
-                         "traffic": round(traffic_b) if traffic_b else None,
-                         "traffic_over_algorithmic": round(traffic_ratio, 4) if traffic_ratio else None,
-                         "traffic_source": "profiles/r01/pmc_summary.json (bytes per launch)",
-                         "kernel": "NTT kernels: k_ntt_tile (radix-16 contiguous pass, 8 B per "
-                                   "element: one read + one write) and k_lde_mid (fused iDFT "
-                                   "pass 2 + coset scale + DFT pass 1, 12 B per input element)",
-                         "launches": tm.ntt_kernel_launches,
-                         "avg_launch_us": round(ntt_avg_us, 2),
-                         "note": "per-launch HIP events on the prover stream; whole-LDE rate "
-                                 "(12*n*w B per coset LDE) is ntt_hbm_gbs"},
+            "roofline": ntt_roofline(tm),
+            "ntt_valu": ntt_valu(tm),
             "poseidon2": poseidon2_roofline(tm),
             "proof_bytes": len(proof),
         }

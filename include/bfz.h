@@ -53,6 +53,7 @@ typedef struct {
   int ntt_kernel_launches;
   double p2_kernel_ms, p2_perms; /* Poseidon2 leaf/compress kernels: time and permutations */
   int p2_launches;
+  double lde_elem_stages; /* radix-2 element-stages of the coset LDEs: 3*n*log2(n)*w per call */
 } bfz_timings;
 
 int bfz_init(int device);

@@ -27,7 +27,9 @@ def per_kernel(rows):
     agg = collections.defaultdict(lambda: {"launches": 0, "value": 0.0, "grid": 0})
     for r in rows:
         name = r.get("Kernel_Name", "?")
-        key = name.split("(")[0]  # template arguments kept: k_ntt_tile<true, 14> etc.
+        # template arguments kept (k_ntt_tile<true, 14>); "(anonymous namespace)::" is dropped
+        # before cutting the parameter list, or every tracegen kernel collapses into "bfz::"
+        key = name.replace("(anonymous namespace)::", "").split("(")[0]
         a = agg[key]
         a["launches"] += 1
         a["value"] += float(r.get("Counter_Value", 0) or 0)

@@ -17,7 +17,7 @@ def main(root):
     agg = collections.defaultdict(lambda: collections.Counter())
     for f in glob.glob(os.path.join(root, "pmc_sq", "**", "*counter_collection*.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            name = r.get("Kernel_Name", "?").split("(")[0]
+            name = r.get("Kernel_Name", "?").replace("(anonymous namespace)::", "").split("(")[0]
             agg[name][r.get("Counter_Name", "?")] += float(r.get("Counter_Value", 0) or 0)
     rows = sorted(agg.items(), key=lambda kv: -kv[1]["SQ_WAVE_CYCLES"])
     print("# SQ wave-state counters (scripts/gpu_sq.sh + scripts/sq_summary.py; fractions of "

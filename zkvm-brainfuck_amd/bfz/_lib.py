@@ -25,7 +25,7 @@ class Timings(ctypes.Structure):
         ("total_ms", c_double), ("lde_ms", c_double), ("lde_bytes", c_double),
         ("lde_calls", c_int), ("ntt_kernel_ms", c_double), ("ntt_kernel_bytes", c_double),
         ("ntt_kernel_launches", c_int), ("p2_kernel_ms", c_double), ("p2_perms", c_double),
-        ("p2_launches", c_int),
+        ("p2_launches", c_int), ("lde_elem_stages", c_double),
     ]
 
     def as_dict(self) -> dict:

@@ -260,6 +260,7 @@ void fill_timings(const bfz::StageTimes& st, bfz_timings* t) {
   t->p2_kernel_ms = st.p2_kernel_ms;
   t->p2_perms = st.p2_perms;
   t->p2_launches = st.p2_launches;
+  t->lde_elem_stages = st.lde_elem_stages;
 }
 struct ShardScope {  // installs the shard context for one proof
   explicit ShardScope(bfz::ShardCtx* c) { bfz::shard_ctx() = c; }

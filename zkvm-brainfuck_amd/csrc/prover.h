@@ -65,6 +65,7 @@ struct StageTimes {          // milliseconds, measured with HIP events on the pr
   double p2_kernel_ms = 0;   // throughput Poseidon2 kernels (leaves, compress, FRI rows)
   double p2_perms = 0;       // permutations they computed
   int p2_launches = 0;
+  double lde_elem_stages = 0;  // iDFT n + DFT n on each coset half: 3 * n * log2(n) * w per call
 };
 
 std::unique_ptr<ProvingKey> setup(const std::string& program_src);

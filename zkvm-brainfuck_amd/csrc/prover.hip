@@ -182,6 +182,7 @@ static void lde_into(CMat& cm, const uint32_t* evals, size_t n, int w, uint32_t 
   if (tm && tm->on) {
     tm->end(b, st, &times->lde_ms);
     times->lde_bytes += 12.0 * (double)n * w;
+    times->lde_elem_stages += 3.0 * (double)n * cm.log_n * w;
     times->lde_calls++;
   }
 }
