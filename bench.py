@@ -164,6 +164,64 @@ def cpu_baseline():
                       f"OpenMP threads"}
 
 
+def end_to_end(client, pk, prog, stdin, jobs=8):
+    """Proofs from (program, stdin) with execution and upload included: the reference's
+    utils/prove.rs:23-66 loop (execute, then prove) as bfz_prove_batch pipelines it -- executor
+    threads into pinned memory, a copy stream for the events, the GPU proving job k while job
+    k+1 executes and uploads -- next to one unpipelined bfz_prove (execute + upload + prove)."""
+    import time as _t
+    client.prove_batch(pk, [stdin] * 2, public_values=False)  # warm the pinned buffers
+    stats = {}
+    t0 = _t.perf_counter()
+    proofs = client.prove_batch(pk, [stdin] * jobs, public_values=False, stats=stats)
+    wall = (_t.perf_counter() - t0) * 1e3
+    import ctypes
+    from bfz import _lib as _l
+    buf, n = _l.u8buf(stdin)
+    singles = []
+    for _ in range(3):
+        t1 = _t.perf_counter()
+        ptr = ctypes.POINTER(ctypes.c_uint8)()
+        plen = ctypes.c_size_t()
+        _l.check(_l.lib().bfz_prove(ctypes.c_void_p(pk.handle), buf, n, ctypes.byref(ptr),
+                                    ctypes.byref(plen)))
+        singles.append((_t.perf_counter() - t1) * 1e3)
+        one = _l.take_bytes(ptr, plen.value)
+    assert all(p.proof == one for p in proofs), "batch proofs differ from bfz_prove"
+    return {"jobs": jobs, "ms_per_proof": round(wall / jobs, 3),
+            "proofs_per_s": round(jobs * 1e3 / wall, 3),
+            "exec_threads": stats["exec_threads"],
+            "exec_ms_per_job": round(stats["exec_ms"] / jobs, 3),
+            "upload_ms_per_job": round(stats["upload_ms"] / jobs, 3),
+            "prove_ms_per_job": round(stats["prove_ms"] / jobs, 3),
+            "unpipelined_bfz_prove_ms": round(min(singles), 3),
+            "what": "bfz_prove_batch of FIBO_X4 stdin [255] from the program text: execution "
+                    "(host threads), event upload (copy stream) and proving overlapped; "
+                    "unpipelined = one bfz_prove (execute, upload, prove in sequence)"}
+
+
+def drop_in_path(pk, prog, stdin, ref_proof, steps=3):
+    """bfz_prove_traces -- the entry a Rust MachineProver::prove would call -- from host
+    row-major traces (the reference's generate_traces output, prover.rs:58-81): pinned
+    double-buffered upload, transpose to the device layout, proof.  Traces are generated on
+    the host before the timed region."""
+    import time as _t
+    from bfz import sdk as _s
+    traces = _s.generate_traces(prog, stdin)
+    prover = _s.CoreProver()
+    prover.prove(pk, traces)  # warm
+    times = []
+    for _ in range(steps):
+        t0 = _t.perf_counter()
+        pf = prover.prove(pk, traces)
+        times.append((_t.perf_counter() - t0) * 1e3)
+    assert pf == ref_proof, "host-trace proof differs from the record path"
+    nbytes = sum(int(t.nbytes) for _, _, t in traces)
+    return {"ms": round(min(times), 3), "trace_bytes": nbytes,
+            "what": "bfz_prove_traces from host row-major traces (all 8 chips, "
+                    f"{nbytes / 1e9:.2f} GB) incl. upload + transpose + proof"}
+
+
 def timed_steps(step, steps, dist=None, sync=lambda: None):
     """Runs `step` exactly `steps` times between barrier + device synchronize on both sides
     and returns ms per step, the max over ranks (every rank proves its own replica; the
@@ -240,6 +298,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the end-to-end batch and drop-in-path figures")
     ap.add_argument("--mode", choices=("replicas", "sharded", "pcs"), default="replicas",
                     help="replicas: one independent proof per rank (weak scaling, default); "
                          "sharded: one proof split across all ranks (strong scaling); "
@@ -349,6 +409,9 @@ def main():
             "poseidon2": poseidon2_roofline(tm),
             "proof_bytes": len(proof),
         }
+        if world == 1 and not args.no_extra:
+            line["end_to_end"] = end_to_end(client, pk, prog, stdin)
+            line["drop_in_path"] = drop_in_path(pk, prog, stdin, proof)
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is timed at N=1 only
             try:
                 line["cpu_baseline"] = cpu_baseline()

@@ -44,6 +44,21 @@ extern "C" {
 
 typedef struct bfz_pk bfz_pk;         /* device-resident proving key (DeviceProvingKey) */
 typedef struct bfz_record bfz_record; /* executed record with traces resident in HBM  */
+/* ShardMainData<SC, DeviceMatrix, DeviceProverData> (crates/stark/src/types.rs:13-18): the main
+ * traces' evaluations, their coset LDEs and Merkle tree, resident in HBM from bfz_main_commit
+ * until bfz_main_data_free. */
+typedef struct bfz_main_data bfz_main_data;
+/* p3 DuplexChallenger<KoalaBear, Poseidon2KoalaBear<16>, 16, 8> (kb31_poseidon2.rs:31) as plain
+ * data, words in Montgomery form (the in-memory MontyField31 value): sponge_state, then
+ * input_buffer[0..n_input) and output_buffer[0..n_output) exactly as the Rust Vecs hold them
+ * (samples pop from the end of output_buffer). */
+typedef struct {
+  uint32_t sponge_state[16];
+  uint32_t input_buffer[8];
+  uint32_t n_input;
+  uint32_t output_buffer[8];
+  uint32_t n_output;
+} bfz_challenger;
 
 typedef struct {
   double trace_ms, main_commit_ms, perm_ms, quotient_ms, open_ms, fri_ms, total_ms;
@@ -76,13 +91,43 @@ int bfz_execute(const char* elf, const uint8_t* stdin_data, size_t nin, uint8_t*
 int bfz_trace(const char* elf, const uint8_t* stdin_data, size_t nin, int chip, int prep,
               uint32_t** out, size_t* height, size_t* width);
 
+/* Diagnostic: the executor's event stream (Executor::run + emit_events, crates/core/executor/src/
+ * executor.rs:71-326) serialized field by field: executor 0 = the record executor (bfz_trace,
+ * oracle-checked traces), 1 = the prover pipeline's executor (bfz_record_new, bfz_prove,
+ * bfz_prove_batch).  Host only; *out is malloc'd (bfz_free). */
+int bfz_execute_events(const char* elf, const uint8_t* stdin_data, size_t nin, int executor,
+                       uint8_t** out, size_t* out_len);
+
 /* Same trace generated on the device from the uploaded events (the prover's own path),
  * returned row-major in natural row order for comparison. */
 int bfz_trace_device(const char* elf, const uint8_t* stdin_data, size_t nin, int chip,
                      uint32_t** out, size_t* height, size_t* width);
 
+/* The preprocessed commit is made once per program text and cached (16 most recent programs):
+ * a repeated setup of the same ELF returns a handle to the same device-resident key. */
 int bfz_setup(const char* elf, bfz_pk** pk, uint32_t vk_commit[8]);
 void bfz_pk_free(bfz_pk* pk);
+
+/* The split MachineProver surface, for a Rust HipProver:
+ *   bfz_main_commit         MachineProver::commit (crates/stark/src/prover.rs:209-236): host
+ *                           row-major main traces (as bfz_prove_traces) -> LDE + MerkleTreeMmcs
+ *                           commit in HBM; root = main_commit (8 Montgomery words, as vk_commit).
+ *   bfz_record_main_commit  the same from a device-resident record (traces generated on device).
+ *   bfz_challenger_observe_pk  MachineProvingKey::observe_into (prover.rs:595-601).
+ *   bfz_open                MachineProver::open (prover.rs:242-553) on the challenger state
+ *                           after observe_into; ch is not modified (the reference opens on a
+ *                           clone, prover.rs:578).  Output = the same BFZ1 proof bfz_prove*
+ *                           returns.  The main data stays valid (it may be opened again).
+ *   bfz_main_data_free      drops ShardMainData (frees its HBM). */
+int bfz_main_commit(const bfz_pk* pk, const int* chips, const uint32_t* const* traces,
+                    const size_t* heights, const size_t* widths, size_t nchips, bfz_main_data** out,
+                    uint32_t root[8]);
+int bfz_record_main_commit(const bfz_pk* pk, const bfz_record* rec, bfz_main_data** out,
+                           uint32_t root[8]);
+int bfz_challenger_observe_pk(const bfz_pk* pk, bfz_challenger* ch);
+int bfz_open(const bfz_pk* pk, bfz_main_data* data, const bfz_challenger* ch, uint8_t** proof,
+             size_t* proof_len);
+void bfz_main_data_free(bfz_main_data* data);
 
 int bfz_prove(const bfz_pk* pk, const uint8_t* stdin_data, size_t nin, uint8_t** proof,
               size_t* proof_len);
@@ -95,6 +140,20 @@ int bfz_prove_traces(const bfz_pk* pk, const int* chips, const uint32_t* const* 
                      size_t* proof_len);
 int bfz_verify(const char* elf, const uint32_t vk_commit[8], const uint8_t* proof,
                size_t proof_len);
+
+/* Pipelined proofs of one program over many inputs (the reference's execute-then-prove loop,
+ * crates/core/machine/src/utils/prove.rs:23-66, with execution off the critical path):
+ * exec_threads host threads run the executor into pinned memory, a copy stream uploads job
+ * k+1's events while the GPU proves job k.  proofs[i] (malloc'd, bfz_free) is byte-identical to
+ * bfz_prove(pk, stdins[i]).  exec_threads <= 0: environment BFZ_EXEC_THREADS or 3.
+ * stats (optional): wall time of the batch and per-stage sums over jobs. */
+typedef struct {
+  double wall_ms, exec_ms, upload_ms, prove_ms;
+  int exec_threads;
+} bfz_batch_stats;
+int bfz_prove_batch(const bfz_pk* pk, const uint8_t* const* stdins, const size_t* nins,
+                    size_t njobs, int exec_threads, uint8_t** proofs, size_t* proof_lens,
+                    bfz_batch_stats* stats);
 
 /* Split prove: bfz_record_new executes the program and copies its events to HBM (the
  * proof's inputs); bfz_record_prove generates every chip trace on the device

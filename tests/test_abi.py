@@ -179,3 +179,55 @@ def test_query_count_validation():
     with pytest.raises(_lib.BfzError, match="num_queries"):
         sdk.set_num_queries(-3)
     sdk.set_num_queries(0)
+
+
+def _events(elf, stdin, executor):
+    import ctypes
+    buf, n = _lib.u8buf(bytes(stdin))
+    p = ctypes.POINTER(ctypes.c_uint8)()
+    ln = ctypes.c_size_t()
+    _lib.check(_lib.lib().bfz_execute_events(elf.encode(), buf, n, executor, ctypes.byref(p),
+                                             ctypes.byref(ln)))
+    return _lib.take_bytes(p, ln.value)
+
+
+def _random_program(rng, size):
+    """A random balanced Brainfuck program that halts: loops always start with a '-' ... ']'
+    body that decrements the cell it tests, over a bounded tape excursion."""
+    out = []
+    for _ in range(size):
+        r = rng.random()
+        if r < 0.25:
+            out.append("+" * rng.integers(1, 6))
+        elif r < 0.35:
+            out.append("-")
+        elif r < 0.55:
+            out.append(">" if rng.random() < 0.6 else "<")
+        elif r < 0.65:
+            out.append(".")
+        elif r < 0.7:
+            out.append(",")
+        else:
+            k = int(rng.integers(1, 4))
+            out.append("[-" + ">" * k + "+" + "<" * k + "]")
+    return "".join(out)
+
+
+@pytest.mark.parametrize("prog,stdin", [(p, s) for _, p, s in guests.REFERENCE_PROGRAMS]
+                         + [(guests.FIBO, [17]), (guests.FIBO, [60])])
+def test_pipeline_executor_matches_record_executor(prog, stdin):
+    """The prover pipeline's executor (pinned arrays, dense cells, address-ordered memory events
+    without a sort) emits the record executor's event stream field for field."""
+    assert _events(prog, stdin, 1) == _events(prog, stdin, 0)
+
+
+def test_pipeline_executor_random_programs_and_tape_wrap():
+    import numpy as np
+    rng = np.random.default_rng(7)
+    progs = [_random_program(rng, int(rng.integers(5, 60))) for _ in range(60)]
+    progs += ["<<<+.>>>>>-.<<", "<" * 5000 + "+" + ">" * 9000 + "-.", ">>+<<<<<<-."]
+    for p in progs:
+        a, b = _events(p, [3], 0), _events(p, [3], 1)
+        assert a == b, p
+    with pytest.raises(_lib.BfzError, match="input"):
+        _events(",", [], 1)

@@ -145,6 +145,82 @@ def test_prove_from_host_traces_matches(client):
     client.verify(sdk.BfProofWithPublicValues(proof=pf, stdin=bytes([17])), vk)
 
 
+def test_split_commit_open_matches_prove(client):
+    """MachineProver::commit + observe_into + open (prover.rs:209-236, 595-601, 242-553) through
+    the split C ABI give the bytes of the one-call prove; open leaves the challenger unchanged
+    (the reference opens on a clone, prover.rs:578) and the main data can be opened again."""
+    pk, vk = client.setup(guests.FIBO)
+    traces = sdk.generate_traces(guests.FIBO, [17])
+    prover = sdk.CoreProver()
+    data = prover.commit(pk, traces)
+    ch = prover.new_challenger()
+    prover.observe_into(pk, ch)
+    before = bytes(ch)
+    pf = prover.open(pk, data, ch)
+    assert bytes(ch) == before
+    assert pf == client.prove(pk, [17]).run().proof
+    assert pf == O.prove(guests.FIBO, [17])
+    assert prover.open(pk, data, ch) == pf
+    # the record path (device-generated traces) commits to the same root
+    rec = ctypes.c_void_p()
+    buf, n = _lib.u8buf(bytes([17]))
+    _lib.check(_lib.lib().bfz_record_new(ctypes.c_void_p(pk.handle), buf, n, ctypes.byref(rec),
+                                         None))
+    data2 = prover.commit_record(pk, rec.value)
+    assert data2.main_commit == data.main_commit
+    assert prover.open(pk, data2, ch) == pf
+    _lib.lib().bfz_record_free(rec)
+    # a challenger that has not observed the key gives a proof the verifier rejects
+    bad = prover.open(pk, data, prover.new_challenger())
+    with pytest.raises(_lib.BfzError):
+        client.verify(sdk.BfProofWithPublicValues(proof=bad, stdin=bytes([17])), vk)
+    # main data committed for another key is refused
+    pk2, _ = client.setup(guests.HELLO)
+    with pytest.raises(_lib.BfzError, match="another key"):
+        prover.open(pk2, data, ch)
+
+
+def test_prove_batch_pipelined_matches_single(client):
+    """bfz_prove_batch (execute + upload of job k+1 under prove(k)) returns, job for job, the
+    bytes of single proofs and of the oracle, for every executor-thread count."""
+    pk, vk = client.setup(guests.FIBO)
+    stdins = [[5], [17], [30], [17], [1], [12], [9]]
+    want = [O.prove(guests.FIBO, s) for s in stdins]
+    for threads in (1, 2, 3):
+        stats = {}
+        got = client.prove_batch(pk, stdins, exec_threads=threads, stats=stats)
+        assert [p.proof for p in got] == want, threads
+        assert stats["exec_threads"] == threads and stats["wall_ms"] > 0
+    client.verify(got[1], vk)
+    assert got[1].public_values == client.execute(guests.FIBO, [17]).run()
+    assert client.prove_batch(pk, []) == []
+
+
+def test_prove_batch_error_does_not_hang(client):
+    """An executor failure (missing input) in the middle of a batch is reported, the other
+    threads stop, and the library stays usable."""
+    pk, _ = client.setup(guests.FIBO)
+    with pytest.raises(_lib.BfzError, match="input"):
+        client.prove_batch(pk, [[5], [6], [], [7], [8]], exec_threads=2)
+    assert client.prove_batch(pk, [[5]])[0].proof == O.prove(guests.FIBO, [5])
+
+
+def test_setup_is_cached_per_program(client):
+    """StarkMachine::setup (machine.rs:154-224) runs once per program: a second setup of the
+    same ELF returns the same device-resident key at once."""
+    import time
+    elf = guests.FIBO + "\n"  # a program text no other test has set up
+    t0 = time.perf_counter()
+    pk1, vk1 = client.setup(elf)
+    t1 = time.perf_counter()
+    pk2, vk2 = client.setup(elf)
+    t2 = time.perf_counter()
+    assert vk1.commit == vk2.commit
+    assert t2 - t1 < max(0.5 * (t1 - t0), 0.005)
+    pf = client.prove(pk2, [5]).run()
+    client.verify(pf, vk1)
+
+
 def test_prove_traces_rejects_bad_shapes(client):
     pk, _ = client.setup(guests.HELLO)
     traces = sdk.generate_traces(guests.HELLO, [])

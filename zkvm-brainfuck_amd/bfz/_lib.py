@@ -32,6 +32,17 @@ class Timings(ctypes.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class BatchStats(ctypes.Structure):
+    _fields_ = [("wall_ms", c_double), ("exec_ms", c_double), ("upload_ms", c_double),
+                ("prove_ms", c_double), ("exec_threads", c_int)]
+
+
+class Challenger(ctypes.Structure):
+    """bfz_challenger: p3 DuplexChallenger state, Montgomery words."""
+    _fields_ = [("sponge_state", c_uint32 * 16), ("input_buffer", c_uint32 * 8),
+                ("n_input", c_uint32), ("output_buffer", c_uint32 * 8), ("n_output", c_uint32)]
+
+
 # collective callbacks of bfz_record_prove_sharded (bfz_allgather_fn / bfz_allreduce_u32_fn)
 ALLGATHER_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_void_p, c_size_t, c_void_p)
 ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, c_void_p, POINTER(c_uint32), c_size_t)
@@ -50,15 +61,28 @@ SIGNATURES = [
                             POINTER(c_size_t), POINTER(c_uint64)]),
     ("bfz_trace", c_int, [c_char_p, POINTER(c_uint8), c_size_t, c_int, c_int,
                           POINTER(POINTER(c_uint32)), POINTER(c_size_t), POINTER(c_size_t)]),
+    ("bfz_execute_events", c_int, [c_char_p, POINTER(c_uint8), c_size_t, c_int,
+                                   POINTER(POINTER(c_uint8)), POINTER(c_size_t)]),
     ("bfz_trace_device", c_int, [c_char_p, POINTER(c_uint8), c_size_t, c_int,
                                  POINTER(POINTER(c_uint32)), POINTER(c_size_t), POINTER(c_size_t)]),
     ("bfz_setup", c_int, [c_char_p, POINTER(c_void_p), POINTER(c_uint32)]),
     ("bfz_pk_free", None, [c_void_p]),
+    ("bfz_main_commit", c_int, [c_void_p, POINTER(c_int), POINTER(POINTER(c_uint32)),
+                                POINTER(c_size_t), POINTER(c_size_t), c_size_t,
+                                POINTER(c_void_p), POINTER(c_uint32)]),
+    ("bfz_record_main_commit", c_int, [c_void_p, c_void_p, POINTER(c_void_p), POINTER(c_uint32)]),
+    ("bfz_challenger_observe_pk", c_int, [c_void_p, POINTER(Challenger)]),
+    ("bfz_open", c_int, [c_void_p, c_void_p, POINTER(Challenger), POINTER(POINTER(c_uint8)),
+                         POINTER(c_size_t)]),
+    ("bfz_main_data_free", None, [c_void_p]),
     ("bfz_prove", c_int, [c_void_p, POINTER(c_uint8), c_size_t, POINTER(POINTER(c_uint8)),
                           POINTER(c_size_t)]),
     ("bfz_prove_traces", c_int, [c_void_p, POINTER(c_int), POINTER(POINTER(c_uint32)),
                                  POINTER(c_size_t), POINTER(c_size_t), c_size_t,
                                  POINTER(POINTER(c_uint8)), POINTER(c_size_t)]),
+    ("bfz_prove_batch", c_int, [c_void_p, POINTER(POINTER(c_uint8)), POINTER(c_size_t), c_size_t,
+                                c_int, POINTER(POINTER(c_uint8)), POINTER(c_size_t),
+                                POINTER(BatchStats)]),
     ("bfz_verify", c_int, [c_char_p, POINTER(c_uint32), POINTER(c_uint8), c_size_t]),
     ("bfz_record_new", c_int, [c_void_p, POINTER(c_uint8), c_size_t, POINTER(c_void_p),
                                POINTER(c_uint64)]),

@@ -10,7 +10,12 @@ bfz C ABI.  Same names, argument meaning and error behaviour:
 and of the core MachineProver boundary (crates/stark/src/prover.rs:27-150):
 
     traces = generate_traces(elf, stdin)         # generate_traces          prover.rs:58-81
-    proof = CoreProver().prove(pk, traces)       # MachineProver::prove     prover.rs:560-582
+    prover = CoreProver()
+    data = prover.commit(pk, traces)             # MachineProver::commit    prover.rs:209-236
+    ch = prover.new_challenger()
+    prover.observe_into(pk, ch)                  # pk.observe_into          prover.rs:595-601
+    proof = prover.open(pk, data, ch)            # MachineProver::open      prover.rs:242-553
+    proof = prover.prove(pk, traces)             # MachineProver::prove     prover.rs:560-582
 
 Errors raise (the reference returns Err / panics in the same places).  Proving runs on the GPU
 through libbfz; verification runs the host verifier compiled into the same library.
@@ -22,7 +27,7 @@ from dataclasses import dataclass, field
 from typing import List, Optional
 
 from . import _lib
-from ._lib import BfzError, check, init, lib, take_bytes, u8buf
+from ._lib import BfzError, Challenger, check, init, lib, take_bytes, u8buf
 
 
 @dataclass
@@ -166,6 +171,31 @@ class ProverClient:
     def prove(self, pk: BfProvingKey, stdin) -> Prove:
         return Prove(pk, bytes(stdin))
 
+    def prove_batch(self, pk: BfProvingKey, stdins, exec_threads: int = 0,
+                    public_values: bool = True, stats: Optional[dict] = None):
+        """Proofs of pk's program over many inputs, pipelined (bfz_prove_batch): executions run
+        on host threads and uploads on a copy stream while the GPU proves the previous job.
+        Each proof equals prove(pk, stdin).run()'s; stats (a dict) receives the batch timings."""
+        init(self.device)
+        ins = [bytes(x) for x in stdins]
+        k = len(ins)
+        bufs = [u8buf(x) for x in ins]
+        arr = (ctypes.POINTER(ctypes.c_uint8) * max(k, 1))(
+            *[ctypes.cast(b, ctypes.POINTER(ctypes.c_uint8)) for b, _ in bufs])
+        lens = (ctypes.c_size_t * max(k, 1))(*[n for _, n in bufs])
+        outs = (ctypes.POINTER(ctypes.c_uint8) * max(k, 1))()
+        olens = (ctypes.c_size_t * max(k, 1))()
+        st = _lib.BatchStats()
+        check(lib().bfz_prove_batch(ctypes.c_void_p(pk.handle), arr, lens, k, int(exec_threads),
+                                    outs, olens, ctypes.byref(st)))
+        proofs = [take_bytes(outs[i], olens[i]) for i in range(k)]
+        if stats is not None:
+            stats.update({name: getattr(st, name) for name, _ in st._fields_})
+        return [BfProofWithPublicValues(
+            proof=pf, stdin=x,
+            public_values=Execute(pk.elf, x).run() if public_values else b"")
+            for pf, x in zip(proofs, ins)]
+
     def verify(self, proof: BfProofWithPublicValues, vk: BfVerifyingKey) -> None:
         buf, n = u8buf(proof.proof)
         commit = (ctypes.c_uint32 * 8)(*vk.commit)
@@ -204,20 +234,74 @@ def generate_traces(elf: str, stdin) -> list:
     return out
 
 
+def _trace_args(traces):
+    import numpy as np
+    mats = [np.ascontiguousarray(t, dtype=np.uint32) for _, _, t in traces]
+    k = len(mats)
+    chips = (ctypes.c_int * k)(*[c for c, _, _ in traces])
+    ptrs = (ctypes.POINTER(ctypes.c_uint32) * k)(
+        *[m.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)) for m in mats])
+    hs = (ctypes.c_size_t * k)(*[m.shape[0] for m in mats])
+    ws = (ctypes.c_size_t * k)(*[m.shape[1] for m in mats])
+    return mats, chips, ptrs, hs, ws, k
+
+
+class ShardMainData:
+    """ShardMainData (crates/stark/src/types.rs:13-18) held in HBM by libbfz: the main traces'
+    evaluations, LDEs and Merkle tree; main_commit is its root (8 Montgomery words)."""
+
+    def __init__(self, handle: int, main_commit):
+        self.handle = handle
+        self.main_commit = list(main_commit)
+
+    def __del__(self):
+        if getattr(self, "handle", None):
+            lib().bfz_main_data_free(ctypes.c_void_p(self.handle))
+            self.handle = None
+
+
 class CoreProver:
-    """HIP implementation of MachineProver::prove (crates/stark/src/prover.rs:560-582) from
-    host traces: commit, LogUp, quotient and open run on the device."""
+    """HIP implementation of the MachineProver trait (crates/stark/src/prover.rs:27-150) from
+    host traces: `commit` (:209-236), `observe_into` (MachineProvingKey, :595-601), `open`
+    (:242-553) and the default `prove` (:560-582) = commit + open on a clone of the
+    challenger.  Every step runs on the device; the challenger is plain data (Challenger)."""
+
+    def commit(self, pk: BfProvingKey, traces) -> ShardMainData:
+        init()
+        mats, chips, ptrs, hs, ws, k = _trace_args(traces)
+        out = ctypes.c_void_p()
+        root = (ctypes.c_uint32 * 8)()
+        check(lib().bfz_main_commit(ctypes.c_void_p(pk.handle), chips, ptrs, hs, ws, k,
+                                    ctypes.byref(out), root))
+        return ShardMainData(out.value, root)
+
+    def commit_record(self, pk: BfProvingKey, record_handle: int) -> ShardMainData:
+        """commit from a device-resident record (bfz_record_new): traces generated on device."""
+        init()
+        out = ctypes.c_void_p()
+        root = (ctypes.c_uint32 * 8)()
+        check(lib().bfz_record_main_commit(ctypes.c_void_p(pk.handle),
+                                           ctypes.c_void_p(record_handle), ctypes.byref(out), root))
+        return ShardMainData(out.value, root)
+
+    @staticmethod
+    def new_challenger() -> Challenger:
+        return Challenger()  # DuplexChallenger::new: all zero, empty buffers
+
+    def observe_into(self, pk: BfProvingKey, ch: Challenger) -> None:
+        check(lib().bfz_challenger_observe_pk(ctypes.c_void_p(pk.handle), ctypes.byref(ch)))
+
+    def open(self, pk: BfProvingKey, data: ShardMainData, ch: Challenger) -> bytes:
+        ptr = ctypes.POINTER(ctypes.c_uint8)()
+        plen = ctypes.c_size_t()
+        check(lib().bfz_open(ctypes.c_void_p(pk.handle), ctypes.c_void_p(data.handle),
+                             ctypes.byref(ch), ctypes.byref(ptr), ctypes.byref(plen)))
+        return take_bytes(ptr, plen.value)
 
     def prove(self, pk: BfProvingKey, traces) -> bytes:
-        import numpy as np
+        """One call (bfz_prove_traces): same bytes as commit + observe_into + open."""
         init()
-        mats = [np.ascontiguousarray(t, dtype=np.uint32) for _, _, t in traces]
-        k = len(mats)
-        chips = (ctypes.c_int * k)(*[c for c, _, _ in traces])
-        ptrs = (ctypes.POINTER(ctypes.c_uint32) * k)(
-            *[m.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)) for m in mats])
-        hs = (ctypes.c_size_t * k)(*[m.shape[0] for m in mats])
-        ws = (ctypes.c_size_t * k)(*[m.shape[1] for m in mats])
+        mats, chips, ptrs, hs, ws, k = _trace_args(traces)
         ptr = ctypes.POINTER(ctypes.c_uint8)()
         plen = ctypes.c_size_t()
         check(lib().bfz_prove_traces(ctypes.c_void_p(pk.handle), chips, ptrs, hs, ws, k,

@@ -13,13 +13,18 @@
 #include "merkle.h"
 #include "ntt.h"
 #include "pcs_sharded.h"
+#include "pipeline.h"
 #include "proof.h"
 #include "prover.h"
 #include "tracegen.h"
 #include "verifier.h"
 
 struct bfz_pk {
-  std::unique_ptr<bfz::ProvingKey> pk;
+  std::shared_ptr<const bfz::ProvingKey> pk;  // shared with the per-program setup cache
+};
+struct bfz_main_data {
+  std::shared_ptr<const bfz::ProvingKey> pk;  // the key the commit was made for
+  bfz::MainData md;
 };
 struct bfz_record {
   bfz::DeviceEvents ev;  // executor events resident in HBM
@@ -138,6 +143,84 @@ int bfz_trace(const char* elf, const uint8_t* in, size_t nin, int chip, int prep
   });
 }
 
+static int emit(std::vector<uint8_t>&& v, uint8_t** proof, size_t* len) {
+  uint8_t* p = (uint8_t*)std::malloc(v.size() ? v.size() : 1);
+  if (!p) throw std::runtime_error("out of host memory");
+  std::memcpy(p, v.data(), v.size());
+  *proof = p;
+  *len = v.size();
+  return 0;
+}
+
+// Field-wise serialization of an event stream (no struct padding), for comparing executors.
+}  // extern "C"
+namespace {
+struct EvBlob {
+  std::vector<uint8_t> b;
+  void u8(uint8_t v) { b.push_back(v); }
+  void u32(uint32_t v) { for (int i = 0; i < 4; i++) b.push_back((uint8_t)(v >> (8 * i))); }
+  void u64(uint64_t v) { u32((uint32_t)v); u32((uint32_t)(v >> 32)); }
+  void acc(const bfz::MemAccess& a) {
+    u8(a.kind); u8(a.value); u8(a.prev_value); u32(a.ts); u32(a.prev_ts);
+  }
+  void ev(const bfz::CpuEvent& e) {
+    u32(e.clk); u32(e.pc); u32(e.next_pc); u32(e.mp); u32(e.next_mp); u8(e.mv); u8(e.next_mv);
+    acc(e.mv_access); acc(e.next_mv_access);
+  }
+  void ev(const bfz::AluEvent& e) { u32(e.pc); u8(e.opcode); u8(e.next_mv); u8(e.mv); }
+  void ev(const bfz::JumpEvent& e) { u32(e.pc); u32(e.next_pc); u8(e.opcode); u32(e.dst); u8(e.mv); }
+  void ev(const bfz::MemInstrEvent& e) { u32(e.clk); u32(e.pc); u8(e.opcode); u32(e.mp); u32(e.next_mp); }
+  void ev(const bfz::IoEvent& e) { u32(e.pc); u8(e.opcode); u32(e.mp); u8(e.mv); }
+  void ev(const bfz::MemoryEvent& e) { u32(e.addr); u32(e.init_ts); u32(e.final_ts); u8(e.init_v); u8(e.final_v); }
+  template <class T>
+  void arr(const T* p, size_t n) {
+    u64(n);
+    for (size_t i = 0; i < n; i++) ev(p[i]);
+  }
+};
+}  // namespace
+extern "C" {
+
+int bfz_execute_events(const char* elf, const uint8_t* in, size_t nin, int executor, uint8_t** out,
+                       size_t* len) {
+  return guarded([&] {
+    bfz::Program p = bfz::Program::parse(elf);
+    EvBlob b;
+    if (executor == 0) {
+      bfz::ExecutionRecord r;
+      bfz::execute(p, in, nin, r);
+      b.arr(r.cpu.data(), r.cpu.size());
+      b.arr(r.alu.data(), r.alu.size());
+      b.arr(r.jump.data(), r.jump.size());
+      b.arr(r.meminstr.data(), r.meminstr.size());
+      b.arr(r.io.data(), r.io.size());
+      b.arr(r.memory.data(), r.memory.size());
+      b.u64(r.global_clk);
+      b.u32(r.pc);
+      b.u32(r.mp);
+      b.u64(r.output.size());
+      b.b.insert(b.b.end(), r.output.begin(), r.output.end());
+    } else if (executor == 1) {
+      static bfz::HostEvents* h = new bfz::HostEvents();  // reused: exercises the reset path
+      bfz::execute_into(p, in, nin, *h);
+      b.arr(h->cpu.p, h->cpu.n);
+      b.arr(h->alu.p, h->alu.n);
+      b.arr(h->jump.p, h->jump.n);
+      b.arr(h->meminstr.p, h->meminstr.n);
+      b.arr(h->io.p, h->io.n);
+      b.arr(h->memory.p, h->memory.n);
+      b.u64(h->global_clk);
+      b.u32(h->pc);
+      b.u32(h->mp);
+      b.u64(h->output.size());
+      b.b.insert(b.b.end(), h->output.begin(), h->output.end());
+    } else {
+      throw std::runtime_error("executor must be 0 (record) or 1 (pipeline)");
+    }
+    return emit(std::move(b.b), out, len);
+  });
+}
+
 int bfz_trace_device(const char* elf, const uint8_t* in, size_t nin, int chip, uint32_t** out,
                      size_t* height, size_t* width) {
   return guarded([&] {
@@ -170,25 +253,47 @@ int bfz_trace_device(const char* elf, const uint8_t* in, size_t nin, int chip, u
   });
 }
 
+// StarkMachine::setup (machine.rs:154-224) runs once per program: the preprocessed commit
+// (Program + Byte LDEs and tree, resident in HBM) is cached by program text, so a repeated
+// ProverClient::setup of the same ELF costs a map lookup.  The cache keeps the 16 most recently
+// used keys; a key stays alive while any bfz_pk handle refers to it.
+}  // extern "C"
+namespace {
+std::shared_ptr<const bfz::ProvingKey> cached_setup(const std::string& elf) {
+  struct Entry {
+    std::string elf;
+    std::shared_ptr<const bfz::ProvingKey> pk;
+  };
+  static std::vector<Entry>* cache = new std::vector<Entry>();  // most recent last
+  constexpr size_t CAP = 16;
+  for (size_t i = 0; i < cache->size(); i++)
+    if ((*cache)[i].elf == elf) {
+      Entry e = std::move((*cache)[i]);
+      cache->erase(cache->begin() + i);
+      cache->push_back(std::move(e));
+      return cache->back().pk;
+    }
+  std::shared_ptr<const bfz::ProvingKey> pk(bfz::setup(elf).release());
+  if (cache->size() == CAP) cache->erase(cache->begin());
+  cache->push_back({elf, pk});
+  return pk;
+}
+}  // namespace
+extern "C" {
+
 int bfz_setup(const char* elf, bfz_pk** pk, uint32_t vk_commit[8]) {
   return guarded([&] {
     auto k = std::make_unique<bfz_pk>();
-    k->pk = bfz::setup(elf);
+    k->pk = cached_setup(elf);
     if (vk_commit) std::memcpy(vk_commit, k->pk->prep.tree.root, 32);
     *pk = k.release();
     return 0;
   });
 }
 
-void bfz_pk_free(bfz_pk* pk) { delete pk; }
-
-static int emit(std::vector<uint8_t>&& v, uint8_t** proof, size_t* len) {
-  uint8_t* p = (uint8_t*)std::malloc(v.size() ? v.size() : 1);
-  if (!p) throw std::runtime_error("out of host memory");
-  std::memcpy(p, v.data(), v.size());
-  *proof = p;
-  *len = v.size();
-  return 0;
+void bfz_pk_free(bfz_pk* pk) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  delete pk;
 }
 
 int bfz_prove(const bfz_pk* pk, const uint8_t* in, size_t nin, uint8_t** proof, size_t* len) {
@@ -212,6 +317,122 @@ int bfz_prove_traces(const bfz_pk* pk, const int* chips, const uint32_t* const* 
   });
 }
 
+// ------------------------------------------------ split MachineProver surface (commit / open)
+}  // extern "C"
+namespace {
+bfz::Challenger from_c(const bfz_challenger* c) {
+  bfz::Challenger ch;
+  if (c->n_input > 8 || c->n_output > 8) throw std::runtime_error("challenger: buffer length > 8");
+  for (int i = 0; i < 16; i++) ch.st[i] = c->sponge_state[i];
+  for (uint32_t i = 0; i < c->n_input; i++) ch.in[i] = c->input_buffer[i];
+  for (uint32_t i = 0; i < c->n_output; i++) ch.out[i] = c->output_buffer[i];
+  ch.nin = (int)c->n_input;
+  ch.nout = (int)c->n_output;
+  for (int i = 0; i < 16; i++)
+    if (ch.st[i] >= kb::P) throw std::runtime_error("challenger: non-canonical word");
+  return ch;
+}
+void to_c(const bfz::Challenger& ch, bfz_challenger* c) {
+  std::memset(c, 0, sizeof *c);
+  for (int i = 0; i < 16; i++) c->sponge_state[i] = ch.st[i];
+  for (int i = 0; i < ch.nin; i++) c->input_buffer[i] = ch.in[i];
+  for (int i = 0; i < ch.nout; i++) c->output_buffer[i] = ch.out[i];
+  c->n_input = (uint32_t)ch.nin;
+  c->n_output = (uint32_t)ch.nout;
+}
+}  // namespace
+extern "C" {
+
+int bfz_challenger_observe_pk(const bfz_pk* pk, bfz_challenger* ch) {
+  return guarded([&] {
+    if (!pk || !ch) throw std::runtime_error("null argument");
+    bfz::Challenger c = from_c(ch);
+    c.observe_digest(pk->pk->prep.tree.root);  // observe_into (prover.rs:595-601)
+    for (int i = 0; i < 7; i++) c.observe(0);
+    to_c(c, ch);
+    return 0;
+  });
+}
+
+int bfz_main_commit(const bfz_pk* pk, const int* chips, const uint32_t* const* traces,
+                    const size_t* heights, const size_t* widths, size_t nchips, bfz_main_data** out,
+                    uint32_t root[8]) {
+  return guarded([&] {
+    if (!pk || !out) throw std::runtime_error("null argument");
+    auto d = std::make_unique<bfz_main_data>();
+    d->pk = pk->pk;
+    bfz::upload_host_traces(chips, traces, heights, widths, nchips, d->md.dt, bfz::stream());
+    bfz::commit_main(d->md);
+    if (root) std::memcpy(root, d->md.mainr.tree.root, 32);
+    *out = d.release();
+    return 0;
+  });
+}
+
+int bfz_record_main_commit(const bfz_pk* pk, const bfz_record* rec, bfz_main_data** out,
+                           uint32_t root[8]) {
+  return guarded([&] {
+    if (!pk || !rec || !out) throw std::runtime_error("null argument");
+    auto d = std::make_unique<bfz_main_data>();
+    d->pk = pk->pk;
+    bfz::generate_traces_device(rec->ev, d->md.dt, bfz::stream());
+    bfz::commit_main(d->md);
+    if (root) std::memcpy(root, d->md.mainr.tree.root, 32);
+    *out = d.release();
+    return 0;
+  });
+}
+
+int bfz_open(const bfz_pk* pk, bfz_main_data* data, const bfz_challenger* ch, uint8_t** proof,
+             size_t* len) {
+  return guarded([&] {
+    if (!pk || !data || !ch) throw std::runtime_error("null argument");
+    if (data->pk != pk->pk) throw std::runtime_error("open: main data was committed for another key");
+    return emit(bfz::open_main(*pk->pk, data->md, from_c(ch), opts()), proof, len);
+  });
+}
+
+void bfz_main_data_free(bfz_main_data* data) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  delete data;
+}
+
+int bfz_prove_batch(const bfz_pk* pk, const uint8_t* const* stdins, const size_t* nins,
+                    size_t njobs, int exec_threads, uint8_t** proofs, size_t* proof_lens,
+                    bfz_batch_stats* stats) {
+  return guarded([&] {
+    if (!pk || (njobs && (!stdins || !nins || !proofs || !proof_lens)))
+      throw std::runtime_error("null argument");
+    for (size_t i = 0; i < njobs; i++) proofs[i] = nullptr;
+    std::vector<bfz::Job> jobs(njobs);
+    for (size_t i = 0; i < njobs; i++) jobs[i] = {stdins[i], nins[i]};
+    int E = exec_threads;
+    if (E <= 0) {
+      const char* e = std::getenv("BFZ_EXEC_THREADS");
+      E = e ? std::atoi(e) : 3;
+    }
+    if (E < 1 || E > 64) throw std::runtime_error("exec_threads must be in 1..64");
+    bfz::BatchStats bs;
+    auto v = bfz::prove_batch(*pk->pk, jobs, opts(), E, &bs);
+    for (size_t i = 0; i < njobs; i++) {
+      try {
+        emit(std::move(v[i]), &proofs[i], &proof_lens[i]);
+      } catch (...) {
+        for (size_t k = 0; k < i; k++) std::free(proofs[k]);
+        throw;
+      }
+    }
+    if (stats) {
+      stats->wall_ms = bs.wall_ms;
+      stats->exec_ms = bs.exec_ms;
+      stats->upload_ms = bs.upload_ms;
+      stats->prove_ms = bs.prove_ms;
+      stats->exec_threads = bs.exec_threads;
+    }
+    return 0;
+  });
+}
+
 int bfz_verify(const char* elf, const uint32_t vk_commit[8], const uint8_t* proof, size_t len) {
   return guarded([&] {
     std::string why;
@@ -231,11 +452,11 @@ int bfz_record_new(const bfz_pk* pk, const uint8_t* in, size_t nin, bfz_record**
                    uint64_t* cycles) {
   return guarded([&] {
     auto r = std::make_unique<bfz_record>();
-    bfz::ExecutionRecord er;
-    bfz::execute(pk->pk->program, in, nin, er);
-    bfz::upload_events(er, r->ev, bfz::stream());
-    r->cycles = er.global_clk;
-    if (cycles) *cycles = er.global_clk;
+    bfz::HostEvents& h = bfz::scratch_events();
+    bfz::execute_into(pk->pk->program, in, nin, h);
+    bfz::upload_events(h, pk->pk->program, r->ev, bfz::stream());
+    r->cycles = h.global_clk;
+    if (cycles) *cycles = h.global_clk;
     *rec = r.release();
     return 0;
   });

@@ -88,27 +88,37 @@ class DevicePool {
 DevicePool& pool();
 
 template <class T>
-struct DBuf {  // RAII device buffer from the pool
+struct DBuf {  // RAII device buffer from the pool (or a borrowed view of memory owned elsewhere)
   T* p = nullptr;
   size_t n = 0;
+  bool owned = true;
   DBuf() = default;
   explicit DBuf(size_t count) { reset(count); }
   DBuf(const DBuf&) = delete;
   DBuf& operator=(const DBuf&) = delete;
-  DBuf(DBuf&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+  DBuf(DBuf&& o) noexcept : p(o.p), n(o.n), owned(o.owned) { o.p = nullptr; o.n = 0; }
   DBuf& operator=(DBuf&& o) noexcept {
-    if (this != &o) { free(); p = o.p; n = o.n; o.p = nullptr; o.n = 0; }
+    if (this != &o) { free(); p = o.p; n = o.n; owned = o.owned; o.p = nullptr; o.n = 0; }
     return *this;
+  }
+  static DBuf borrow(T* ptr, size_t count) {  // not released on destruction
+    DBuf b;
+    b.p = ptr;
+    b.n = count;
+    b.owned = false;
+    return b;
   }
   void reset(size_t count) {
     free();
     n = count;
+    owned = true;
     p = (T*)pool().alloc(count * sizeof(T));
   }
   void free() {
-    if (p) pool().release(p);
+    if (p && owned) pool().release(p);
     p = nullptr;
     n = 0;
+    owned = true;
   }
   ~DBuf() { free(); }
 };

@@ -2,6 +2,8 @@
 #include "machine.h"
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <stdexcept>
 #include <unordered_map>
 
@@ -142,6 +144,163 @@ void execute(const Program& prog, const uint8_t* in, size_t nin, ExecutionRecord
   rec.mp = mp;
 }
 
+// ---------------------------------------------------------------- pipeline executor
+HostEvents::~HostEvents() {
+  FreeFn f = dealloc ? dealloc : std::free;
+  f(cpu.p);
+  f(alu.p);
+  f(jump.p);
+  f(meminstr.p);
+  f(io.p);
+  f(memory.p);
+}
+
+template <class T>
+void HostEvents::grow(Arr<T>& a, size_t need) {
+  if (need <= a.cap) return;
+  size_t cap = std::max<size_t>(a.cap ? a.cap : 1024, 1024);
+  while (cap < need) cap *= 2;
+  T* p = static_cast<T*>((alloc ? alloc : std::malloc)(cap * sizeof(T)));
+  if (!p) throw std::runtime_error("executor: out of host memory");
+  if (a.n) std::memcpy(p, a.p, a.n * sizeof(T));
+  (dealloc ? dealloc : std::free)(a.p);
+  a.p = p;
+  a.cap = cap;
+}
+
+// Executor::run (crates/core/executor/src/executor.rs:71-326) with emit_events (:178-239) and
+// rr_traced / rw_traced (:262-326) -- the same event stream as execute() above.
+void execute_into(const Program& prog, const uint8_t* in, size_t nin, HostEvents& ev) {
+  if (prog.instructions.empty()) throw std::runtime_error("empty program");
+  ev.cpu.n = ev.alu.n = ev.jump.n = ev.meminstr.n = ev.io.n = ev.memory.n = 0;
+  ev.output.clear();
+  // memory cells: offsets [lo, hi) relative to address 0 (mp moves by one, so the cells a run
+  // touches form one interval); the array is cleared here, sized by the previous run
+  std::fill(ev.cells.begin(), ev.cells.end(), HostEvents::Cell{0, 0, 0});
+  if (ev.cells.empty()) {
+    ev.cells.assign(1 << 16, HostEvents::Cell{0, 0, 0});
+    ev.cell_lo = -(1 << 12);
+  }
+  int64_t lo = ev.cell_lo, hi = lo + (int64_t)ev.cells.size();
+  HostEvents::Cell* cells = ev.cells.data();
+  const Instruction* code = prog.instructions.data();
+  const uint32_t n = (uint32_t)prog.instructions.size();
+  uint32_t pc = 0, clk = 0;
+  int64_t off = 0;  // memory pointer as an unwrapped offset; mp = (u32)off
+  uint64_t gclk = 0;
+  auto ensure_cell = [&](int64_t o) {
+    if (o >= lo && o < hi) return;
+    const int64_t span = hi - lo;
+    const int64_t nlo = o < lo ? std::min(o, lo - span) : lo;
+    const int64_t nhi = o >= hi ? std::max(o + 1, hi + span) : hi;
+    std::vector<HostEvents::Cell> nc((size_t)(nhi - nlo), HostEvents::Cell{0, 0, 0});
+    std::memcpy(&nc[(size_t)(lo - nlo)], cells, (size_t)span * sizeof(HostEvents::Cell));
+    ev.cells.swap(nc);
+    lo = nlo;
+    hi = nhi;
+    cells = ev.cells.data();
+  };
+  ensure_cell(0);
+  for (;;) {
+    if (ev.cpu.n == ev.cpu.cap) {  // every cycle emits one Cpu event and at most one other
+      const size_t want = ev.cpu.cap ? 2 * ev.cpu.cap : (size_t)1 << 16;
+      ev.grow(ev.cpu, want);
+      ev.grow(ev.alu, std::min(want, std::max(ev.alu.cap, ev.alu.n + want / 2)));
+      ev.grow(ev.jump, std::min(want, std::max(ev.jump.cap, ev.jump.n + want / 2)));
+      ev.grow(ev.meminstr, std::min(want, std::max(ev.meminstr.cap, ev.meminstr.n + want / 2)));
+      ev.grow(ev.io, std::min(want, std::max(ev.io.cap, ev.io.n + 1024)));
+    }
+    const Instruction ins = code[pc];
+    CpuEvent& ce = ev.cpu.p[ev.cpu.n++];
+    const uint32_t mp0 = (uint32_t)off;
+    uint32_t next_pc = pc + 1;
+    ce.clk = clk;
+    ce.pc = pc;
+    ce.mp = mp0;
+    ce.mv = ce.next_mv = 0;
+    ce.mv_access = MemAccess();
+    ce.next_mv_access = MemAccess();
+    const uint8_t op = ins.opcode;
+    if (op == OP_MEM_FWD || op == OP_MEM_BWD) {
+      off += op == OP_MEM_FWD ? 1 : -1;
+      if (ev.meminstr.n == ev.meminstr.cap) ev.grow(ev.meminstr, ev.meminstr.n + 1);
+      ev.meminstr.p[ev.meminstr.n++] = {clk, pc, op, mp0, (uint32_t)off};
+    } else {
+      ensure_cell(off);
+      HostEvents::Cell& c = cells[off - lo];
+      c.touched = 1;
+      MemAccess& a = ce.mv_access;  // the first access of the cycle: read, or the input write
+      a.prev_value = c.value;
+      a.prev_ts = c.ts;
+      const bool input = op == OP_INPUT;
+      if (input) {
+        if (nin == 0) throw std::runtime_error("input stream exhausted");
+        c.value = in[0];  // the reference never advances input_stream_ptr
+      }
+      c.ts = clk + 1;
+      a.kind = input ? 2 : 1;
+      a.value = c.value;
+      a.ts = c.ts;
+      const uint8_t mv = c.value;
+      ce.mv = mv;
+      switch (op) {
+        case OP_ADD:
+        case OP_SUB: {
+          const uint8_t nv = op == OP_ADD ? (uint8_t)(mv + 1) : (uint8_t)(mv - 1);
+          MemAccess& b = ce.next_mv_access;
+          b.prev_value = c.value;
+          b.prev_ts = c.ts;
+          c.value = nv;
+          c.ts = clk + 2;
+          b.kind = 2;
+          b.value = nv;
+          b.ts = c.ts;
+          ce.next_mv = nv;
+          if (ev.alu.n == ev.alu.cap) ev.grow(ev.alu, ev.alu.n + 1);
+          ev.alu.p[ev.alu.n++] = {pc, op, nv, mv};
+          break;
+        }
+        case OP_LOOP_START:
+        case OP_LOOP_END:
+          if (op == OP_LOOP_START) next_pc = mv == 0 ? ins.op_a : pc + 1;
+          else next_pc = mv != 0 ? ins.op_a : pc + 1;
+          if (ev.jump.n == ev.jump.cap) ev.grow(ev.jump, ev.jump.n + 1);
+          ev.jump.p[ev.jump.n++] = {pc, next_pc, op, next_pc, mv};
+          break;
+        default:  // OP_INPUT / OP_OUTPUT
+          if (op == OP_OUTPUT) ev.output.push_back(mv);
+          if (ev.io.n == ev.io.cap) ev.grow(ev.io, ev.io.n + 1);
+          ev.io.p[ev.io.n++] = {pc, op, mp0, mv};
+          break;
+      }
+    }
+    ce.next_pc = next_pc;
+    ce.next_mp = (uint32_t)off;
+    pc = next_pc;
+    clk += 2;
+    gclk++;
+    if (pc == n) break;
+  }
+  // memory events in address order: offsets [0, hi) are addresses 0.., offsets [lo, 0) wrap to
+  // 2^32 + off, above every non-negative one; first access saw (value 0, ts 0)
+  size_t touched = 0;
+  for (int64_t o = lo; o < hi; o++) touched += cells[o - lo].touched;
+  ev.grow(ev.memory, touched);
+  ev.memory.n = 0;
+  auto emit = [&](int64_t a, int64_t b) {
+    for (int64_t o = a; o < b; o++) {
+      const HostEvents::Cell& c = cells[o - lo];
+      if (c.touched) ev.memory.p[ev.memory.n++] = {(uint32_t)o, 0, c.ts, 0, c.value};
+    }
+  };
+  emit(std::max<int64_t>(0, lo), hi);
+  emit(lo, std::min<int64_t>(0, hi));
+  ev.cell_lo = lo;
+  ev.global_clk = gclk;
+  ev.pc = pc;
+  ev.mp = (uint32_t)off;
+}
+
 void generate_dependencies(ExecutionRecord& rec) {
   // CpuChip (cpu/trace.rs:58-79,182-243), MemoryAccessCols::populate_access
   // (memory/consistency/trace.rs:52-77), AddSubChip (alu/mod.rs:95-116; operations/add.rs:20-40).
@@ -170,19 +329,44 @@ void generate_dependencies(ExecutionRecord& rec) {
   }
 }
 
-bool chip_included(int chip, const ExecutionRecord& r) {
+EventCounts counts_of(const ExecutionRecord& r) {
+  EventCounts n;
+  n.cpu = r.cpu.size();
+  n.alu = r.alu.size();
+  n.jump = r.jump.size();
+  n.meminstr = r.meminstr.size();
+  n.io = r.io.size();
+  n.memory = r.memory.size();
+  n.program = r.program ? r.program->instructions.size() : 0;
+  return n;
+}
+
+EventCounts counts_of(const HostEvents& e, const Program& prog) {
+  EventCounts n;
+  n.cpu = e.cpu.n;
+  n.alu = e.alu.n;
+  n.jump = e.jump.n;
+  n.meminstr = e.meminstr.n;
+  n.io = e.io.n;
+  n.memory = e.memory.n;
+  n.program = prog.instructions.size();
+  return n;
+}
+
+bool chip_included(int chip, const EventCounts& n) {
   switch (chip) {
-    case CHIP_CPU: return !r.cpu.empty();
+    case CHIP_CPU: return n.cpu != 0;
     case CHIP_PROGRAM: return true;
-    case CHIP_ADDSUB: return !r.alu.empty();
-    case CHIP_JUMP: return !r.jump.empty();
-    case CHIP_MEMORY: return !r.memory.empty();
+    case CHIP_ADDSUB: return n.alu != 0;
+    case CHIP_JUMP: return n.jump != 0;
+    case CHIP_MEMORY: return n.memory != 0;
     case CHIP_BYTE: return true;
-    case CHIP_MEMINSTRS: return !r.meminstr.empty();
-    case CHIP_IO: return !r.io.empty();
+    case CHIP_MEMINSTRS: return n.meminstr != 0;
+    case CHIP_IO: return n.io != 0;
   }
   return false;
 }
+bool chip_included(int chip, const ExecutionRecord& r) { return chip_included(chip, counts_of(r)); }
 
 static size_t npot(size_t n) {
   size_t p = 1;
@@ -191,18 +375,21 @@ static size_t npot(size_t n) {
 }
 static size_t npot16(size_t n) { return std::max<size_t>(16, npot(n)); }
 
-size_t main_trace_height(int chip, const ExecutionRecord& r) {
+size_t main_trace_height(int chip, const EventCounts& n) {
   switch (chip) {
-    case CHIP_CPU: return npot(r.cpu.size());  // no minimum (cpu/trace.rs:33)
-    case CHIP_PROGRAM: return npot16(r.program->instructions.size());
-    case CHIP_ADDSUB: return npot16(r.alu.size());
-    case CHIP_JUMP: return npot16(r.jump.size());
-    case CHIP_MEMORY: return npot16((r.memory.size() + 1) / 2);
+    case CHIP_CPU: return npot(n.cpu);  // no minimum (cpu/trace.rs:33)
+    case CHIP_PROGRAM: return npot16(n.program);
+    case CHIP_ADDSUB: return npot16(n.alu);
+    case CHIP_JUMP: return npot16(n.jump);
+    case CHIP_MEMORY: return npot16((n.memory + 1) / 2);
     case CHIP_BYTE: return 1u << 16;
-    case CHIP_MEMINSTRS: return npot16(r.meminstr.size());
-    case CHIP_IO: return npot16(r.io.size());
+    case CHIP_MEMINSTRS: return npot16(n.meminstr);
+    case CHIP_IO: return npot16(n.io);
   }
   return 0;
+}
+size_t main_trace_height(int chip, const ExecutionRecord& r) {
+  return main_trace_height(chip, counts_of(r));
 }
 
 namespace {

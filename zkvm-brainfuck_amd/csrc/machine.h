@@ -59,6 +59,45 @@ void execute(const Program& prog, const uint8_t* in, size_t nin, ExecutionRecord
 // StarkMachine::generate_dependencies (crates/stark/src/machine.rs:228-248)
 void generate_dependencies(ExecutionRecord& rec);
 
+// The prover pipeline's executor: the same events as execute(), written into growable arrays
+// whose memory the caller chooses (pinned host memory, so the upload to HBM is one DMA per array
+// with no staging), memory cells in a dense offset-indexed array reused across runs, and the
+// memory events emitted in address order from the final cells (the normal form) with no sort.
+// Reused across runs, a HostEvents stops allocating once it has seen the largest run.
+struct HostEvents {
+  using AllocFn = void* (*)(size_t);
+  using FreeFn = void (*)(void*);
+  template <class T>
+  struct Arr {
+    T* p = nullptr;
+    size_t n = 0, cap = 0;
+  };
+  AllocFn alloc = nullptr;  // malloc / free when null
+  FreeFn dealloc = nullptr;
+  Arr<CpuEvent> cpu;
+  Arr<AluEvent> alu;
+  Arr<JumpEvent> jump;
+  Arr<MemInstrEvent> meminstr;
+  Arr<IoEvent> io;
+  Arr<MemoryEvent> memory;
+  std::vector<uint8_t> output;
+  uint64_t global_clk = 0;
+  uint32_t pc = 0, mp = 0;
+  struct Cell {
+    uint32_t ts;
+    uint8_t value, touched;
+  };
+  std::vector<Cell> cells;  // cells[off - cell_lo] for memory offset off (address = (u32)off)
+  int64_t cell_lo = 0;
+  HostEvents() = default;
+  HostEvents(const HostEvents&) = delete;
+  HostEvents& operator=(const HostEvents&) = delete;
+  ~HostEvents();
+  template <class T>
+  void grow(Arr<T>& a, size_t need);
+};
+void execute_into(const Program& prog, const uint8_t* in, size_t nin, HostEvents& ev);
+
 // Chips in machine order (crates/core/machine/src/brainfuck/mod.rs:53-81).
 enum Chip : int {
   CHIP_CPU = 0, CHIP_PROGRAM, CHIP_ADDSUB, CHIP_JUMP, CHIP_MEMORY, CHIP_BYTE,
@@ -75,6 +114,15 @@ inline int perm_width(int chip) {  // permutation_trace_width (permutation.rs:15
   int n = CHIP_INFO[chip].n_interactions;
   return n ? (n + 1) / 2 + 1 : 0;
 }
+
+// What chip inclusion and main-trace heights depend on: the event count of each kind.
+struct EventCounts {
+  size_t cpu = 0, alu = 0, jump = 0, meminstr = 0, io = 0, memory = 0, program = 0;
+};
+EventCounts counts_of(const ExecutionRecord& rec);
+EventCounts counts_of(const HostEvents& ev, const Program& prog);
+bool chip_included(int chip, const EventCounts& n);
+size_t main_trace_height(int chip, const EventCounts& n);
 
 bool chip_included(int chip, const ExecutionRecord& rec);
 // Row-major main trace in Montgomery form; returns height.

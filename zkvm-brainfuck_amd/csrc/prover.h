@@ -101,6 +101,24 @@ void upload_host_traces(const int* chips, const uint32_t* const* mats, const siz
 std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const ProveOptions& opt,
                                   StageTimes* times);
 
+// The split MachineProver surface (crates/stark/src/prover.rs:209-236 commit, :242-553 open).
+// MainData is ShardMainData (types.rs:13-18) kept in HBM: the traces' evaluations, the
+// committed LDEs and their Merkle tree, alive from commit until the owner frees it.
+struct MainData {
+  DeviceTraces dt;
+  std::vector<int> order;   // dt index of the k-th committed matrix
+  std::vector<int> chip;    // chip of the k-th committed matrix, sorted (Reverse(height), name)
+  std::vector<size_t> hn;   // its height
+  Round mainr;              // the main commit (LDEs + tree)
+};
+void commit_main(MainData& md);  // md.dt holds the traces
+// Challenger state after pk.observe_into (prover.rs:595-601) on a fresh DuplexChallenger.
+Challenger challenger_after_pk(const ProvingKey& pk);
+// ch = the prover's challenger after pk.observe_into; not modified (the reference opens on a
+// clone, prover.rs:578).  md may be opened more than once.
+std::vector<uint8_t> open_main(const ProvingKey& pk, MainData& md, const Challenger& ch,
+                               const ProveOptions& opt);
+
 int num_queries_from_env();
 bool observe_openings_from_env();  // BFZ_OBSERVE_OPENINGS = 1 (default) | 0
 

@@ -6,6 +6,7 @@
 // and the p3 TwoAdicFriPcs::{commit, open} / fri::prover [p3-recalled].  All bulk data stays
 // in HBM; only digests, challenges, opened values and the query openings cross to the host.
 #include "prover.h"
+#include "pipeline.h"
 
 #include <algorithm>
 #include <cerrno>
@@ -257,53 +258,127 @@ void upload_host_traces(const int* chips, const uint32_t* const* mats, const siz
 }
 
 // ------------------------------------------------------------------------ prove
-std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const ProveOptions& opt,
-                                  StageTimes* times) {
-  hipStream_t st = stream();
-  StageTimes local_times;
-  StageTimes* tms = times ? times : &local_times;
+namespace {
+// Timing and host-staging scope of one prove call (or one commit / open call of the split
+// MachineProver surface).  Kernel probes and stage events are on only when timing is asked for.
+struct ProofScope {
   EvTimer ev;
-  ev.on = opt.timing && times;
-  ntt_probe().reset();
-  ntt_probe().on = ev.on;
-  p2_probe().reset();
-  p2_probe().on = ev.on;
+  StageTimes local;
+  StageTimes* tms;
+  hipEvent_t e_total = nullptr;
   std::vector<std::vector<EF>> keep;  // host buffers of async uploads live until the end
-  struct StagingScope {  // the pinned upload arena is rewound when the proof is done
-    ~StagingScope() {
-      (void)hipStreamSynchronize(stream());
-      staging_reset();
-    }
-  } staging_scope;
-  const auto t_start = std::chrono::steady_clock::now();
-  hipEvent_t e_total = ev.on ? ev.begin(st) : nullptr;
+  ProofScope(bool timing, StageTimes* times) : tms(times ? times : &local) {
+    ev.on = timing && times;
+    ntt_probe().reset();
+    ntt_probe().on = ev.on;
+    p2_probe().reset();
+    p2_probe().on = ev.on;
+    if (ev.on) e_total = ev.begin(stream());
+  }
+  void finish() {  // collects every event of the call into *tms
+    if (!ev.on) return;
+    ev.end(e_total, stream(), &tms->total);
+    ev.collect();
+    KernelProbe& pr = ntt_probe();
+    pr.collect();
+    pr.on = false;
+    tms->ntt_kernel_ms = pr.ms;
+    tms->ntt_kernel_bytes = pr.bytes;
+    tms->ntt_kernel_launches = pr.launches;
+    KernelProbe& p2 = p2_probe();
+    p2.collect();
+    p2.on = false;
+    tms->p2_kernel_ms = p2.ms;
+    tms->p2_perms = p2.bytes;
+    tms->p2_launches = p2.launches;
+  }
+  ~ProofScope() {  // the pinned upload arena is rewound when the call is done
+    (void)hipStreamSynchronize(stream());
+    staging_reset();
+    ntt_probe().on = false;
+    p2_probe().on = false;
+  }
+};
 
-  Challenger ch;
-  ch.observe_digest(pk.prep.tree.root);  // observe_into: commit + 7 zeros
-  for (int i = 0; i < 7; i++) ch.observe(0);
-
-  // ---- commit main (prover.rs:209-236)
+// MachineProver::commit (prover.rs:209-236): sort by (Reverse(height), name), coset LDE of
+// every main trace, one MerkleTreeMmcs commit.  md.dt must hold the traces.
+void commit_main_impl(MainData& md, ProofScope& ps) {
+  hipStream_t st = stream();
+  DeviceTraces& dt = md.dt;
   const int nc = (int)dt.chips.size();
-  std::vector<int> order(nc);
-  for (int i = 0; i < nc; i++) order[i] = i;
-  std::sort(order.begin(), order.end(), [&](int a, int b) {
+  md.order.resize(nc);
+  for (int i = 0; i < nc; i++) md.order[i] = i;
+  std::sort(md.order.begin(), md.order.end(), [&](int a, int b) {
     if (dt.heights[a] != dt.heights[b]) return dt.heights[a] > dt.heights[b];
     return std::strcmp(CHIP_INFO[dt.chips[a]].name, CHIP_INFO[dt.chips[b]].name) < 0;
   });
-  std::vector<int> chip(nc);
-  std::vector<size_t> hn(nc);
+  md.chip.resize(nc);
+  md.hn.resize(nc);
   for (int k = 0; k < nc; k++) {
-    chip[k] = dt.chips[order[k]];
-    hn[k] = dt.heights[order[k]];
+    md.chip[k] = dt.chips[md.order[k]];
+    md.hn[k] = dt.heights[md.order[k]];
   }
-  hipEvent_t e0 = ev.on ? ev.begin(st) : nullptr;
-  Round mainr;
-  mainr.mats.resize(nc);
+  hipEvent_t e0 = ps.ev.on ? ps.ev.begin(st) : nullptr;
+  md.mainr = Round();
+  md.mainr.mats.resize(nc);
   for (int k = 0; k < nc; k++)
-    lde_into(mainr.mats[k], dt.evals[order[k]].p, hn[k], CHIP_INFO[chip[k]].main_w, ONE, st, &ev,
-             tms);
-  mainr.commit(st);
-  if (ev.on) ev.end(e0, st, &tms->main_commit);
+    lde_into(md.mainr.mats[k], dt.evals[md.order[k]].p, md.hn[k], CHIP_INFO[md.chip[k]].main_w, ONE,
+             st, &ps.ev, ps.tms);
+  md.mainr.commit(st);
+  if (ps.ev.on) ps.ev.end(e0, st, &ps.tms->main_commit);
+}
+
+std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch,
+                               const ProveOptions& opt, ProofScope& ps);
+}  // namespace
+
+void commit_main(MainData& md) {
+  ProofScope ps(false, nullptr);
+  commit_main_impl(md, ps);
+  HIP_CHECK(hipStreamSynchronize(stream()));
+}
+
+std::vector<uint8_t> open_main(const ProvingKey& pk, MainData& md, const Challenger& ch,
+                               const ProveOptions& opt) {
+  ProofScope ps(false, nullptr);
+  return open_impl(pk, md, ch, opt, ps);
+}
+
+Challenger challenger_after_pk(const ProvingKey& pk) {
+  Challenger ch;
+  ch.observe_digest(pk.prep.tree.root);  // observe_into (prover.rs:595-601): commit + 7 zeros
+  for (int i = 0; i < 7; i++) ch.observe(0);
+  return ch;
+}
+
+std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const ProveOptions& opt,
+                                  StageTimes* times) {
+  ProofScope ps(opt.timing, times);
+  MainData md;
+  md.dt = std::move(dt);
+  commit_main_impl(md, ps);
+  auto proof = open_impl(pk, md, challenger_after_pk(pk), opt, ps);
+  ps.finish();
+  dt = std::move(md.dt);
+  return proof;
+}
+
+namespace {
+// MachineProver::open (prover.rs:242-553) on the challenger state after pk.observe_into (the
+// reference opens on a clone of it, prover.rs:578): observe the main commit, LogUp, quotient,
+// PCS open, FRI, grind, queries, BFZ1 serialization.
+std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch,
+                               const ProveOptions& opt, ProofScope& ps) {
+  hipStream_t st = stream();
+  EvTimer& ev = ps.ev;
+  StageTimes* tms = ps.tms;
+  std::vector<std::vector<EF>>& keep = ps.keep;
+  DeviceTraces& dt = md.dt;
+  const std::vector<int>& order = md.order;
+  const std::vector<int>& chip = md.chip;
+  const std::vector<size_t>& hn = md.hn;
+  const Round& mainr = md.mainr;
+  const int nc = (int)chip.size();
 
   // ---- open (prover.rs:242-553), on a clone of the challenger (prover.rs:578)
   ch.observe_digest(mainr.tree.root);
@@ -702,25 +777,9 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
   }
   w.ef(fin[0]);
   w.u32(witness);
-  if (ev.on) {
-    ev.end(e_total, st, &tms->total);
-    ev.collect();
-    KernelProbe& pr = ntt_probe();
-    pr.collect();
-    pr.on = false;
-    tms->ntt_kernel_ms = pr.ms;
-    tms->ntt_kernel_bytes = pr.bytes;
-    tms->ntt_kernel_launches = pr.launches;
-    KernelProbe& p2 = p2_probe();
-    p2.collect();
-    p2.on = false;
-    tms->p2_kernel_ms = p2.ms;
-    tms->p2_perms = p2.bytes;
-    tms->p2_launches = p2.launches;
-  }
-  (void)t_start;
   return std::move(w.b);
 }
+}  // namespace
 
 std::vector<uint8_t> prove_events(const ProvingKey& pk, const DeviceEvents& ev,
                                   const ProveOptions& opt, StageTimes* times) {
@@ -750,12 +809,12 @@ std::vector<uint8_t> prove_events(const ProvingKey& pk, const DeviceEvents& ev,
 std::vector<uint8_t> prove(const ProvingKey& pk, const uint8_t* in, size_t nin,
                            const ProveOptions& opt, StageTimes* times,
                            std::vector<uint8_t>* output_stream, uint64_t* cycles) {
-  ExecutionRecord rec;
-  execute(pk.program, in, nin, rec);
+  HostEvents& h = scratch_events();  // the pipeline executor into pinned memory
+  execute_into(pk.program, in, nin, h);
   DeviceEvents ev;
-  upload_events(rec, ev, stream());
-  if (output_stream) *output_stream = rec.output;
-  if (cycles) *cycles = rec.global_clk;
+  upload_events(h, pk.program, ev, stream());
+  if (output_stream) *output_stream = h.output;
+  if (cycles) *cycles = h.global_clk;
   return prove_events(pk, ev, opt, times);
 }
 

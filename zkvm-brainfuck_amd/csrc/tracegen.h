@@ -26,6 +26,16 @@ struct DeviceEvents {
 // Host -> HBM copy of the record's events (the proof's inputs).
 void upload_events(const ExecutionRecord& rec, DeviceEvents& ev, hipStream_t st);
 
+// The same from the pipeline executor's events (machine.h HostEvents; pinned host memory gives
+// one DMA per event array).  Returns when the copies are done.
+void upload_events(const HostEvents& h, const Program& prog, DeviceEvents& ev, hipStream_t st);
+// Chip inclusion, heights and counts of ev from the event counts (the device buffers are set
+// by the caller).
+void set_event_meta(DeviceEvents& ev, const EventCounts& n, uint64_t global_clk);
+// Pinned host memory for HostEvents (hipHostMalloc / hipHostFree).
+void* pinned_alloc(size_t bytes);
+void pinned_free(void* p);
+
 // generate_dependencies + generate_traces on the device, into dt (replaces its contents).
 void generate_traces_device(const DeviceEvents& ev, DeviceTraces& dt, hipStream_t st);
 

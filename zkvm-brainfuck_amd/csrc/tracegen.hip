@@ -315,6 +315,22 @@ void put(DBuf<T>& d, const std::vector<T>& v, hipStream_t st) {
 
 }  // namespace
 
+void set_event_meta(DeviceEvents& ev, const EventCounts& n, uint64_t global_clk) {
+  ev.n[CHIP_CPU] = n.cpu;
+  ev.n[CHIP_PROGRAM] = n.program;
+  ev.n[CHIP_ADDSUB] = n.alu;
+  ev.n[CHIP_JUMP] = n.jump;
+  ev.n[CHIP_MEMORY] = n.memory;
+  ev.n[CHIP_BYTE] = 0;
+  ev.n[CHIP_MEMINSTRS] = n.meminstr;
+  ev.n[CHIP_IO] = n.io;
+  for (int c = 0; c < NUM_CHIPS; c++) {
+    ev.included[c] = chip_included(c, n);
+    ev.height[c] = main_trace_height(c, n);
+  }
+  ev.global_clk = global_clk;
+}
+
 void upload_events(const ExecutionRecord& rec, DeviceEvents& ev, hipStream_t st) {
   put(ev.cpu, rec.cpu, st);
   put(ev.alu, rec.alu, st);
@@ -323,20 +339,37 @@ void upload_events(const ExecutionRecord& rec, DeviceEvents& ev, hipStream_t st)
   put(ev.io, rec.io, st);
   put(ev.memory, rec.memory, st);
   put(ev.prog, rec.program->instructions, st);
-  ev.n[CHIP_CPU] = rec.cpu.size();
-  ev.n[CHIP_PROGRAM] = rec.program->instructions.size();
-  ev.n[CHIP_ADDSUB] = rec.alu.size();
-  ev.n[CHIP_JUMP] = rec.jump.size();
-  ev.n[CHIP_MEMORY] = rec.memory.size();
-  ev.n[CHIP_BYTE] = 0;
-  ev.n[CHIP_MEMINSTRS] = rec.meminstr.size();
-  ev.n[CHIP_IO] = rec.io.size();
-  for (int c = 0; c < NUM_CHIPS; c++) {
-    ev.included[c] = chip_included(c, rec);
-    ev.height[c] = main_trace_height(c, rec);
-  }
-  ev.global_clk = rec.global_clk;
+  set_event_meta(ev, counts_of(rec), rec.global_clk);
   HIP_CHECK(hipStreamSynchronize(st));  // the host vectors may be freed after this returns
+}
+
+namespace {
+template <class T>
+void put_arr(DBuf<T>& d, const HostEvents::Arr<T>& a, hipStream_t st) {
+  d.reset(std::max<size_t>(a.n, 1));
+  if (a.n) HIP_CHECK(hipMemcpyAsync(d.p, a.p, a.n * sizeof(T), hipMemcpyHostToDevice, st));
+}
+}  // namespace
+
+void upload_events(const HostEvents& h, const Program& prog, DeviceEvents& ev, hipStream_t st) {
+  put_arr(ev.cpu, h.cpu, st);
+  put_arr(ev.alu, h.alu, st);
+  put_arr(ev.jump, h.jump, st);
+  put_arr(ev.meminstr, h.meminstr, st);
+  put_arr(ev.io, h.io, st);
+  put_arr(ev.memory, h.memory, st);
+  put(ev.prog, prog.instructions, st);
+  set_event_meta(ev, counts_of(h, prog), h.global_clk);
+  HIP_CHECK(hipStreamSynchronize(st));
+}
+
+void* pinned_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+  return p;
+}
+void pinned_free(void* p) {
+  if (p) (void)hipHostFree(p);
 }
 
 void generate_traces_device(const DeviceEvents& ev, DeviceTraces& dt, hipStream_t st) {
