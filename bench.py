@@ -164,13 +164,14 @@ def cpu_baseline():
                       f"OpenMP threads"}
 
 
-def end_to_end(client, pk, prog, stdin, jobs=8):
+def end_to_end(client, pk, prog, stdin, jobs=24):
     """Proofs from (program, stdin) with execution and upload included: the reference's
     utils/prove.rs:23-66 loop (execute, then prove) as bfz_prove_batch pipelines it -- executor
     threads into pinned memory, a copy stream for the events, the GPU proving job k while job
     k+1 executes and uploads -- next to one unpipelined bfz_prove (execute + upload + prove)."""
     import time as _t
-    client.prove_batch(pk, [stdin] * 2, public_values=False)  # warm the pinned buffers
+    # warm-up batch: every pinned host buffer reaches its steady size (growth pins fresh pages)
+    client.prove_batch(pk, [stdin] * 8, public_values=False)
     stats = {}
     t0 = _t.perf_counter()
     proofs = client.prove_batch(pk, [stdin] * jobs, public_values=False, stats=stats)
