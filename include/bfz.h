@@ -112,6 +112,8 @@ void bfz_pk_free(bfz_pk* pk);
  *   bfz_main_commit         MachineProver::commit (crates/stark/src/prover.rs:209-236): host
  *                           row-major main traces (as bfz_prove_traces) -> LDE + MerkleTreeMmcs
  *                           commit in HBM; root = main_commit (8 Montgomery words, as vk_commit).
+ *                           pk may be NULL (the trait's commit takes no key); if given, bfz_open
+ *                           refuses the data for any other key.
  *   bfz_record_main_commit  the same from a device-resident record (traces generated on device).
  *   bfz_challenger_observe_pk  MachineProvingKey::observe_into (prover.rs:595-601).
  *   bfz_open                MachineProver::open (prover.rs:242-553) on the challenger state

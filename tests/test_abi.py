@@ -231,3 +231,23 @@ def test_pipeline_executor_random_programs_and_tape_wrap():
         assert a == b, p
     with pytest.raises(_lib.BfzError, match="input"):
         _events(",", [], 1)
+
+
+def _arity(params: str) -> int:
+    params = re.sub(r"\([^()]*\)", "", params)  # function-pointer types
+    params = params.strip()
+    return 0 if params in ("", "void") else params.count(",") + 1
+
+
+def test_rust_ffi_matches_header():
+    """crates/bfz-sys (the Rust binding a maintainer adds; not compiled here) declares every
+    entry point of include/bfz.h with the same number of arguments."""
+    hdr = open(os.path.join(ROOT, "include", "bfz.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    c = {m.group(1): _arity(m.group(2))
+         for m in re.finditer(r"\b(bfz_[a-z0-9_]+)\s*\(((?:[^()]|\([^()]*\))*)\)\s*;", hdr)}
+    rs = open(os.path.join(ROOT, "crates", "bfz-sys", "src", "lib.rs")).read()
+    r = {m.group(1): _arity(re.sub(r"\w+\s*:", "", m.group(2)))
+         for m in re.finditer(r"pub fn (bfz_[a-z0-9_]+)\(((?:[^()]|\([^()]*\))*)\)", rs)}
+    assert set(c) == set(declared_symbols())
+    assert c == r

@@ -174,10 +174,18 @@ def test_split_commit_open_matches_prove(client):
     bad = prover.open(pk, data, prover.new_challenger())
     with pytest.raises(_lib.BfzError):
         client.verify(sdk.BfProofWithPublicValues(proof=bad, stdin=bytes([17])), vk)
-    # main data committed for another key is refused
+    # main data committed for another key is refused; a key-less commit (the trait's commit
+    # takes no key) opens under any key
     pk2, _ = client.setup(guests.HELLO)
     with pytest.raises(_lib.BfzError, match="another key"):
         prover.open(pk2, data, ch)
+    mats, chips, ptrs, hs, ws, k = sdk._trace_args(traces)
+    out = ctypes.c_void_p()
+    root = (ctypes.c_uint32 * 8)()
+    _lib.check(_lib.lib().bfz_main_commit(None, chips, ptrs, hs, ws, k, ctypes.byref(out), root))
+    keyless = sdk.ShardMainData(out.value, root)
+    assert keyless.main_commit == data.main_commit
+    assert prover.open(pk, keyless, ch) == pf
 
 
 def test_prove_batch_pipelined_matches_single(client):
