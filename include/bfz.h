@@ -171,7 +171,9 @@ void bfz_record_free(bfz_record* rec);
  * FRI commit phase, crates/stark/src/prover.rs:209-236,460-470); the ranks exchange subtree
  * roots and query openings through the callbacks (torch.distributed / RCCL on the host
  * side).  Every rank returns the same proof, byte-identical to bfz_record_prove's.  The
- * callbacks return 0 on success. */
+ * callbacks return 0 on success.  Their buffers (send / recv / data) are DEVICE pointers on the
+ * rank's GPU (the library's stream is synchronized before each call and the data must be in
+ * place when the callback returns): ncclAllGather / ncclAllReduce run on them directly. */
 typedef int (*bfz_allgather_fn)(void* ctx, const void* send, size_t bytes, void* recv);
 typedef int (*bfz_allreduce_u32_fn)(void* ctx, uint32_t* data, size_t n);
 int bfz_record_prove_sharded(const bfz_pk* pk, const bfz_record* rec, int rank, int world,
@@ -187,7 +189,8 @@ int bfz_record_prove_sharded(const bfz_pk* pk, const bfz_record* rec, int rank, 
  * device exchange buffers of 2n * w_local words; alltoall(ctx) must exchange equal blocks of
  * d_send into d_recv (block j to rank j, e.g. ncclAllToAll / torch all_to_all_single), and
  * allgather is as above.  out receives [root (8) | FRI roots (8 per round) | final value (4)]
- * (*nwords words, identical on every rank and to world = 1).  cap = capacity of out in words. */
+ * (*nwords words, identical on every rank and to world = 1).  cap = capacity of out in words.
+ * As above, the allgather buffers are device pointers. */
 typedef int (*bfz_alltoall_fn)(void* ctx);
 int bfz_commit_fri_sharded(const uint32_t* d_cols, int log_n, size_t w_local, int rank, int world,
                            uint32_t* d_send, uint32_t* d_recv, bfz_alltoall_fn alltoall,

@@ -53,7 +53,8 @@ def test_timed_steps_two_gloo_ranks_take_max():
 
 def _coll_rank(rank, world, port, q):
     """The host side of the sharded prover's two exchanges (bfz/shard.py Collectives), driven
-    through the same ctypes callback objects libbfz calls, on a gloo group (no GPU)."""
+    through the same ctypes callback objects libbfz calls, on a gloo group.  With no GPU here the
+    buffers are host memory (pointers="host"); the GPU tests run the device-pointer form."""
     import ctypes
 
     import numpy as np
@@ -62,7 +63,7 @@ def _coll_rank(rank, world, port, q):
     from bfz import shard
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    coll = shard.Collectives(dist)
+    coll = shard.Collectives(dist, pointers="host")
     # all-gather of 32-byte subtree roots: rank r sends its own digest
     send = np.arange(1, 9, dtype=np.uint32) + 1000 * rank
     recv = np.zeros(8 * world, dtype=np.uint32)

@@ -2,9 +2,10 @@
 
 Every rank holds the same record and proving key; bfz_record_prove_sharded hashes this
 rank's subtree of every large Merkle tree and calls back here for the two exchanges: an
-all-gather of subtree roots and a sum all-reduce of the owner-masked query openings.  With the
-nccl backend (RCCL on ROCm) the exchanged buffers travel as device tensors over xGMI; with
-gloo they stay on the host (used by the tests, which run several ranks on one GPU).
+all-gather of subtree roots and a sum all-reduce of the owner-masked query openings.  The
+callbacks receive device pointers: with the nccl backend (RCCL on ROCm) the collectives run on
+zero-copy tensor views of them, over xGMI; with gloo (the tests, several ranks on one GPU) they
+go through host tensors.
 """
 from __future__ import annotations
 
@@ -16,30 +17,61 @@ import numpy as np
 from . import _lib
 
 
-class Collectives:
-    """ctypes callbacks over a torch.distributed process group."""
+class _DeviceSpan:
+    """A raw device pointer seen by torch.as_tensor through __cuda_array_interface__ (no copy)."""
 
-    def __init__(self, dist, group=None, device=None):
+    def __init__(self, ptr: int, nbytes: int, typestr: str = "|u1"):
+        item = int(typestr[-1])
+        self.__cuda_array_interface__ = {"shape": (nbytes // item,), "typestr": typestr,
+                                         "data": (int(ptr), False), "version": 2, "strides": None}
+
+
+class Collectives:
+    """ctypes callbacks over a torch.distributed process group.
+
+    libbfz passes DEVICE pointers on the rank's GPU (its stream already synchronized).  With the
+    nccl backend (RCCL) the collective runs on views of those buffers, device to device over
+    xGMI; with gloo (several test ranks sharing one GPU) the data goes through host tensors."""
+
+    def __init__(self, dist, group=None, device=None, pointers="device"):
+        """pointers="host" reads the callback buffers as host memory: only for testing the
+        exchange logic on a machine without a GPU (libbfz always passes device pointers)."""
         import torch
         self.dist, self.group, self.torch = dist, group, torch
         self.world = dist.get_world_size(group)
         backend = str(dist.get_backend(group)).lower()
-        self.dev = (torch.device("cuda", device if device is not None else 0)
-                    if "nccl" in backend else torch.device("cpu"))
+        self.cuda = torch.device("cuda", device if device is not None else 0)
+        self.host_ptrs = pointers == "host"
+        self.nccl = "nccl" in backend and not self.host_ptrs
+        self.dev = self.cuda if self.nccl else torch.device("cpu")
         self.allgather = _lib.ALLGATHER_FN(self._allgather)
         self.allreduce = _lib.ALLREDUCE_FN(self._allreduce)
         self.alltoall = _lib.ALLTOALL_FN(self._alltoall)
         self.exchange = None  # (send, recv) device tensors of the pending all-to-all
 
+    def _view(self, ptr, nbytes, typestr="|u1"):
+        if self.host_ptrs:
+            dt = {"|u1": np.uint8, "<i4": np.int32}[typestr]
+            buf = (ctypes.c_uint8 * nbytes).from_address(ptr)
+            return self.torch.from_numpy(np.frombuffer(buf, dtype=dt))
+        return self.torch.as_tensor(_DeviceSpan(ptr, nbytes, typestr), device=self.cuda)
+
+    def _sync(self):
+        if not self.host_ptrs:
+            self.torch.cuda.synchronize(self.cuda)
+
     def _allgather(self, _ctx, send, nbytes, recv):
         try:
             torch = self.torch
-            buf = (ctypes.c_uint8 * nbytes).from_address(send)
-            t = torch.frombuffer(bytearray(buf), dtype=torch.uint8).to(self.dev)
-            parts = [torch.empty_like(t) for _ in range(self.world)]
-            self.dist.all_gather(parts, t, group=self.group)
-            out = torch.cat(parts).cpu().numpy()
-            ctypes.memmove(recv, out.ctypes.data, out.nbytes)
+            src = self._view(send, nbytes)
+            dst = self._view(recv, nbytes * self.world)
+            if self.nccl:
+                self.dist.all_gather_into_tensor(dst, src, group=self.group)
+            else:
+                parts = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(self.world)]
+                self.dist.all_gather(parts, src.cpu(), group=self.group)
+                dst.copy_(torch.cat(parts))
+            self._sync()
             return 0
         except Exception:  # noqa: BLE001 - reported to the C side as a failed collective
             traceback.print_exc()
@@ -48,23 +80,26 @@ class Collectives:
     def _allreduce(self, _ctx, data, n):
         try:
             torch = self.torch
-            arr = np.ctypeslib.as_array(data, shape=(n,))
             # exactly one rank contributes each word (< 2^31): an int32 sum is exact
-            t = torch.from_numpy(arr.view(np.int32).copy()).to(self.dev)
-            self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
-            arr[:] = t.cpu().numpy().view(np.uint32)
+            t = self._view(ctypes.cast(data, ctypes.c_void_p).value, 4 * n, "<i4")
+            if self.nccl:
+                self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
+            else:
+                h = t.cpu()
+                self.dist.all_reduce(h, op=self.dist.ReduceOp.SUM, group=self.group)
+                t.copy_(h)
+            self._sync()
             return 0
         except Exception:  # noqa: BLE001
             traceback.print_exc()
             return 1
-
 
     def _alltoall(self, _ctx):
         """Equal-block all-to-all of the registered device tensors (RCCL with nccl; through
         host memory with gloo)."""
         try:
             send, recv = self.exchange
-            if self.dev.type == "cuda":
+            if self.nccl:
                 self.dist.all_to_all_single(recv, send, group=self.group)
                 self.torch.cuda.synchronize(recv.device)
             else:

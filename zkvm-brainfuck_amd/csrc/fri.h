@@ -3,6 +3,7 @@
 #include <vector>
 
 #include "gpu.h"
+#include "merkle.h"
 
 namespace bfz {
 
@@ -60,11 +61,12 @@ struct GatherSeg {
   int32_t own_shift;
   int32_t pad;
 };
-// out[q * words_per_query + ...] = the segments' words for qidx[q], segments in order
-// (this rank's share when rank/world describe a sharded proof).
+// out[q * words_per_query + ...] = the segments' words for qidx[q], segments in order.  In a
+// sharded proof (shard != nullptr, world > 1) every rank writes the words it owns and one sum
+// all-reduce over the device buffer completes them.
 // Returns the nwords gathered words (canonical form) in a pinned host buffer that stays valid
 // until the next call.
 uint32_t* gather_queries(const std::vector<GatherSeg>& segs, const std::vector<uint32_t>& qidx,
-                         size_t& nwords, int rank, hipStream_t st);
+                         size_t& nwords, const ShardCtx* shard, hipStream_t st);
 
 }  // namespace bfz

@@ -395,7 +395,8 @@ uint32_t grind(const GrindState& gs, int bits, hipStream_t st) {
 // The gathered words land in a pinned host buffer (grown on demand, reused by every proof):
 // the device-to-host copy is a plain DMA instead of a runtime staging through pageable memory.
 uint32_t* gather_queries(const std::vector<GatherSeg>& segs, const std::vector<uint32_t>& qidx,
-                         size_t& nwords, int rank, hipStream_t st) {
+                         size_t& nwords, const ShardCtx* shard, hipStream_t st) {
+  const int rank = shard ? shard->rank : 0;
   std::vector<uint32_t> off(segs.size());
   uint32_t wpq = 0;
   for (size_t s = 0; s < segs.size(); s++) {
@@ -421,6 +422,10 @@ uint32_t* gather_queries(const std::vector<GatherSeg>& segs, const std::vector<u
                      (const GatherSeg*)dseg.p, (int)segs.size(), (const uint32_t*)doff.p, wpq,
                      (const uint32_t*)dq.p, (int)qidx.size(), rank, dout.p);
   KCHECK();
+  if (shard && shard->world > 1) {  // owner-masked words: one sum all-reduce, device to device
+    HIP_CHECK(hipStreamSynchronize(st));
+    shard->allreduce_sum_u32(dout.p, nwords);
+  }
   HIP_CHECK(hipMemcpyAsync(host, dout.p, nwords * 4, hipMemcpyDeviceToHost, st));
   HIP_CHECK(hipStreamSynchronize(st));
   return host;

@@ -29,6 +29,8 @@ struct MerkleTree {
 // SHARD_MIN_LEAVES leaves are built as one subtree per rank plus redundant top layers.
 struct ShardCtx {
   int rank = 0, world = 1;
+  // Every buffer below is DEVICE memory on this rank's GPU (RCCL moves it over xGMI with no host
+  // copy).  The prover stream is synchronized before a call; the data is in place on return.
   // all-gather `bytes` from every rank into recv (world * bytes, rank order)
   std::function<void(const void* send, size_t bytes, void* recv)> allgather;
   // element-wise sum over ranks, in place

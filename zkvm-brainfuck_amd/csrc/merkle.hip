@@ -359,14 +359,12 @@ static void build_sharded(MerkleTree& t, size_t h0, const std::vector<const MatR
     launch_layer(t, L, k * (nlen / G), nlen / G, grp, st);
     len = nlen;
   }
-  uint32_t mine[8];  // layer nl - lg has G nodes; node k is ours
-  std::vector<uint32_t> all(8 * G);
+  // layer nl - lg has G nodes; node k is ours: all-gather them device to device
   DBuf<uint32_t>& lay = t.layers[nl - lg];
-  HIP_CHECK(hipMemcpyAsync(mine, lay.p + 8 * k, 32, hipMemcpyDeviceToHost, st));
+  DBuf<uint32_t> all(8 * G);
   HIP_CHECK(hipStreamSynchronize(st));
-  c.allgather(mine, 32, all.data());
-  HIP_CHECK(hipMemcpyAsync(lay.p, all.data(), all.size() * 4, hipMemcpyHostToDevice, st));
-  HIP_CHECK(hipStreamSynchronize(st));  // `all` goes out of scope
+  c.allgather(lay.p + 8 * k, 32, all.p);
+  HIP_CHECK(hipMemcpyAsync(lay.p, all.p, 32 * G, hipMemcpyDeviceToDevice, st));
   build_layers(t, nl - lg + 1, G, sorted, next, st, fetch_root, rc);
 }
 

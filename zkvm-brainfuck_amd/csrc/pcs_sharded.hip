@@ -103,13 +103,10 @@ PcsShardedResult commit_fri_sharded(const uint32_t* cols, int log_n, int w_local
   for (int rd = 0; len > 2; rd++) {
     const size_t h = len / 2;
     if (local && h < (size_t)G * SHARD_MIN_LEAVES) {  // gather the layer, finish redundantly
-      std::vector<EF> mine(len / G), all(len);
-      HIP_CHECK(hipMemcpyAsync(mine.data(), cur.p, mine.size() * sizeof(EF), hipMemcpyDeviceToHost, st));
+      DBuf<EF> all(len);  // device to device
       HIP_CHECK(hipStreamSynchronize(st));
-      sc->allgather(mine.data(), mine.size() * sizeof(EF), all.data());
-      cur.reset(len);
-      HIP_CHECK(hipMemcpyAsync(cur.p, all.data(), len * sizeof(EF), hipMemcpyHostToDevice, st));
-      HIP_CHECK(hipStreamSynchronize(st));
+      sc->allgather(cur.p, (len / G) * sizeof(EF), all.p);
+      cur = std::move(all);
       local = false;
     }
     const size_t i0 = local ? (size_t)k * (h / G) : 0, cnt = local ? h / G : h;

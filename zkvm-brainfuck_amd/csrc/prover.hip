@@ -697,8 +697,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   }
   size_t nwords = 0;
   const ShardCtx* shard = shard_ctx();
-  uint32_t* words = gather_queries(segs, qidx, nwords, shard ? shard->rank : 0, st);
-  if (shard && shard->world > 1) shard->allreduce_sum_u32(words, nwords);
+  uint32_t* words = gather_queries(segs, qidx, nwords, shard, st);
   if (ev.on) ev.end(e4, st, &tms->fri);
 
   // ---- serialize (BFZ1 normal form)
