@@ -223,6 +223,33 @@ def drop_in_path(pk, prog, stdin, ref_proof, steps=3):
                     f"{nbytes / 1e9:.2f} GB) incl. upload + transpose + proof"}
 
 
+def sharded_latency(dist, pk, rec, rank, world, device, ref_proof, steps=3):
+    """Latency of ONE proof split over all ranks (bfz_record_prove_sharded: every rank hashes
+    its subtree of each large Merkle tree; the subtree roots are all-gathered and the query
+    openings sum-all-reduced over RCCL on device buffers), measured after the replica timing
+    on the same record and checked byte for byte against the single-GPU proof.  Needs one GPU
+    per rank; guarded by a 120 s collective timeout so a failure cannot hang the bench."""
+    import datetime
+    import torch
+    from bfz import _lib as _l, shard as _sh
+    if "BFZ_DEVICE" in os.environ or torch.cuda.device_count() < world:
+        return {"skipped": "ranks share a GPU (RCCL needs one GPU per rank)"}
+    try:
+        torch.cuda.set_device(device)
+        grp = dist.new_group(backend="nccl", timeout=datetime.timedelta(seconds=120))
+        coll = _sh.Collectives(dist, group=grp, device=device)
+        pf = _sh.prove_record_sharded(pk.handle, rec, coll, rank)
+        exact = pf == ref_proof
+        ms = timed_steps(lambda: _sh.prove_record_sharded(pk.handle, rec, coll, rank), steps, dist,
+                         sync=lambda: _l.check(_l.lib().bfz_synchronize()))
+        return {"ms_per_proof": round(ms, 3), "steps": steps, "bit_exact_vs_single_gpu": exact,
+                "ranks": world, "scaling": "strong (one proof over all ranks)",
+                "collectives": "RCCL (torch nccl backend): subtree-root all-gather + query-word "
+                               "all-reduce on HBM buffers"}
+    except Exception as e:  # keep the replica line if the sharded path fails
+        return {"error": f"{type(e).__name__}: {e}"}
+
+
 def timed_steps(step, steps, dist=None, sync=lambda: None):
     """Runs `step` exactly `steps` times between barrier + device synchronize on both sides
     and returns ms per step, the max over ranks (every rank proves its own replica; the
@@ -320,6 +347,8 @@ def main():
     saved_stdout = os.dup(1)
     os.dup2(2, 1)
     if world > 1:
+        # a failed RCCL collective raises after its timeout instead of hanging (sharded_latency)
+        os.environ.setdefault("TORCH_NCCL_BLOCKING_WAIT", "1")
         import torch.distributed as dist
         if sharded:
             import torch
@@ -378,6 +407,9 @@ def main():
     client.verify(sdk.BfProofWithPublicValues(proof=proof, stdin=stdin), vk)
 
     ms = timed_steps(lambda: one(), args.steps, dist, sync=lambda: _lib.check(L.bfz_synchronize()))
+    extra = {}
+    if world > 1 and not sharded and not args.no_extra:  # every rank takes part
+        extra["sharded_proof"] = sharded_latency(dist, pk, rec, rank, world, device, proof)
 
     if rank == 0:
         lde_gbs = tm.lde_bytes / (tm.lde_ms * 1e-3) / 1e9 if tm.lde_ms > 0 else 0.0
@@ -410,6 +442,8 @@ def main():
             "poseidon2": poseidon2_roofline(tm),
             "proof_bytes": len(proof),
         }
+        if world > 1 and not sharded and not args.no_extra and "sharded_proof" in extra:
+            line["sharded_proof"] = extra["sharded_proof"]
         if world == 1 and not args.no_extra:
             line["end_to_end"] = end_to_end(client, pk, prog, stdin)
             line["drop_in_path"] = drop_in_path(pk, prog, stdin, proof)
