@@ -1,0 +1,62 @@
+"""The index and coset algebra of the sharded proof, checked in plain Python.
+
+A rank of a G-way sharded proof holds bit-reversed LDE positions [k m, (k+1) m), m = 2n / G.
+Those are the natural points i = G t + r (r = bitrev_G(k)) of shift * H_2n, i.e. the coset
+a <w_m> with a = shift * w_2n^r, so the shard is a size-m forward DIF (bit-reversed output) of
+the folded coefficients d_u = sum_l c_(u + l m) a^(u + l m) -- what ntt.hip's coset_residue
+computes.  The quotient's next row (i + 2) of every point of a shard lies in the one residue
+class (r + 2) mod G, owned by rank bitrev_G(r + 2 mod G).
+"""
+import random
+
+import pytest
+
+P = 0x7F000001
+
+
+def _gen(bits):
+    return pow(pow(3, 127, P), 1 << (24 - bits), P)
+
+
+def _brev(x, b):
+    return int(format(x, f"0{b}b")[::-1], 2) if b else 0
+
+
+@pytest.mark.parametrize("logn", [4, 5, 6])
+def test_residue_shards_are_the_bitreversed_coset_lde(logn):
+    rng = random.Random(logn)
+    n = 1 << logn
+    c = [rng.randrange(P) for _ in range(n)]
+    shift = 3
+    w2n = _gen(logn + 1)
+    lde = [0] * (2 * n)
+    for i in range(2 * n):
+        x = shift * pow(w2n, i, P) % P
+        lde[_brev(i, logn + 1)] = sum(cj * pow(x, j, P) for j, cj in enumerate(c)) % P
+    for lg in (1, 2, 3):
+        G = 1 << lg
+        m = 2 * n // G
+        zeta = _gen(logn + 1 - lg)
+        for k in range(G):
+            r = _brev(k, lg)
+            a = shift * pow(w2n, r, P) % P
+            d = [sum(c[j] * pow(a, j, P) for j in range(u, n, m)) % P for u in range(m)]
+            shard = [sum(d[u] * pow(zeta, u * _brev(t, logn + 1 - lg), P) for u in range(m)) % P
+                     for t in range(m)]
+            assert shard == lde[k * m:(k + 1) * m]
+            k2 = _brev((r + 2) % G, lg)
+            for t in range(m):
+                i = _brev(k * m + t, logn + 1)
+                assert _brev((i + 2) % (2 * n), logn + 1) // m == k2
+
+
+def test_coefficient_slices_sum_to_the_opening():
+    """sum over ranks of the slice sum_(j in [k n/G, (k+1) n/G)) c_j z^j is p(z)."""
+    rng = random.Random(7)
+    n, G = 64, 4
+    c = [rng.randrange(P) for _ in range(n)]
+    z = rng.randrange(P)
+    full = sum(cj * pow(z, j, P) for j, cj in enumerate(c)) % P
+    parts = [sum(c[j] * pow(z, j, P) for j in range(k * n // G, (k + 1) * n // G)) % P
+             for k in range(G)]
+    assert sum(parts) % P == full

@@ -26,6 +26,16 @@ struct GrindState {        // DuplexChallenger state at grind time
 
 // out[t] = 1 / (x_t - z), x_t = 3 * w_H^bitrev(t), t < 2^logH
 void inv_denoms(const kb::EF& z, int logH, kb::EF* out, hipStream_t st);
+// out[t - t0] = 1 / (x_t - z) for the positions t in [t0, t0 + count) of an LDE of height 2^logH
+void inv_denoms_range(const kb::EF& z, int logH, size_t t0, size_t count, kb::EF* out,
+                      hipStream_t st);
+// out[t] = z^(j0 + t), t < count
+void pow_table(const kb::EF& z, size_t j0, size_t count, kb::EF* out, hipStream_t st);
+// Coefficient-form opening (sharded proofs): out[c] = scale * sum_(t < count) coef[c * col_stride
+// + t] tab[t] for each point (tab = powers of the point from the range's first exponent).
+void open_coefficients(const uint32_t* coef, size_t col_stride, int w, size_t count,
+                       const kb::EF* tab_a, const kb::EF& scale_a, kb::EF* out_a,
+                       const kb::EF* tab_b, const kb::EF& scale_b, kb::EF* out_b, hipStream_t st);
 // out_dev[c] = value at z of column c of a committed LDE (height = 2n), via the low coset.
 void open_matrix(const uint32_t* mat, size_t height, int w, const kb::EF* invd_a,
                  const kb::EF& scale_a, kb::EF* out_a, const kb::EF* invd_b,
@@ -35,6 +45,10 @@ void open_matrix(const uint32_t* mat, size_t height, int w, const kb::EF* invd_a
 void reduce_height(const RedCol* cols, const RedMat* mats, int nmats, size_t H,
                    const kb::EF* invd_a, const kb::EF* invd_b, const kb::EF& ya, const kb::EF& yb,
                    bool has_b, kb::EF* ro, hipStream_t st);
+// The same over the positions [t0, t0 + count) only; pointers indexed by the global position.
+void reduce_range(const RedCol* cols, const RedMat* mats, int nmats, size_t t0, size_t count,
+                  const kb::EF* invd_a, const kb::EF* invd_b, const kb::EF& ya, const kb::EF& yb,
+                  bool has_b, kb::EF* ro, hipStream_t st);
 void fri_fold(const kb::EF* in, kb::EF* out, size_t h, const kb::EF& beta, const kb::EF* add,
               hipStream_t st);
 uint32_t grind(const GrindState& gs, int bits, hipStream_t st);

@@ -27,18 +27,19 @@ __device__ __forceinline__ uint32_t coset_point(uint32_t t, int logH, const uint
 
 constexpr int INV_CHUNK = 8;
 
-__global__ __launch_bounds__(256) void k_inv_denoms(EF z, int logH, const uint32_t* __restrict__ twf,
+// out[t - t0] = 1 / (x_t - z) for t in [t0, t0 + count)
+__global__ __launch_bounds__(256) void k_inv_denoms(EF z, int logH, size_t t0, size_t count,
+                                                    const uint32_t* __restrict__ twf,
                                                     EF* __restrict__ out) {
-  const size_t H = (size_t)1 << logH;
   const size_t base = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * INV_CHUNK;
-  if (base >= H) return;
+  if (base >= count) return;
   EF d[INV_CHUNK], pre[INV_CHUNK];
-  const int cnt = (int)min((size_t)INV_CHUNK, H - base);
+  const int cnt = (int)min((size_t)INV_CHUNK, count - base);
   EF run = ef_one();
 #pragma unroll
   for (int k = 0; k < INV_CHUNK; k++) {
     if (k < cnt) {
-      d[k] = ef_sub(ef_base(coset_point((uint32_t)(base + k), logH, twf)), z);
+      d[k] = ef_sub(ef_base(coset_point((uint32_t)(t0 + base + k), logH, twf)), z);
       run = ef_mul(run, d[k]);
     }
     pre[k] = run;
@@ -78,7 +79,10 @@ __device__ __forceinline__ uint32_t row_sum16(uint32_t v) {
 // matrix element is read once for both points.  Per column the lane sums go through the
 // 16-lane DPP rows only; the 16 row sums of the block meet in LDS once per OPEN_CB columns.
 // Loads run two columns ahead (16 per thread in flight) to cover HBM latency.
-template <int NP>
+// TAB = false: barycentric weights W_k,t = -x_t invd_k[t] over the low coset (mat = the LDE).
+// TAB = true: W_k,t = invd_k[t] read as a weight table (coefficient form: mat = a range of
+// coefficients, the table = powers of the point), logH/twf unused.
+template <int NP, bool TAB = false>
 __global__ __launch_bounds__(OPEN_T) void k_open_partial(const uint32_t* __restrict__ mat,
                                                          size_t height, int w, size_t n, int logH,
                                                          const EF* __restrict__ invd_a,
@@ -93,6 +97,11 @@ __global__ __launch_bounds__(OPEN_T) void k_open_partial(const uint32_t* __restr
 #pragma unroll
   for (int r = 0; r < OPEN_R; r++) {
     const size_t t = c0 + (size_t)r * OPEN_T;
+    if (TAB) {
+#pragma unroll
+      for (int k = 0; k < NP; k++) W[k][r] = r < nr ? (k ? invd_b : invd_a)[t] : ef_zero();
+      continue;
+    }
     const uint32_t x = r < nr ? coset_point((uint32_t)t, logH, twf) : 0u;
 #pragma unroll
     for (int k = 0; k < NP; k++)
@@ -172,12 +181,13 @@ __global__ __launch_bounds__(256) void k_open_final(const EF* __restrict__ parti
 }
 
 // ------------------------------------------------------------------ reduced openings
+// Positions [t0, t1) (a shard's range; every pointer indexed by the global position).
 __global__ __launch_bounds__(256) void k_reduce(const RedCol* __restrict__ cols,
                                                 const RedMat* __restrict__ mats, int nmats,
-                                                size_t H, const EF* __restrict__ invd_a,
+                                                size_t t0, size_t t1, const EF* __restrict__ invd_a,
                                                 const EF* __restrict__ invd_b, EF ya, EF yb,
                                                 int has_b, EF* __restrict__ ro) {
-  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < H;
+  for (size_t t = t0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < t1;
        t += (size_t)gridDim.x * blockDim.x) {
     EF sa = ef_zero(), sb = ef_zero();
     for (int m = 0; m < nmats; m++) {
@@ -209,6 +219,19 @@ __global__ __launch_bounds__(256) void k_reduce(const RedCol* __restrict__ cols,
     EF r = ef_mul(ef_sub(sa, ya), invd_a[t]);
     if (has_b) r = ef_add(r, ef_mul(ef_sub(sb, yb), invd_b[t]));
     ro[t] = r;  // one launch covers every matrix of the height
+  }
+}
+
+// out[t] = z^(j0 + t), t < count (eight consecutive powers per thread)
+__global__ __launch_bounds__(256) void k_pow_table(EF z, size_t j0, size_t count,
+                                                   EF* __restrict__ out) {
+  const size_t b = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (b >= count) return;
+  EF p = ef_pow(z, j0 + b);
+  const int cnt = (int)min((size_t)8, count - b);
+  for (int k = 0; k < cnt; k++) {
+    out[b + k] = p;
+    p = ef_mul(p, z);
   }
 }
 
@@ -306,11 +329,42 @@ __global__ __launch_bounds__(256) void k_gather_segs(const GatherSeg* __restrict
 
 // ================================================================== host wrappers
 void inv_denoms(const EF& z, int logH, EF* out, hipStream_t st) {
+  inv_denoms_range(z, logH, 0, (size_t)1 << logH, out, st);
+}
+
+void inv_denoms_range(const EF& z, int logH, size_t t0, size_t count, EF* out, hipStream_t st) {
   twiddles().ensure(std::max(logH, 1));
-  const size_t H = (size_t)1 << logH;
-  const size_t nthreads = (H + INV_CHUNK - 1) / INV_CHUNK;
-  hipLaunchKernelGGL(k_inv_denoms, dim3(ceil_div(nthreads, 256)), dim3(256), 0, st, z, logH,
-                     (const uint32_t*)twiddles().fwd.p, out);
+  const size_t nthreads = (count + INV_CHUNK - 1) / INV_CHUNK;
+  hipLaunchKernelGGL(k_inv_denoms, dim3(ceil_div(nthreads, 256)), dim3(256), 0, st, z, logH, t0,
+                     count, (const uint32_t*)twiddles().fwd.p, out);
+  KCHECK();
+}
+
+void pow_table(const EF& z, size_t j0, size_t count, EF* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_pow_table, dim3(ceil_div(ceil_div(count, 8), 256)), dim3(256), 0, st, z, j0,
+                     count, out);
+  KCHECK();
+}
+
+void open_coefficients(const uint32_t* coef, size_t col_stride, int w, size_t count,
+                       const EF* tab_a, const EF& scale_a, EF* out_a, const EF* tab_b,
+                       const EF& scale_b, EF* out_b, hipStream_t st) {
+  const int nchunks = (int)ceil_div(count, OPEN_CH);
+  const int np = tab_b ? 2 : 1;
+  DBuf<EF> partial((size_t)nchunks * w * np);
+  if (np == 2) {
+    hipLaunchKernelGGL((k_open_partial<2, true>), dim3(nchunks), dim3(OPEN_T), 0, st, coef,
+                       col_stride, w, count, 0, tab_a, tab_b, nullptr, partial.p);
+    KCHECK();
+    hipLaunchKernelGGL(k_open_final<2>, dim3(w), dim3(256), 0, st, (const EF*)partial.p, nchunks,
+                       w, scale_a, scale_b, out_a, out_b);
+  } else {
+    hipLaunchKernelGGL((k_open_partial<1, true>), dim3(nchunks), dim3(OPEN_T), 0, st, coef,
+                       col_stride, w, count, 0, tab_a, tab_a, nullptr, partial.p);
+    KCHECK();
+    hipLaunchKernelGGL(k_open_final<1>, dim3(w), dim3(256), 0, st, (const EF*)partial.p, nchunks,
+                       w, scale_a, scale_a, out_a, out_a);
+  }
   KCHECK();
 }
 
@@ -341,9 +395,15 @@ void open_matrix(const uint32_t* mat, size_t height, int w, const EF* invd_a, co
 void reduce_height(const RedCol* cols, const RedMat* mats, int nmats, size_t H, const EF* invd_a,
                    const EF* invd_b, const EF& ya, const EF& yb, bool has_b, EF* ro,
                    hipStream_t st) {
-  const unsigned grid = std::min<unsigned>(ceil_div(H, 256), 8192);
-  hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(256), 0, st, cols, mats, nmats, H, invd_a, invd_b,
-                     ya, yb, has_b ? 1 : 0, ro);
+  reduce_range(cols, mats, nmats, 0, H, invd_a, invd_b, ya, yb, has_b, ro, st);
+}
+
+void reduce_range(const RedCol* cols, const RedMat* mats, int nmats, size_t t0, size_t count,
+                  const EF* invd_a, const EF* invd_b, const EF& ya, const EF& yb, bool has_b,
+                  EF* ro, hipStream_t st) {
+  const unsigned grid = std::min<unsigned>(ceil_div(count, 256), 8192);
+  hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(256), 0, st, cols, mats, nmats, t0, t0 + count,
+                     invd_a, invd_b, ya, yb, has_b ? 1 : 0, ro);
   KCHECK();
 }
 

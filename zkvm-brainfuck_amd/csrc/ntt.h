@@ -22,6 +22,15 @@ void ntt_passes(const uint32_t* src, uint32_t* dst, size_t src_stride, size_t ds
 void coset_lde(const uint32_t* evals, size_t n, int w, uint32_t shift, uint32_t* lde,
                hipStream_t st);
 
+// Sharded LDE.  lde_coefficients: coef = n * (coefficients of the interpolant
+// over H_n), natural order (the iDFT alone).  coset_residue: the rank shard of the coset LDE
+// on shift * H_2n for G = 2^logG ranks and residue r = bitrev_G(rank): bit-reversed positions
+// [rank m, (rank+1) m), m = 2n / G, column-major (m x w) -- word-for-word the same rows as
+// coset_lde's.
+void lde_coefficients(const uint32_t* evals, size_t n, int w, uint32_t* coef, hipStream_t st);
+void coset_residue(const uint32_t* coef, size_t n, int w, uint32_t shift, int logG, int r,
+                   uint32_t* out, hipStream_t st);
+
 // Row-major natural-order host layout -> column-major bit-reversed device layout.
 void transpose_bitrev(const uint32_t* rowmajor, size_t n, int w, uint32_t* colmajor,
                       hipStream_t st);

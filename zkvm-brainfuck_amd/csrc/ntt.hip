@@ -702,6 +702,68 @@ void coset_lde(const uint32_t* evals, size_t n, int w, uint32_t shift, uint32_t*
   // coef goes back to the pool here; every consumer is ordered on the same stream.
 }
 
+// ---------------------------------------------------------------- residue-class shards
+// A row shard of a sharded proof: rank k holds bit-reversed LDE positions
+// [k m, (k+1) m), m = 2n / G, i.e. the natural points i = G t + r (r = bitrev_G(k)), which
+// form the coset a <w_m> with a = shift w_2n^r.  With the coefficients c_j of the trace
+// interpolant,  p(a w_m^t) = sum_(u < m) w_m^(u t) d_u,  d_u = sum_l c_(u + l m) a^(u + l m),
+// so the shard is a size-m forward DIF of d (natural in -> bit-reversed out, exactly the shard's
+// position order): no exchange between ranks, the iDFT is the only full-size transform.
+
+// d[u] = sum_(l < n/m) coef[u + l m] a^(u + l m) / n  (coef = n c: the iDFT leaves 1/n out;
+// a^j / n = A[j & mask] * AH[j >> B] with the 1/n folded into AH)
+__global__ __launch_bounds__(256) void k_fold_residue(const uint32_t* __restrict__ coef, size_t n,
+                                                      uint32_t* __restrict__ out, size_t m, int B,
+                                                      const uint32_t* __restrict__ pw) {
+  const uint32_t* c = coef + (size_t)blockIdx.y * n;
+  uint32_t* o = out + (size_t)blockIdx.y * m;
+  const size_t mask = ((size_t)1 << B) - 1, nb = mask + 1;
+  for (size_t u = (size_t)blockIdx.x * blockDim.x + threadIdx.x; u < m;
+       u += (size_t)gridDim.x * blockDim.x) {
+    uint32_t acc = 0;
+    for (size_t j = u; j < n; j += m) acc = madd(acc, mmul(c[j], mmul(pw[j & mask], pw[nb + (j >> B)])));
+    o[u] = acc;
+  }
+}
+
+// Two-level power table of a (with 1/2^L folded into the high half), cached per (a, L).
+static const uint32_t* residue_powers(uint32_t a, int L, int B) {
+  static auto* cache = new std::map<std::pair<uint32_t, int>, DBuf<uint32_t>>();
+  auto it = cache->find({a, L});
+  if (it != cache->end()) return it->second.p;
+  const size_t nb = (size_t)1 << B;
+  std::vector<uint32_t> h(2 * nb);
+  uint32_t x = ONE;
+  for (size_t k = 0; k < nb; k++) { h[k] = x; x = mmul(x, a); }
+  const uint32_t step = x;  // a^(2^B)
+  uint32_t y = minv(to_mont((uint32_t)(((uint64_t)1 << L) % P)));
+  for (size_t k = 0; k < nb; k++) { h[nb + k] = y; y = mmul(y, step); }
+  DBuf<uint32_t> d(2 * nb);
+  HIP_CHECK(hipMemcpyAsync(d.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, stream()));
+  HIP_CHECK(hipStreamSynchronize(stream()));
+  const uint32_t* p = d.p;
+  cache->emplace(std::make_pair(a, L), std::move(d));
+  return p;
+}
+
+void lde_coefficients(const uint32_t* evals, size_t n, int w, uint32_t* coef, hipStream_t st) {
+  ntt_passes(evals, coef, n, n, w, log2i(n), /*dif=*/false, st);
+}
+
+void coset_residue(const uint32_t* coef, size_t n, int w, uint32_t shift, int logG, int r,
+                   uint32_t* out, hipStream_t st) {
+  const int L = log2i(n);
+  if (logG < 1 || logG > L + 1) throw std::runtime_error("coset_residue: bad shard count");
+  const size_t m = (2 * n) >> logG;
+  const uint32_t a = mmul(shift, mpow(two_adic_gen(L + 1), (uint64_t)r));
+  const int B = (L + 1) / 2;
+  const uint32_t* pw = residue_powers(a, L, B);
+  const dim3 grid(std::min<unsigned>(ceil_div(m, 256), 2048), w);
+  hipLaunchKernelGGL(k_fold_residue, grid, dim3(256), 0, st, coef, n, out, m, B, pw);
+  KCHECK();
+  ntt_passes(out, out, m, m, w, log2i(m), /*dif=*/true, st);
+}
+
 void transpose_to_rowmajor(const uint32_t* colmajor, size_t H, int w, uint32_t* rowmajor,
                            hipStream_t st) {
   hipLaunchKernelGGL(k_transpose_rowmajor, dim3(ceil_div(H * (size_t)w, 256)), dim3(256), 0, st,

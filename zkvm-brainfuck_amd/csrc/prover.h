@@ -34,10 +34,22 @@ struct Challenger {
 };
 
 struct CMat {               // a committed matrix: LDE on 3*H_2n (bit-reversed, column-major)
-  DevMatrix lde;
+  DevMatrix lde;            // lde.height = 2n always; a sharded matrix's buffer holds blk rows
   size_t n = 0;             // trace-domain size
   int log_n = 0;
   uint32_t shift = 0;       // trace-domain shift (Montgomery)
+  // Sharded proofs: this rank's positions [row0, row0 + blk) of the LDE (its
+  // residue class of natural rows), the interpolant's coefficients (n c_j, natural order, for
+  // the coefficient-form opening) and, for G >= 4, the shard of the residue class the quotient's
+  // next rows (i + 2) fall in, at positions [nxt_row0, nxt_row0 + blk).
+  bool sharded = false;
+  size_t blk = 0, row0 = 0, nxt_row0 = 0;
+  DBuf<uint32_t> coef, nxt;
+  // column c, global position t  ->  rows()[c * stride() + t]
+  const uint32_t* rows() const { return sharded ? lde.buf.p - row0 : lde.buf.p; }
+  size_t stride() const { return sharded ? blk : lde.height; }
+  const uint32_t* next_rows() const { return sharded && nxt.p ? nxt.p - nxt_row0 : rows(); }
+  MatRef ref() const { return MatRef{rows(), lde.height, lde.width, stride()}; }
 };
 
 struct Round {

@@ -164,19 +164,68 @@ struct Writer {  // appends into a buffer sized up front (reserve): a memcpy per
 
 void Round::commit(hipStream_t st) {
   std::vector<MatRef> refs;
-  for (CMat& m : mats) refs.push_back({m.lde.buf.p, m.lde.height, m.lde.width});
+  for (CMat& m : mats) refs.push_back(m.ref());
   merkle_build(refs, tree, st);
 }
 
+namespace {
+// How one proof is split over the ranks of a shard context.  Rank k owns the
+// bit-reversed positions [k H/G, (k+1) H/G) of every vector of height H >= G * 1024 (LDEs,
+// Merkle layers, reduced openings, FRI layers): the natural rows i = r (mod G), r = bitrev_G(k).
+// Shorter vectors are replicated.
+struct Plan {
+  int G = 1, lg = 0, k = 0, r = 0;
+  int r2 = 0, k2 = 0;  // residue class of the quotient's next rows (i + 2) and its owner
+  bool on() const { return G > 1; }
+  bool sharded(size_t H) const { return G > 1 && H >= (size_t)G * SHARD_MIN_LEAVES; }
+  size_t blk(size_t H) const { return H >> lg; }
+  size_t row0(size_t H) const { return (size_t)k * blk(H); }
+};
+Plan make_plan() {
+  Plan p;
+  const ShardCtx* c = shard_ctx();
+  if (!c || c->world <= 1) return p;
+  p.G = c->world;
+  p.lg = log2i((size_t)p.G);
+  p.k = c->rank;
+  p.r = (int)bitrev32((uint32_t)p.k, p.lg);
+  p.r2 = (p.r + 2) % p.G;
+  p.k2 = (int)bitrev32((uint32_t)p.r2, p.lg);
+  return p;
+}
+}  // namespace
+
+// plan != nullptr and a height it shards: this rank's residue-class shard of the LDE (plus the
+// next-row shard when want_next and G >= 4) from the interpolant's coefficients, kept in cm.coef.
 static void lde_into(CMat& cm, const uint32_t* evals, size_t n, int w, uint32_t domain_shift,
-                     hipStream_t st, EvTimer* tm, StageTimes* times) {
+                     hipStream_t st, EvTimer* tm, StageTimes* times, const Plan* plan = nullptr,
+                     bool want_next = false) {
   cm.n = n;
   cm.log_n = log2i(n);
   cm.shift = domain_shift;
   cm.lde.height = 2 * n;
   cm.lde.width = w;
-  cm.lde.buf.reset(2 * n * (size_t)w);
   const uint32_t lde_shift = mmul(to_mont(3), minv(domain_shift));  // GENERATOR / shift
+  cm.sharded = plan && plan->sharded(2 * n);
+  cm.nxt.free();
+  cm.coef.free();
+  if (cm.sharded) {
+    cm.blk = plan->blk(2 * n);
+    cm.row0 = plan->row0(2 * n);
+    cm.coef.reset(n * (size_t)w);
+    cm.lde.buf.reset(cm.blk * (size_t)w);
+    lde_coefficients(evals, n, w, cm.coef.p, st);
+    coset_residue(cm.coef.p, n, w, lde_shift, plan->lg, plan->r, cm.lde.buf.p, st);
+    if (want_next && plan->G >= 4) {
+      cm.nxt_row0 = (size_t)plan->k2 * cm.blk;
+      cm.nxt.reset(cm.blk * (size_t)w);
+      coset_residue(cm.coef.p, n, w, lde_shift, plan->lg, plan->r2, cm.nxt.p, st);
+    }
+    return;
+  }
+  cm.blk = 2 * n;
+  cm.row0 = 0;
+  cm.lde.buf.reset(2 * n * (size_t)w);
   hipEvent_t b = nullptr;
   if (tm && tm->on) b = tm->begin(st);
   coset_lde(evals, n, w, lde_shift, cm.lde.buf.p, st);
@@ -319,17 +368,55 @@ void commit_main_impl(MainData& md, ProofScope& ps) {
     md.hn[k] = dt.heights[md.order[k]];
   }
   hipEvent_t e0 = ps.ev.on ? ps.ev.begin(st) : nullptr;
+  const Plan plan = make_plan();
   md.mainr = Round();
   md.mainr.mats.resize(nc);
   for (int k = 0; k < nc; k++)
     lde_into(md.mainr.mats[k], dt.evals[md.order[k]].p, md.hn[k], CHIP_INFO[md.chip[k]].main_w, ONE,
-             st, &ps.ev, ps.tms);
+             st, &ps.ev, ps.tms, &plan, /*want_next=*/true);
   md.mainr.commit(st);
   if (ps.ev.on) ps.ev.end(e0, st, &ps.tms->main_commit);
 }
 
 std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch,
                                const ProveOptions& opt, ProofScope& ps);
+
+// Sharded chips' quotient values: rank j computed LDE positions [j b, (j+1) b) (b = 2n / G),
+// which land in chunk (j b) / n at rows [(j b) mod n, + b) of its 4 columns.  One all-gather of
+// every sharded chip's part completes qv on every rank (the chunk LDEs need whole columns).
+void gather_quotients(const Round& mainr, const std::vector<size_t>& hn,
+                      std::vector<DBuf<uint32_t>>& qv, const Plan& plan, const ShardCtx& sc,
+                      hipStream_t st) {
+  const int nc = (int)hn.size();
+  std::vector<size_t> off(nc, 0);
+  size_t total = 0;
+  for (int k = 0; k < nc; k++)
+    if (mainr.mats[k].sharded) {
+      off[k] = total;
+      total += 4 * plan.blk(2 * hn[k]);
+    }
+  if (!total) return;
+  auto part = [&](int k, int rank) {  // first word of rank's part (chunk column 0) in qv[k]
+    const size_t n = hn[k], b = plan.blk(2 * n), t0 = (size_t)rank * b;
+    return qv[k].p + (t0 / n) * 4 * n + (t0 % n);
+  };
+  DBuf<uint32_t> send(total), recv(total * plan.G);
+  for (int k = 0; k < nc; k++)
+    if (mainr.mats[k].sharded) {
+      const size_t n = hn[k], b = plan.blk(2 * n);
+      HIP_CHECK(hipMemcpy2DAsync(send.p + off[k], b * 4, part(k, plan.k), n * 4, b * 4, 4,
+                                 hipMemcpyDeviceToDevice, st));
+    }
+  HIP_CHECK(hipStreamSynchronize(st));
+  sc.allgather(send.p, total * 4, recv.p);
+  for (int j = 0; j < plan.G; j++)
+    for (int k = 0; k < nc; k++)
+      if (mainr.mats[k].sharded && j != plan.k) {
+        const size_t n = hn[k], b = plan.blk(2 * n);
+        HIP_CHECK(hipMemcpy2DAsync(part(k, j), n * 4, recv.p + (size_t)j * total + off[k], b * 4,
+                                   b * 4, 4, hipMemcpyDeviceToDevice, st));
+      }
+}
 }  // namespace
 
 void commit_main(MainData& md) {
@@ -377,8 +464,10 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   const std::vector<int>& order = md.order;
   const std::vector<int>& chip = md.chip;
   const std::vector<size_t>& hn = md.hn;
-  const Round& mainr = md.mainr;
+  Round& mainr = md.mainr;
   const int nc = (int)chip.size();
+  const Plan plan = make_plan();
+  const ShardCtx* shard = shard_ctx();
 
   // ---- open (prover.rs:242-553), on a clone of the challenger (prover.rs:578)
   ch.observe_digest(mainr.tree.root);
@@ -400,7 +489,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     const int pi = pk.idx_of_chip[c];
     const uint32_t* prep = pi >= 0 ? pk.prep_evals[pi].p : nullptr;
     perm_trace(c, dt.evals[order[k]].p, prep, hn[k], pc, pe.p, cums_d.p + k, st);
-    lde_into(permr.mats[k], pe.p, hn[k], 4 * pw, ONE, st, &ev, tms);
+    lde_into(permr.mats[k], pe.p, hn[k], 4 * pw, ONE, st, &ev, tms, &plan, /*want_next=*/true);
   }
   permr.commit(st);
   std::vector<EF> cums(nc);
@@ -416,6 +505,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   Round quotr;
   quotr.mats.resize(2 * nc);
   std::vector<DBuf<EF>> apows(nc);
+  std::vector<DBuf<uint32_t>> qv(nc);  // Q on 3 H_2n: 2 chunks x 4 columns of n rows
   for (int k = 0; k < nc; k++) {
     const int c = chip[k];
     const size_t n = hn[k];
@@ -445,14 +535,32 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     qp.shift = three;
     const int pi = pk.idx_of_chip[c];
     const uint32_t* prep_lde = pi >= 0 ? pk.prep.mats[pi].lde.buf.p : nullptr;
-    DBuf<uint32_t> q(8 * n);
-    quotient(c, mainr.mats[k].lde.buf.p, prep_lde, permr.mats[k].lde.buf.p, logn + 1, qp, q.p, st);
-    const uint32_t w2n = two_adic_gen(logn + 1);
-    for (int cc = 0; cc < 2; cc++) {
-      const uint32_t dshift = mmul(three, cc ? w2n : ONE);  // split_domains: shift * g^cc
-      lde_into(quotr.mats[2 * k + cc], q.p + (size_t)4 * cc * n, n, 4, dshift, st, &ev, tms);
+    qv[k].reset(8 * n);
+    const CMat& mm = mainr.mats[k];
+    const CMat& pm = permr.mats[k];
+    if (mm.sharded) {  // this rank's points only; next rows from the next-residue shards
+      const QuotRows in{mm.rows(), mm.next_rows(), pm.rows(), pm.next_rows(), prep_lde,
+                        mm.stride(), mm.row0, mm.blk};
+      quotient_rows(c, in, logn + 1, qp, qv[k].p, st);
+    } else {
+      quotient(c, mm.lde.buf.p, prep_lde, pm.lde.buf.p, logn + 1, qp, qv[k].p, st);
     }
   }
+  if (plan.on()) gather_quotients(mainr, hn, qv, plan, *shard, st);
+  for (int k = 0; k < nc; k++) {  // the next-row shards are done with
+    mainr.mats[k].nxt.free();
+    permr.mats[k].nxt.free();
+  }
+  for (int k = 0; k < nc; k++) {
+    const size_t n = hn[k];
+    const uint32_t w2n = two_adic_gen(log2i(n) + 1);
+    for (int cc = 0; cc < 2; cc++) {
+      const uint32_t dshift = mmul(to_mont(3), cc ? w2n : ONE);  // split_domains: shift * g^cc
+      lde_into(quotr.mats[2 * k + cc], qv[k].p + (size_t)4 * cc * n, n, 4, dshift, st, &ev, tms,
+               &plan);
+    }
+  }
+  qv.clear();
   quotr.commit(st);
   if (ev.on) ev.end(e2, st, &tms->quotient);
   ch.observe_digest(quotr.tree.root);
@@ -488,24 +596,93 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
       Lmax = std::max(Lmax, m.log_n + LOG_BLOWUP);
     }
   }
-  DBuf<EF> invd_zeta((size_t)1 << Lmax);
-  inv_denoms(zeta, Lmax, invd_zeta.p, st);
-  std::map<int, DBuf<EF>> invd_next;  // by LDE log height
+  // Inverse denominators 1 / (x_t - point), indexed by global LDE position.  Unsharded: one
+  // table over the tallest height for zeta (smaller heights read its prefix) and one per height
+  // for the second point.  Sharded: per height, the rank's range where the height is sharded
+  // and the whole height where it is replicated.
+  // A replicated matrix at a sharded height (the preprocessed ones) is opened over its whole
+  // low coset: that height also gets full tables (fa, fb).
+  struct Invd {
+    DBuf<EF> a, b, fa, fb;
+    size_t t0 = 0;
+    const EF* pa() const { return a.p - t0; }
+    const EF* pb() const { return b.p ? b.p - t0 : nullptr; }
+    const EF* full_a() const { return fa.p ? fa.p : a.p; }  // a is full where fa is absent
+    const EF* full_b() const { return fa.p ? fb.p : b.p; }
+  };
+  std::map<int, bool> two_at;  // LDE log heights present -> some matrix opened at two points
+  std::map<int, bool> rep_at;  // ... -> a replicated matrix is opened at that height
   for (int r = 0; r < 4; r++)
     for (size_t i = 0; i < rounds[r]->mats.size(); i++) {
-      const CMat& m = rounds[r]->mats[i];
-      const int lh = m.log_n + LOG_BLOWUP;
-      if (mp[r][i].npts == 2 && !invd_next.count(lh)) {
-        DBuf<EF> d((size_t)1 << lh);
-        inv_denoms(mp[r][i].pts[1], lh, d.p, st);
-        invd_next.emplace(lh, std::move(d));
+      const int lh = rounds[r]->mats[i].log_n + LOG_BLOWUP;
+      two_at[lh] |= mp[r][i].npts == 2;
+      rep_at[lh] |= !rounds[r]->mats[i].sharded;
+    }
+  DBuf<EF> invd_zeta;
+  if (!plan.on()) {
+    invd_zeta.reset((size_t)1 << Lmax);
+    inv_denoms(zeta, Lmax, invd_zeta.p, st);
+  }
+  std::map<int, Invd> invd;
+  for (const auto& [lh, two] : two_at) {
+    const size_t H = (size_t)1 << lh;
+    const bool sh = plan.sharded(H);
+    const size_t t0 = sh ? plan.row0(H) : 0, cnt = sh ? plan.blk(H) : H;
+    Invd& d = invd[lh];
+    d.t0 = t0;
+    if (plan.on()) {
+      d.a.reset(cnt);
+      inv_denoms_range(zeta, lh, t0, cnt, d.a.p, st);
+    } else {
+      d.a = DBuf<EF>::borrow(invd_zeta.p, H);
+    }
+    const EF znext = ef_mul_base(zeta, two_adic_gen(lh - LOG_BLOWUP));
+    if (two) {
+      d.b.reset(cnt);
+      inv_denoms_range(znext, lh, t0, cnt, d.b.p, st);
+    }
+    if (sh && rep_at[lh]) {  // the low coset only: positions [0, H / 2)
+      d.fa.reset(H / 2);
+      inv_denoms_range(zeta, lh, 0, H / 2, d.fa.p, st);
+      if (two) {
+        d.fb.reset(H / 2);
+        inv_denoms_range(znext, lh, 0, H / 2, d.fb.p, st);
       }
     }
+  }
+  // Opened values.  Replicated matrices: barycentric over the low coset of the LDE.  Sharded
+  // matrices: the rank's 1/G slice of sum_j c_j (z / s)^j (s = the trace domain's shift) from
+  // the kept coefficients; the slices are summed across ranks below.
   DBuf<EF> opened_d(nvals);
+  std::map<std::array<uint32_t, 5>, DBuf<EF>> ptabs;  // (point, log n) -> powers on the range
+  auto ptable = [&](const EF& z, int log_n, size_t j0, size_t len) {
+    const std::array<uint32_t, 5> key{z.c[0], z.c[1], z.c[2], z.c[3], (uint32_t)log_n};
+    auto it = ptabs.find(key);
+    if (it != ptabs.end()) return (const EF*)it->second.p;
+    DBuf<EF> t(len);
+    pow_table(z, j0, len, t.p, st);
+    const EF* p = t.p;
+    ptabs.emplace(key, std::move(t));
+    return p;
+  };
   for (int r = 0; r < 4; r++)
     for (size_t i = 0; i < rounds[r]->mats.size(); i++) {
       const CMat& m = rounds[r]->mats[i];
       const int lh = m.log_n + LOG_BLOWUP;
+      const bool two = mp[r][i].npts == 2;
+      EF* out_a = opened_d.p + mp[r][i].off[0];
+      EF* out_b = two ? opened_d.p + mp[r][i].off[1] : nullptr;
+      if (m.sharded) {
+        const size_t len = m.n >> plan.lg, j0 = (size_t)plan.k * len;
+        const uint32_t sinv = minv(m.shift);
+        const EF* tab[2] = {nullptr, nullptr};
+        for (int j = 0; j < mp[r][i].npts; j++)
+          tab[j] = ptable(ef_mul_base(mp[r][i].pts[j], sinv), m.log_n, j0, len);
+        const EF ninv = ef_base(minv(to_mont((uint32_t)(m.n % P))));
+        open_coefficients(m.coef.p + j0, m.n, m.lde.width, len, tab[0], ninv, out_a, tab[1], ninv,
+                          out_b, st);
+        continue;
+      }
       const EF three_n = ef_base(mpow(to_mont(3), m.n));
       const uint32_t n_f = to_mont((uint32_t)(m.n % P));
       EF scale[2];
@@ -513,14 +690,36 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
         const EF zn = ef_pow(mp[r][i].pts[j], m.n);
         scale[j] = ef_mul(ef_sub(zn, three_n), ef_inv(ef_mul_base(three_n, n_f)));
       }
-      const bool two = mp[r][i].npts == 2;
-      open_matrix(m.lde.buf.p, m.lde.height, m.lde.width, invd_zeta.p, scale[0],
-                  opened_d.p + mp[r][i].off[0], two ? invd_next.at(lh).p : nullptr,
-                  two ? scale[1] : scale[0], two ? opened_d.p + mp[r][i].off[1] : nullptr, st);
+      const Invd& d = invd.at(lh);
+      open_matrix(m.lde.buf.p, m.lde.height, m.lde.width, d.full_a(), scale[0], out_a,
+                  two ? d.full_b() : nullptr, two ? scale[1] : scale[0], out_b, st);
     }
   std::vector<EF> opened(nvals);
-  HIP_CHECK(hipMemcpyAsync(opened.data(), opened_d.p, nvals * sizeof(EF), hipMemcpyDeviceToHost, st));
-  HIP_CHECK(hipStreamSynchronize(st));
+  if (plan.on()) {  // one all-gather; sharded matrices' slices summed, replicated ones kept
+    DBuf<EF> all(nvals * plan.G);
+    HIP_CHECK(hipStreamSynchronize(st));
+    shard->allgather(opened_d.p, nvals * sizeof(EF), all.p);
+    std::vector<EF> h(nvals * plan.G);
+    HIP_CHECK(hipMemcpyAsync(h.data(), all.p, h.size() * sizeof(EF), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    for (int r = 0; r < 4; r++)
+      for (size_t i = 0; i < rounds[r]->mats.size(); i++) {
+        const CMat& m = rounds[r]->mats[i];
+        for (int j = 0; j < mp[r][i].npts; j++)
+          for (int c = 0; c < m.lde.width; c++) {
+            const size_t o = mp[r][i].off[j] + c;
+            EF v = h[(size_t)plan.k * nvals + o];
+            if (m.sharded) {
+              v = ef_zero();
+              for (int g = 0; g < plan.G; g++) v = ef_add(v, h[(size_t)g * nvals + o]);
+            }
+            opened[o] = v;
+          }
+      }
+  } else {
+    HIP_CHECK(hipMemcpyAsync(opened.data(), opened_d.p, nvals * sizeof(EF), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+  }
   if (opt.observe_openings)  // decision D1: opened values enter the transcript
     for (int r = 0; r < 4; r++)
       for (size_t i = 0; i < rounds[r]->mats.size(); i++)
@@ -530,6 +729,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   const EF fri_alpha = ch.sample_ef();
 
   // ---- reduced openings per LDE height: every height's column descriptors go up in one copy
+  // (a sharded height: the rank's positions only, ro holding that range)
   std::map<int, DBuf<EF>> ro;
   struct RedJob {
     int lh;
@@ -555,7 +755,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
         const size_t base = cols.size();
         for (int c = 0; c < w; c++) {
           RedCol rc{};
-          rc.col = m.lde.buf.p + (size_t)c * m.lde.height;
+          rc.col = m.rows() + (size_t)c * m.stride();
           cols.push_back(rc);
         }
         RedMat rm{};
@@ -594,18 +794,33 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   upload_async(red_cols_d.p, red_cols.data(), red_cols.size() * sizeof(RedCol), st);
   upload_async(red_mats_d.p, red_mats.data(), red_mats.size() * sizeof(RedMat), st);
   for (const RedJob& j : red_jobs) {
-    DBuf<EF> r((size_t)1 << j.lh);
-    reduce_height(red_cols_d.p + j.col0, red_mats_d.p + j.mat0, j.nmats, (size_t)1 << j.lh,
-                  invd_zeta.p, j.has_b ? invd_next.at(j.lh).p : nullptr, j.ya, j.yb, j.has_b, r.p, st);
+    const size_t H = (size_t)1 << j.lh;
+    const bool sh = plan.sharded(H);
+    const size_t t0 = sh ? plan.row0(H) : 0, cnt = sh ? plan.blk(H) : H;
+    DBuf<EF> r(cnt);
+    const Invd& d = invd.at(j.lh);
+    reduce_range(red_cols_d.p + j.col0, red_mats_d.p + j.mat0, j.nmats, t0, cnt, d.pa(),
+                 j.has_b ? d.pb() : nullptr, j.ya, j.yb, j.has_b, r.p - t0, st);
     ro.emplace(j.lh, std::move(r));
   }
   if (ev.on) ev.end(e3, st, &tms->open);
 
   // ---- FRI commit phase (fri::prover::commit_phase)
   hipEvent_t e4 = ev.on ? ev.begin(st) : nullptr;
-  std::vector<DBuf<EF>> layers;
+  // A layer of a sharded proof stays row-sharded (values [e0, e0 + len / G)) while its fold
+  // output has >= G * 1024 values; the first shorter one is all-gathered and the rest is
+  // computed by every rank.
+  struct FriLayer {
+    DBuf<EF> v;
+    size_t e0 = 0;
+    bool local = false;
+  };
+  std::vector<FriLayer> layers;
   std::vector<MerkleTree> trees;
-  layers.push_back(std::move(ro.at(Lmax)));
+  {
+    const size_t H = (size_t)1 << Lmax;
+    layers.push_back({std::move(ro.at(Lmax)), plan.sharded(H) ? plan.row0(H) : 0, plan.sharded(H)});
+  }
   ro.erase(Lmax);
   // The transcript steps of the rounds run on the device (fri_challenge): the input buffer is
   // empty here (fri_alpha was just sampled), so each round is observe(root) -> one duplex ->
@@ -618,15 +833,26 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   size_t len = (size_t)1 << Lmax;
   for (int rd = 0; len > ((size_t)1 << LOG_BLOWUP); rd++) {
     const size_t h = len / 2;
+    FriLayer& cur = layers.back();
+    if (cur.local && !plan.sharded(h)) {
+      DBuf<EF> all(len);
+      HIP_CHECK(hipStreamSynchronize(st));
+      shard->allgather(cur.v.p, plan.blk(len) * sizeof(EF), all.p);
+      cur.v = std::move(all);
+      cur.e0 = 0;
+      cur.local = false;
+    }
+    const bool loc = cur.local;
+    const size_t i0 = loc ? plan.row0(h) : 0, cnt = loc ? plan.blk(h) : h;
     trees.emplace_back();
     MerkleTree& t = trees.back();
-    merkle_from_rows8(t, (const uint32_t*)layers.back().p, h, st, /*fetch_root=*/false,
+    merkle_from_rows8(t, (const uint32_t*)(cur.v.p - 2 * i0), h, st, /*fetch_root=*/false,
                       RootChallenge{dstate.p, betas.p + rd});
-    DBuf<EF> next(h);
+    DBuf<EF> next(cnt);
     const int lgh = log2i(h);
-    const EF* add = ro.count(lgh) ? ro.at(lgh).p : nullptr;
-    fri_fold_dev(layers.back().p, next.p, h, betas.p + rd, add, st);
-    layers.push_back(std::move(next));
+    const EF* add = ro.count(lgh) ? ro.at(lgh).p : nullptr;  // same range as next
+    fri_fold_range(cur.v.p, next.p, h, i0, cnt, betas.p + rd, add, st);
+    layers.push_back({std::move(next), i0, loc});
     len = h;
   }
   // one device-to-host copy for the commit-phase roots, the transcript state and the final
@@ -637,7 +863,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   for (int i = 0; i < nt; i++) tail.root[i] = trees[i].layers.back().p;
   tail.nroots = nt;
   tail.state = dstate.p;
-  tail.fin = layers.back().p;
+  tail.fin = layers.back().v.p;
   DBuf<uint32_t> packed(8 * MAX_FRI_ROUNDS + 16 + 8);
   hipLaunchKernelGGL(k_pack_fri_tail, dim3(1), dim3(256), 0, st, tail, packed.p);
   KCHECK();
@@ -681,22 +907,23 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     const int lrm = (int)R.tree.layers.size() - 1;
     for (const CMat& m : R.mats) {  // row (index >> (Lmax - lh)) of every column
       const int lh = log2i(m.lde.height);
-      segs.push_back({m.lde.buf.p, (uint64_t)m.lde.height, (uint32_t)(Lmax - lh), 0, 1,
-                      (uint32_t)m.lde.width, -1, 0});
+      segs.push_back({m.rows(), (uint64_t)m.stride(), (uint32_t)(Lmax - lh), 0, 1,
+                      (uint32_t)m.lde.width, m.sharded ? lh - plan.lg : -1, 0});
     }
     for (int L = 0; L < lrm; L++)  // sibling digest at layer L
       segs.push_back({R.tree.layers[L].p, 1, (uint32_t)(Lmax - lrm + L), 1, 8, 8,
                       owner_shift(R.tree, L), 0});
   }
   for (int i = 0; i < ncommit; i++) {
-    segs.push_back({(const uint32_t*)layers[i].p, 1, (uint32_t)i, 1, 4, 4, -1, 0});  // sibling EF
+    const FriLayer& fl = layers[i];  // sibling EF
+    segs.push_back({(const uint32_t*)(fl.v.p - fl.e0), 1, (uint32_t)i, 1, 4, 4,
+                    fl.local ? Lmax - i - plan.lg : -1, 0});
     const int lm = (int)trees[i].layers.size() - 1;
     for (int L = 0; L < lm; L++)
       segs.push_back({trees[i].layers[L].p, 1, (uint32_t)(i + 1 + L), 1, 8, 8,
                       owner_shift(trees[i], L), 0});
   }
   size_t nwords = 0;
-  const ShardCtx* shard = shard_ctx();
   uint32_t* words = gather_queries(segs, qidx, nwords, shard, st);
   if (ev.on) ev.end(e4, st, &tms->fri);
 

@@ -85,18 +85,16 @@ __global__ __launch_bounds__(256) void k_sel_inv(int logN, uint32_t shift, uint3
 }
 
 template <int CHIP>
-__global__ __launch_bounds__(256, 3) void k_quotient(const uint32_t* __restrict__ mainc,
-                                                  const uint32_t* __restrict__ prepc,
-                                                  const uint32_t* __restrict__ permc, int logN,
-                                                  QuotParams qp, const uint32_t* __restrict__ twf,
+__global__ __launch_bounds__(256, 3) void k_quotient(QuotRows in, int logN, QuotParams qp,
+                                                  const uint32_t* __restrict__ twf,
                                                   const uint32_t* __restrict__ sel_inv,
                                                   uint32_t* __restrict__ qout) {
   constexpr int MW = QMAIN_W[CHIP];
   constexpr int PWD = QPREP_W[CHIP] > 0 ? QPREP_W[CHIP] : 1;
   constexpr int PMW = QPERM_W[CHIP];
   const size_t N = (size_t)1 << logN, n = N >> 1;
-  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= N) return;
+  const size_t t = in.t0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= in.t0 + in.count) return;
   const uint32_t i = dbitrev((uint32_t)t, logN);
   const uint32_t inext = (i + 2) & (uint32_t)(N - 1);
   const size_t tn = dbitrev(inext, logN);
@@ -104,21 +102,21 @@ __global__ __launch_bounds__(256, 3) void k_quotient(const uint32_t* __restrict_
   uint32_t L[MW], Nx[MW], PL[PWD], PN[PWD];
 #pragma unroll
   for (int c = 0; c < MW; c++) {
-    L[c] = mainc[(size_t)c * N + t];
-    Nx[c] = mainc[(size_t)c * N + tn];
+    L[c] = in.main_l[(size_t)c * in.stride + t];
+    Nx[c] = in.main_n[(size_t)c * in.stride + tn];
   }
 #pragma unroll
   for (int c = 0; c < PWD; c++) {
-    PL[c] = QPREP_W[CHIP] > 0 ? prepc[(size_t)c * N + t] : 0;
-    PN[c] = QPREP_W[CHIP] > 0 ? prepc[(size_t)c * N + tn] : 0;
+    PL[c] = QPREP_W[CHIP] > 0 ? in.prep[(size_t)c * N + t] : 0;
+    PN[c] = QPREP_W[CHIP] > 0 ? in.prep[(size_t)c * N + tn] : 0;
   }
   EF pl[PMW], pn[PMW];
 #pragma unroll
   for (int e = 0; e < PMW; e++)
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      pl[e].c[k] = permc[(size_t)(4 * e + k) * N + t];
-      pn[e].c[k] = permc[(size_t)(4 * e + k) * N + tn];
+      pl[e].c[k] = in.perm_l[(size_t)(4 * e + k) * in.stride + t];
+      pn[e].c[k] = in.perm_n[(size_t)(4 * e + k) * in.stride + tn];
     }
 
   const uint32_t x = quot_point(i, (uint32_t)n, qp.shift, twf);
@@ -141,11 +139,10 @@ __global__ __launch_bounds__(256, 3) void k_quotient(const uint32_t* __restrict_
 }
 
 template <int CHIP>
-static void launch_q(const uint32_t* mainc, const uint32_t* prepc, const uint32_t* permc, int logN,
-                     const QuotParams& qp, const uint32_t* sel, uint32_t* qout, hipStream_t st) {
-  const size_t N = (size_t)1 << logN;
-  hipLaunchKernelGGL(k_quotient<CHIP>, dim3(ceil_div(N, 256)), dim3(256), 0, st, mainc, prepc,
-                     permc, logN, qp, (const uint32_t*)twiddles().fwd.p, sel, qout);
+static void launch_q(const QuotRows& in, int logN, const QuotParams& qp, const uint32_t* sel,
+                     uint32_t* qout, hipStream_t st) {
+  hipLaunchKernelGGL(k_quotient<CHIP>, dim3(ceil_div(in.count, 256)), dim3(256), 0, st, in, logN,
+                     qp, (const uint32_t*)twiddles().fwd.p, sel, qout);
   KCHECK();
 }
 
@@ -167,17 +164,24 @@ static const uint32_t* sel_inv_table(int logN, const QuotParams& qp, hipStream_t
 
 void quotient(int chip, const uint32_t* mainc, const uint32_t* prepc, const uint32_t* permc,
               int logN, const QuotParams& qp, uint32_t* qout, hipStream_t st) {
+  const size_t N = (size_t)1 << logN;
+  QuotRows in{mainc, mainc, permc, permc, prepc, N, 0, N};
+  quotient_rows(chip, in, logN, qp, qout, st);
+}
+
+void quotient_rows(int chip, const QuotRows& in, int logN, const QuotParams& qp, uint32_t* qout,
+                   hipStream_t st) {
   twiddles().ensure(logN);
   const uint32_t* sel = sel_inv_table(logN, qp, st);
   switch (chip) {
-    case CHIP_CPU: launch_q<CHIP_CPU>(mainc, prepc, permc, logN, qp, sel, qout, st); break;
-    case CHIP_PROGRAM: launch_q<CHIP_PROGRAM>(mainc, prepc, permc, logN, qp, sel, qout, st); break;
-    case CHIP_ADDSUB: launch_q<CHIP_ADDSUB>(mainc, prepc, permc, logN, qp, sel, qout, st); break;
-    case CHIP_JUMP: launch_q<CHIP_JUMP>(mainc, prepc, permc, logN, qp, sel, qout, st); break;
-    case CHIP_MEMORY: launch_q<CHIP_MEMORY>(mainc, prepc, permc, logN, qp, sel, qout, st); break;
-    case CHIP_BYTE: launch_q<CHIP_BYTE>(mainc, prepc, permc, logN, qp, sel, qout, st); break;
-    case CHIP_MEMINSTRS: launch_q<CHIP_MEMINSTRS>(mainc, prepc, permc, logN, qp, sel, qout, st); break;
-    case CHIP_IO: launch_q<CHIP_IO>(mainc, prepc, permc, logN, qp, sel, qout, st); break;
+    case CHIP_CPU: launch_q<CHIP_CPU>(in, logN, qp, sel, qout, st); break;
+    case CHIP_PROGRAM: launch_q<CHIP_PROGRAM>(in, logN, qp, sel, qout, st); break;
+    case CHIP_ADDSUB: launch_q<CHIP_ADDSUB>(in, logN, qp, sel, qout, st); break;
+    case CHIP_JUMP: launch_q<CHIP_JUMP>(in, logN, qp, sel, qout, st); break;
+    case CHIP_MEMORY: launch_q<CHIP_MEMORY>(in, logN, qp, sel, qout, st); break;
+    case CHIP_BYTE: launch_q<CHIP_BYTE>(in, logN, qp, sel, qout, st); break;
+    case CHIP_MEMINSTRS: launch_q<CHIP_MEMINSTRS>(in, logN, qp, sel, qout, st); break;
+    case CHIP_IO: launch_q<CHIP_IO>(in, logN, qp, sel, qout, st); break;
     default: throw std::runtime_error("quotient: bad chip");
   }
 }
