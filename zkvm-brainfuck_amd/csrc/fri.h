@@ -36,6 +36,25 @@ void pow_table(const kb::EF& z, size_t j0, size_t count, kb::EF* out, hipStream_
 void open_coefficients(const uint32_t* coef, size_t col_stride, int w, size_t count,
                        const kb::EF* tab_a, const kb::EF& scale_a, kb::EF* out_a,
                        const kb::EF* tab_b, const kb::EF& scale_b, kb::EF* out_b, hipStream_t st);
+// One matrix of a batched barycentric opening (open_batch): columns of an LDE of height
+// `height` (column stride) opened over its low coset at one or two points; out_a[c] / out_b[c]
+// = scale_a / scale_b times the weighted column sums.  chunk0 .. part_off are filled in by
+// open_batch.
+struct OpenDesc {
+  const uint32_t* mat;
+  uint64_t height;
+  int w, logH;
+  const kb::EF* invd_a;
+  const kb::EF* invd_b;
+  kb::EF scale_a, scale_b;
+  kb::EF* out_a;
+  kb::EF* out_b;
+  uint32_t chunk0, col0, nchunks, pad;
+  uint64_t part_off;
+};
+// Every descriptor of ds is opened at np (1 or 2) points: one partial-sum launch over all of
+// their row chunks, one final launch over all of their columns.
+void open_batch(std::vector<OpenDesc>& ds, int np, hipStream_t st);
 // out_dev[c] = value at z of column c of a committed LDE (height = 2n), via the low coset.
 void open_matrix(const uint32_t* mat, size_t height, int w, const kb::EF* invd_a,
                  const kb::EF& scale_a, kb::EF* out_a, const kb::EF* invd_b,

@@ -82,16 +82,15 @@ __device__ __forceinline__ uint32_t row_sum16(uint32_t v) {
 // TAB = false: barycentric weights W_k,t = -x_t invd_k[t] over the low coset (mat = the LDE).
 // TAB = true: W_k,t = invd_k[t] read as a weight table (coefficient form: mat = a range of
 // coefficients, the table = powers of the point), logH/twf unused.
-template <int NP, bool TAB = false>
-__global__ __launch_bounds__(OPEN_T) void k_open_partial(const uint32_t* __restrict__ mat,
-                                                         size_t height, int w, size_t n, int logH,
-                                                         const EF* __restrict__ invd_a,
-                                                         const EF* __restrict__ invd_b,
-                                                         const uint32_t* __restrict__ twf,
-                                                         EF* __restrict__ partial) {
+template <int NP, bool TAB>
+__device__ __forceinline__ void open_tile(const uint32_t* __restrict__ mat, size_t height, int w,
+                                          size_t n, int logH, const EF* __restrict__ invd_a,
+                                          const EF* __restrict__ invd_b,
+                                          const uint32_t* __restrict__ twf,
+                                          EF* __restrict__ partial, unsigned chunk) {
   constexpr int NROW = OPEN_T / 16;
   __shared__ EF sh[NP][NROW][OPEN_CB];
-  const size_t c0 = (size_t)blockIdx.x * OPEN_CH + threadIdx.x;
+  const size_t c0 = (size_t)chunk * OPEN_CH + threadIdx.x;
   const int nr = c0 >= n ? 0 : (int)min((size_t)OPEN_R, (n - c0 + OPEN_T - 1) / OPEN_T);
   EF W[NP][OPEN_R];
 #pragma unroll
@@ -147,19 +146,42 @@ __global__ __launch_bounds__(OPEN_T) void k_open_partial(const uint32_t* __restr
       EF a = sh[k][0][c];
 #pragma unroll
       for (int q = 1; q < NROW; q++) a = ef_add(a, sh[k][q][c]);
-      partial[((size_t)blockIdx.x * w + cb + c) * NP + k] = a;
+      partial[((size_t)chunk * w + cb + c) * NP + k] = a;
     }
     __syncthreads();
   }
 }
 
+template <int NP, bool TAB = false>
+__global__ __launch_bounds__(OPEN_T) void k_open_partial(const uint32_t* __restrict__ mat,
+                                                         size_t height, int w, size_t n, int logH,
+                                                         const EF* __restrict__ invd_a,
+                                                         const EF* __restrict__ invd_b,
+                                                         const uint32_t* __restrict__ twf,
+                                                         EF* __restrict__ partial) {
+  open_tile<NP, TAB>(mat, height, w, n, logH, invd_a, invd_b, twf, partial, blockIdx.x);
+}
+
+// Batched barycentric openings: block b works on chunk (b - chunk0) of the matrix whose block
+// range holds b; every matrix of a proof opened at NP points goes in one launch.
+template <int NP>
+__global__ __launch_bounds__(OPEN_T) void k_open_partial_batch(const OpenDesc* __restrict__ d,
+                                                               int nd,
+                                                               const uint32_t* __restrict__ twf,
+                                                               EF* __restrict__ partial) {
+  int m = 0;
+  while (m + 1 < nd && d[m + 1].chunk0 <= blockIdx.x) m++;
+  const OpenDesc& o = d[m];
+  open_tile<NP, false>(o.mat, o.height, o.w, o.height / 2, o.logH, o.invd_a, o.invd_b, twf,
+                       partial + o.part_off, blockIdx.x - o.chunk0);
+}
+
 // out_k[c] = scale_k * sum_chunks partial[(chunk * w + c) * NP + k]   (one block per column)
 template <int NP>
-__global__ __launch_bounds__(256) void k_open_final(const EF* __restrict__ partial, int nchunks,
-                                                    int w, EF scale_a, EF scale_b,
-                                                    EF* __restrict__ out_a, EF* __restrict__ out_b) {
+__device__ __forceinline__ void open_final(const EF* __restrict__ partial, int nchunks, int w,
+                                           int c, EF scale_a, EF scale_b, EF* __restrict__ out_a,
+                                           EF* __restrict__ out_b) {
   __shared__ EF sh[NP][4];
-  const int c = blockIdx.x;
   EF s[NP];
 #pragma unroll
   for (int k = 0; k < NP; k++) s[k] = ef_zero();
@@ -178,6 +200,24 @@ __global__ __launch_bounds__(256) void k_open_final(const EF* __restrict__ parti
     for (int q = 1; q < (int)(blockDim.x / 64); q++) tot = ef_add(tot, sh[k][q]);
     (k ? out_b : out_a)[c] = ef_mul(tot, k ? scale_b : scale_a);
   }
+}
+
+template <int NP>
+__global__ __launch_bounds__(256) void k_open_final(const EF* __restrict__ partial, int nchunks,
+                                                    int w, EF scale_a, EF scale_b,
+                                                    EF* __restrict__ out_a, EF* __restrict__ out_b) {
+  open_final<NP>(partial, nchunks, w, blockIdx.x, scale_a, scale_b, out_a, out_b);
+}
+
+// Batched final sums: block b is column (b - col0) of the matrix whose column range holds b.
+template <int NP>
+__global__ __launch_bounds__(256) void k_open_final_batch(const OpenDesc* __restrict__ d, int nd,
+                                                          const EF* __restrict__ partial) {
+  int m = 0;
+  while (m + 1 < nd && d[m + 1].col0 <= blockIdx.x) m++;
+  const OpenDesc& o = d[m];
+  open_final<NP>(partial + o.part_off, (int)o.nchunks, o.w, (int)(blockIdx.x - o.col0), o.scale_a,
+                 o.scale_b, o.out_a, o.out_b);
 }
 
 // ------------------------------------------------------------------ reduced openings
@@ -388,6 +428,38 @@ void open_matrix(const uint32_t* mat, size_t height, int w, const EF* invd_a, co
     KCHECK();
     hipLaunchKernelGGL(k_open_final<1>, dim3(w), dim3(256), 0, st, (const EF*)partial.p, nchunks,
                        w, scale_a, scale_a, out_a, out_a);
+  }
+  KCHECK();
+}
+
+void open_batch(std::vector<OpenDesc>& ds, int np, hipStream_t st) {
+  if (ds.empty()) return;
+  uint32_t chunks = 0, cols = 0;
+  uint64_t part = 0;
+  for (OpenDesc& o : ds) {
+    o.nchunks = ceil_div(o.height / 2, OPEN_CH);
+    o.chunk0 = chunks;
+    o.col0 = cols;
+    o.part_off = part;
+    chunks += o.nchunks;
+    cols += (uint32_t)o.w;
+    part += (uint64_t)o.nchunks * o.w * np;
+  }
+  DBuf<OpenDesc> dd(ds.size());
+  upload_async(dd.p, ds.data(), ds.size() * sizeof(OpenDesc), st);
+  DBuf<EF> partial(std::max<uint64_t>(part, 1));
+  const uint32_t* twf = (const uint32_t*)twiddles().fwd.p;
+  const int nd = (int)ds.size();
+  if (np == 2) {
+    hipLaunchKernelGGL(k_open_partial_batch<2>, dim3(chunks), dim3(OPEN_T), 0, st, dd.p, nd, twf,
+                       partial.p);
+    KCHECK();
+    hipLaunchKernelGGL(k_open_final_batch<2>, dim3(cols), dim3(256), 0, st, dd.p, nd, partial.p);
+  } else {
+    hipLaunchKernelGGL(k_open_partial_batch<1>, dim3(chunks), dim3(OPEN_T), 0, st, dd.p, nd, twf,
+                       partial.p);
+    KCHECK();
+    hipLaunchKernelGGL(k_open_final_batch<1>, dim3(cols), dim3(256), 0, st, dd.p, nd, partial.p);
   }
   KCHECK();
 }

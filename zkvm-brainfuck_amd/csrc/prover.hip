@@ -665,6 +665,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     ptabs.emplace(key, std::move(t));
     return p;
   };
+  std::vector<OpenDesc> open1, open2;
   for (int r = 0; r < 4; r++)
     for (size_t i = 0; i < rounds[r]->mats.size(); i++) {
       const CMat& m = rounds[r]->mats[i];
@@ -691,9 +692,21 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
         scale[j] = ef_mul(ef_sub(zn, three_n), ef_inv(ef_mul_base(three_n, n_f)));
       }
       const Invd& d = invd.at(lh);
-      open_matrix(m.lde.buf.p, m.lde.height, m.lde.width, d.full_a(), scale[0], out_a,
-                  two ? d.full_b() : nullptr, two ? scale[1] : scale[0], out_b, st);
+      OpenDesc o{};
+      o.mat = m.lde.buf.p;
+      o.height = m.lde.height;
+      o.w = m.lde.width;
+      o.logH = lh;
+      o.invd_a = d.full_a();
+      o.invd_b = two ? d.full_b() : o.invd_a;
+      o.scale_a = scale[0];
+      o.scale_b = two ? scale[1] : scale[0];
+      o.out_a = out_a;
+      o.out_b = two ? out_b : out_a;
+      (two ? open2 : open1).push_back(o);
     }
+  open_batch(open2, 2, st);  // every barycentric opening: two partial + two final launches
+  open_batch(open1, 1, st);
   std::vector<EF> opened(nvals);
   if (plan.on()) {  // one all-gather; sharded matrices' slices summed, replicated ones kept
     DBuf<EF> all(nvals * plan.G);
