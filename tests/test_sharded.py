@@ -79,7 +79,7 @@ def _run(world, cases):
     return res
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_sharded_proof_is_bit_exact(world):
     from bfz import guests
     import oracle_lib as O

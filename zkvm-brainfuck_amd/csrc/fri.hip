@@ -55,7 +55,10 @@ __global__ __launch_bounds__(256) void k_inv_denoms(EF z, int logH, size_t t0, s
 }
 
 // ------------------------------------------------------------------ openings
-constexpr int OPEN_T = 256, OPEN_R = 8, OPEN_CH = OPEN_T * OPEN_R, OPEN_CB = 32;
+#ifndef BFZ_OPEN_R
+#define BFZ_OPEN_R 8
+#endif
+constexpr int OPEN_T = 256, OPEN_R = BFZ_OPEN_R, OPEN_CH = OPEN_T * OPEN_R, OPEN_CB = 32;
 
 __device__ __forceinline__ EF wave_sum(EF v) {
 #pragma unroll
@@ -517,8 +520,7 @@ uint32_t grind(const GrindState& gs, int bits, hipStream_t st) {
                        (uint32_t)bits, best.p);
     KCHECK();
     uint32_t h = 0;
-    HIP_CHECK(hipMemcpyAsync(&h, best.p, 4, hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipStreamSynchronize(st));
+    fetch(&h, best.p, 4, st);
     if (h != 0xffffffffu) return h;
   }
   throw std::runtime_error("grind: no witness");
@@ -559,7 +561,7 @@ uint32_t* gather_queries(const std::vector<GatherSeg>& segs, const std::vector<u
     shard->allreduce_sum_u32(dout.p, nwords);
   }
   HIP_CHECK(hipMemcpyAsync(host, dout.p, nwords * 4, hipMemcpyDeviceToHost, st));
-  HIP_CHECK(hipStreamSynchronize(st));
+  spin_sync(st);  // host is pinned already
   return host;
 }
 

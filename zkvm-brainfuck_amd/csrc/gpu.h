@@ -146,6 +146,10 @@ hipStream_t stream();
 // stall.  staging_reset() once no earlier copy can be pending (after a stream synchronize).
 void upload_async(void* dst, const void* src, size_t bytes, hipStream_t st);
 void staging_reset();
+// Device -> host copy of a few bytes for the transcript, waited for by spinning (runtime.hip);
+// spin_sync waits for everything queued on st so far.
+void fetch(void* dst, const void* src, size_t bytes, hipStream_t st);
+void spin_sync(hipStream_t st);
 // Large pageable host -> device copy through double-buffered pinned chunks (runtime.hip);
 // returns when the data has arrived.
 void upload_bulk(void* dst, const void* src, size_t bytes, hipStream_t st);

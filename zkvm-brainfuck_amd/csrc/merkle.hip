@@ -322,8 +322,7 @@ static void build_layers(MerkleTree& t, int L0, size_t len, const std::vector<co
   }
   if (next != sorted.size()) throw std::runtime_error("merkle: non power-of-two heights");
   if (!fetch_root) return;
-  HIP_CHECK(hipMemcpyAsync(t.root, t.layers[nl].p, 32, hipMemcpyDeviceToHost, st));
-  HIP_CHECK(hipStreamSynchronize(st));
+  fetch(t.root, t.layers[nl].p, 32, st);
 }
 
 // ------------------------------------------------------------------ sharded trees

@@ -11,10 +11,12 @@
 #include <algorithm>
 #include <cerrno>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
 #include "fri.h"
+#include "host_p2.h"
 #include "logup.h"
 #include "ntt.h"
 #include "poseidon2.h"
@@ -53,7 +55,7 @@ bool observe_openings_from_env() {
 void Challenger::duplex() {
   for (int i = 0; i < nin; i++) st[i] = in[i];
   nin = 0;
-  poseidon2_permute(st);
+  host_permute(st);
   for (int i = 0; i < 8; i++) out[i] = st[i];
   nout = 8;
 }
@@ -100,6 +102,22 @@ __global__ void k_pack_fri_tail(FriTail t, uint32_t* __restrict__ packed) {
 }
 
 namespace {
+// BFZ_HOST_TRACE=1: host timestamps (us since the last mark 0) at the transcript points of each
+// proof on stderr -- splits the GPU's idle gaps into host work and launch latency.
+struct HostTrace {
+  bool on = std::getenv("BFZ_HOST_TRACE") != nullptr;
+  std::chrono::steady_clock::time_point t0;
+  void mark(const char* what, bool reset = false) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    if (reset) t0 = now;
+    std::fprintf(stderr, "host %9.1f %s\n", std::chrono::duration<double, std::micro>(now - t0).count(), what);
+  }
+};
+HostTrace& htrace() {
+  static HostTrace h;
+  return h;
+}
 struct EvTimer {
   bool on = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
@@ -470,6 +488,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   const ShardCtx* shard = shard_ctx();
 
   // ---- open (prover.rs:242-553), on a clone of the challenger (prover.rs:578)
+  htrace().mark("main root fetched");
   ch.observe_digest(mainr.tree.root);
   const EF perm_alpha = ch.sample_ef();
   const EF perm_beta = ch.sample_ef();
@@ -488,13 +507,14 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     DBuf<uint32_t> pe(4 * (size_t)pw * hn[k]);
     const int pi = pk.idx_of_chip[c];
     const uint32_t* prep = pi >= 0 ? pk.prep_evals[pi].p : nullptr;
+    if (k == 0) htrace().mark("perm_rows launch");
     perm_trace(c, dt.evals[order[k]].p, prep, hn[k], pc, pe.p, cums_d.p + k, st);
     lde_into(permr.mats[k], pe.p, hn[k], 4 * pw, ONE, st, &ev, tms, &plan, /*want_next=*/true);
   }
   permr.commit(st);
   std::vector<EF> cums(nc);
-  HIP_CHECK(hipMemcpyAsync(cums.data(), cums_d.p, nc * sizeof(EF), hipMemcpyDeviceToHost, st));
-  HIP_CHECK(hipStreamSynchronize(st));
+  fetch(cums.data(), cums_d.p, nc * sizeof(EF), st);
+  htrace().mark("cums fetched");
   if (ev.on) ev.end(e1, st, &tms->perm);
   ch.observe_digest(permr.tree.root);
   for (int k = 0; k < nc; k++) ch.observe_ef(cums[k]);
@@ -538,6 +558,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     qv[k].reset(8 * n);
     const CMat& mm = mainr.mats[k];
     const CMat& pm = permr.mats[k];
+    if (k == 0) htrace().mark("quotient launch");
     if (mm.sharded) {  // this rank's points only; next rows from the next-residue shards
       const QuotRows in{mm.rows(), mm.next_rows(), pm.rows(), pm.next_rows(), prep_lde,
                         mm.stride(), mm.row0, mm.blk};
@@ -564,6 +585,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   quotr.commit(st);
   if (ev.on) ev.end(e2, st, &tms->quotient);
   ch.observe_digest(quotr.tree.root);
+  htrace().mark("quotient root fetched");
   const EF zeta = ch.sample_ef();
 
   // ---- PCS open: opened values (prover.rs:417-470)
@@ -618,6 +640,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
       two_at[lh] |= mp[r][i].npts == 2;
       rep_at[lh] |= !rounds[r]->mats[i].sharded;
     }
+  htrace().mark("inv_denoms launch");
   DBuf<EF> invd_zeta;
   if (!plan.on()) {
     invd_zeta.reset((size_t)1 << Lmax);
@@ -730,8 +753,8 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
           }
       }
   } else {
-    HIP_CHECK(hipMemcpyAsync(opened.data(), opened_d.p, nvals * sizeof(EF), hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipStreamSynchronize(st));
+    fetch(opened.data(), opened_d.p, nvals * sizeof(EF), st);
+    htrace().mark("opened fetched");
   }
   if (opt.observe_openings)  // decision D1: opened values enter the transcript
     for (int r = 0; r < 4; r++)
@@ -740,6 +763,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
           for (int c = 0; c < rounds[r]->mats[i].lde.width; c++)
             ch.observe_ef(opened[mp[r][i].off[j] + c]);
   const EF fri_alpha = ch.sample_ef();
+  htrace().mark("fri alpha");
 
   // ---- reduced openings per LDE height: every height's column descriptors go up in one copy
   // (a sharded height: the rank's positions only, ro holding that range)
@@ -804,6 +828,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   }
   DBuf<RedCol> red_cols_d(std::max<size_t>(red_cols.size(), 1));
   DBuf<RedMat> red_mats_d(std::max<size_t>(red_mats.size(), 1));
+  htrace().mark("reduce descriptors");
   upload_async(red_cols_d.p, red_cols.data(), red_cols.size() * sizeof(RedCol), st);
   upload_async(red_mats_d.p, red_mats.data(), red_mats.size() * sizeof(RedMat), st);
   for (const RedJob& j : red_jobs) {
@@ -881,8 +906,8 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   hipLaunchKernelGGL(k_pack_fri_tail, dim3(1), dim3(256), 0, st, tail, packed.p);
   KCHECK();
   std::vector<uint32_t> hp(packed.n);
-  HIP_CHECK(hipMemcpyAsync(hp.data(), packed.p, packed.n * 4, hipMemcpyDeviceToHost, st));
-  HIP_CHECK(hipStreamSynchronize(st));
+  fetch(hp.data(), packed.p, packed.n * 4, st);
+  htrace().mark("fri tail fetched");
   for (int i = 0; i < nt; i++) std::memcpy(trees[i].root, &hp[8 * i], 32);
   uint32_t st_after[16];
   std::memcpy(st_after, &hp[8 * MAX_FRI_ROUNDS], 64);
@@ -901,7 +926,9 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   for (int i = 0; i < 16; i++) gs.st[i] = ch.st[i];
   for (int i = 0; i < 8; i++) gs.in[i] = ch.in[i];
   gs.nin = ch.nin;
+  htrace().mark("grind");
   const uint32_t witness = grind(gs, POW_BITS, st);
+  htrace().mark("grind done");
   if (!ch.check_witness(POW_BITS, witness)) throw std::runtime_error("grind: bad witness");
   const int nq = opt.num_queries;
   std::vector<uint32_t> qidx(nq);
@@ -1030,6 +1057,7 @@ std::vector<uint8_t> prove_events(const ProvingKey& pk, const DeviceEvents& ev,
     HIP_CHECK(hipEventCreate(&b));
     HIP_CHECK(hipEventRecord(a, st));
   }
+  htrace().mark("proof start", true);
   DeviceTraces dt;
   generate_traces_device(ev, dt, st);
   if (timing) HIP_CHECK(hipEventRecord(b, st));

@@ -12,6 +12,7 @@
 // 3 w_2n^k H_n (split_evals / split_domains), ready for the chunk LDE.
 #include "quotient.h"
 
+#include <array>
 #include <map>
 
 #include "air.h"
@@ -203,7 +204,9 @@ static int count_chip() {
   return acc.n;
 }
 
-int num_constraints(int chip) {
+// The count is a property of the AIR: evaluated symbolically once per chip and cached (the
+// prover needs it for every chip of every proof).
+static int num_constraints_eval(int chip) {
   switch (chip) {
     case CHIP_CPU: return count_chip<CHIP_CPU>();
     case CHIP_PROGRAM: return count_chip<CHIP_PROGRAM>();
@@ -215,6 +218,16 @@ int num_constraints(int chip) {
     case CHIP_IO: return count_chip<CHIP_IO>();
   }
   return 0;
+}
+
+int num_constraints(int chip) {
+  static const auto counts = [] {
+    std::array<int, NUM_CHIPS> c{};
+    for (int i = 0; i < NUM_CHIPS; i++) c[i] = num_constraints_eval(i);
+    return c;
+  }();
+  if (chip < 0 || chip >= NUM_CHIPS) return 0;
+  return counts[chip];
 }
 
 }  // namespace bfz

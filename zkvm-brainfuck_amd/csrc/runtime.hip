@@ -121,6 +121,38 @@ void upload_bulk(void* dst, const void* src, size_t bytes, hipStream_t st) {
   HIP_CHECK(hipEventSynchronize(b->done[1]));
 }
 
+// Transcript round trips: the host needs a few bytes from the device (a root, the opened
+// values, the FRI tail) before it can pick the next challenge, while the GPU idles.  The copy
+// goes to a pinned mailbox (a pageable destination makes the runtime stage it), and the host
+// spins on an event instead of a stream synchronize that may put the thread to sleep.
+void spin_sync(hipStream_t st) {
+  static hipEvent_t ev = [] {
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return e;
+  }();
+  HIP_CHECK(hipEventRecord(ev, st));
+  for (;;) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) HIP_CHECK(e);
+  }
+}
+
+void fetch(void* dst, const void* src, size_t bytes, hipStream_t st) {
+  if (!bytes) return;
+  static uint8_t* box = nullptr;
+  static size_t cap = 0;
+  if (bytes > cap) {  // no copy into it is pending: every fetch waits for its copy
+    if (box) HIP_CHECK(hipHostFree(box));
+    cap = std::max(bytes, (size_t)1 << 16);
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&box), cap, hipHostMallocDefault));
+  }
+  HIP_CHECK(hipMemcpyAsync(box, src, bytes, hipMemcpyDeviceToHost, st));
+  spin_sync(st);
+  std::memcpy(dst, box, bytes);
+}
+
 Twiddles& twiddles() {
   static Twiddles* t = new Twiddles();
   return *t;

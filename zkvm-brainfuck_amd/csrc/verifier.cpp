@@ -5,6 +5,7 @@
 //                              folded(zeta) * 1/Z_H(zeta) == recomputed quotient(zeta),
 //                              sum of cumulative sums == 0.
 #include "verifier.h"
+#include "host_p2.h"
 
 #include <algorithm>
 #include <array>
@@ -72,18 +73,18 @@ void sponge(uint32_t st[16], const std::vector<const uint32_t*>& rows, const std
     for (int c = 0; c < ws[m]; c++) {
       st[pos++] = rows[m][c];
       if (pos == 8) {
-        poseidon2_permute(st);
+        host_permute(st);
         pos = 0;
       }
     }
-  if (pos) poseidon2_permute(st);
+  if (pos) host_permute(st);
 }
 
 void compress(const uint32_t* l, const uint32_t* r, uint32_t* out) {
   uint32_t s[16];
   std::memcpy(s, l, 32);
   std::memcpy(s + 8, r, 32);
-  poseidon2_permute(s);
+  host_permute(s);
   std::memcpy(out, s, 32);
 }
 
