@@ -23,8 +23,10 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, cases, q):
+def _worker(rank, world, port, cases, q, fri_min=None):
     try:
+        if fri_min is not None:  # shard the FRI rounds of these small proofs too
+            os.environ["BFZ_FRI_SHARD_MIN"] = str(fri_min)
         sys.path.insert(0, os.path.join(ROOT, "zkvm-brainfuck_amd"))
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -60,12 +62,13 @@ def _worker(rank, world, port, cases, q):
         q.put((rank, None, traceback.format_exc()))
 
 
-def _run(world, cases):
+def _run(world, cases, fri_min=None):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, cases, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, cases, q, fri_min))
+          for r in range(world)]
     for p in ps:
         p.start()
     res = {}
@@ -79,12 +82,14 @@ def _run(world, cases):
     return res
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_sharded_proof_is_bit_exact(world):
+@pytest.mark.parametrize("world,fri_min", [(2, None), (4, None), (8, None), (2, 1024), (4, 1024)])
+def test_sharded_proof_is_bit_exact(world, fri_min):
+    """fri_min=1024 keeps every FRI round with >= world * 1024 leaves row-sharded (the default
+    replicates the rounds below 2^18 leaves, i.e. all of these small proofs' rounds)."""
     from bfz import guests
     import oracle_lib as O
     cases = [(guests.FIBO, [17]), (guests.FIBO, [255])]
-    res = _run(world, cases)
+    res = _run(world, cases, fri_min)
     for i, (prog, stdin) in enumerate(cases):
         digests = {res[r][i][0] for r in range(world)}
         assert len(digests) == 1, "ranks disagree"

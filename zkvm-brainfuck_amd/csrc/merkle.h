@@ -60,6 +60,6 @@ struct RootChallenge {
 // permutation each).  With fetch_root = false the root stays on the device
 // (tree.layers.back()) and tree.root is not filled.
 void merkle_from_rows8(MerkleTree& tree, const uint32_t* rows, size_t h, hipStream_t st,
-                       bool fetch_root = true, RootChallenge rc = {});
+                       bool fetch_root = true, RootChallenge rc = {}, bool allow_shard = true);
 
 }  // namespace bfz

@@ -415,7 +415,7 @@ static void hash_rows8_range(const uint32_t* rows, size_t r0, size_t count, uint
 }
 
 void merkle_from_rows8(MerkleTree& t, const uint32_t* rows, size_t h, hipStream_t st,
-                       bool fetch_root, RootChallenge rc) {
+                       bool fetch_root, RootChallenge rc, bool allow_shard) {
   t.mats = {MatRef{rows, h, 8}};
   t.layers.clear();
   t.layers.resize(log2i(h) + 1);
@@ -425,7 +425,7 @@ void merkle_from_rows8(MerkleTree& t, const uint32_t* rows, size_t h, hipStream_
     hash_rows8_range(rows, r0, count, t.layers[0].p, st);
   };
   if (h < 2) throw std::runtime_error("merkle: rows8 tree needs two leaves");
-  if (shard_tree(h)) {
+  if (allow_shard && shard_tree(h)) {
     build_sharded(t, h, {}, 0, leaves, st, fetch_root, rc);
     return;
   }

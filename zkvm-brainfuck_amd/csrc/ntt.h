@@ -30,6 +30,9 @@ void coset_lde(const uint32_t* evals, size_t n, int w, uint32_t shift, uint32_t*
 void lde_coefficients(const uint32_t* evals, size_t n, int w, uint32_t* coef, hipStream_t st);
 void coset_residue(const uint32_t* coef, size_t n, int w, uint32_t shift, int logG, int r,
                    uint32_t* out, hipStream_t st);
+// The same for the listed columns only (out column y = coefficient column cols[y]).
+void coset_residue_cols(const uint32_t* coef, size_t n, const std::vector<int>& cols,
+                        uint32_t shift, int logG, int r, uint32_t* out, hipStream_t st);
 
 // Row-major natural-order host layout -> column-major bit-reversed device layout.
 void transpose_bitrev(const uint32_t* rowmajor, size_t n, int w, uint32_t* colmajor,

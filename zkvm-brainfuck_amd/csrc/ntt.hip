@@ -712,10 +712,13 @@ void coset_lde(const uint32_t* evals, size_t n, int w, uint32_t shift, uint32_t*
 
 // d[u] = sum_(l < n/m) coef[u + l m] a^(u + l m) / n  (coef = n c: the iDFT leaves 1/n out;
 // a^j / n = A[j & mask] * AH[j >> B] with the 1/n folded into AH)
+struct ColMap {  // output column y reads input column col[y]
+  uint8_t col[64];
+};
 __global__ __launch_bounds__(256) void k_fold_residue(const uint32_t* __restrict__ coef, size_t n,
                                                       uint32_t* __restrict__ out, size_t m, int B,
-                                                      const uint32_t* __restrict__ pw) {
-  const uint32_t* c = coef + (size_t)blockIdx.y * n;
+                                                      const uint32_t* __restrict__ pw, ColMap cm) {
+  const uint32_t* c = coef + (size_t)cm.col[blockIdx.y] * n;
   uint32_t* o = out + (size_t)blockIdx.y * m;
   const size_t mask = ((size_t)1 << B) - 1, nb = mask + 1;
   for (size_t u = (size_t)blockIdx.x * blockDim.x + threadIdx.x; u < m;
@@ -752,6 +755,17 @@ void lde_coefficients(const uint32_t* evals, size_t n, int w, uint32_t* coef, hi
 
 void coset_residue(const uint32_t* coef, size_t n, int w, uint32_t shift, int logG, int r,
                    uint32_t* out, hipStream_t st) {
+  std::vector<int> all(w);
+  for (int c = 0; c < w; c++) all[c] = c;
+  coset_residue_cols(coef, n, all, shift, logG, r, out, st);
+}
+
+void coset_residue_cols(const uint32_t* coef, size_t n, const std::vector<int>& cols,
+                        uint32_t shift, int logG, int r, uint32_t* out, hipStream_t st) {
+  const int w = (int)cols.size();
+  if (w < 1 || w > 64) throw std::runtime_error("coset_residue: 1..64 columns");
+  ColMap map{};
+  for (int y = 0; y < w; y++) map.col[y] = (uint8_t)cols[y];
   const int L = log2i(n);
   if (logG < 1 || logG > L + 1) throw std::runtime_error("coset_residue: bad shard count");
   const size_t m = (2 * n) >> logG;
@@ -759,7 +773,7 @@ void coset_residue(const uint32_t* coef, size_t n, int w, uint32_t shift, int lo
   const int B = (L + 1) / 2;
   const uint32_t* pw = residue_powers(a, L, B);
   const dim3 grid(std::min<unsigned>(ceil_div(m, 256), 2048), w);
-  hipLaunchKernelGGL(k_fold_residue, grid, dim3(256), 0, st, coef, n, out, m, B, pw);
+  hipLaunchKernelGGL(k_fold_residue, grid, dim3(256), 0, st, coef, n, out, m, B, pw, map);
   KCHECK();
   ntt_passes(out, out, m, m, w, log2i(m), /*dif=*/true, st);
 }

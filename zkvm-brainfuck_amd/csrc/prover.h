@@ -45,10 +45,16 @@ struct CMat {               // a committed matrix: LDE on 3*H_2n (bit-reversed, 
   bool sharded = false;
   size_t blk = 0, row0 = 0, nxt_row0 = 0;
   DBuf<uint32_t> coef, nxt;
+  std::array<uint8_t, 64> nmap{};  // column c's next row: column nmap[c] of next_rows()
   // column c, global position t  ->  rows()[c * stride() + t]
   const uint32_t* rows() const { return sharded ? lde.buf.p - row0 : lde.buf.p; }
   size_t stride() const { return sharded ? blk : lde.height; }
-  const uint32_t* next_rows() const { return sharded && nxt.p ? nxt.p - nxt_row0 : rows(); }
+  // Next rows of a sharded matrix come from positions [nxt_row0, nxt_row0 + blk): the next-row
+  // shard when one was computed (G >= 4), the rank's own shard otherwise (G = 2: the same class;
+  // G >= 4 without next-row columns: never read, but every address stays inside the buffer).
+  const uint32_t* next_rows() const {
+    return sharded ? (nxt.p ? nxt.p : lde.buf.p) - nxt_row0 : rows();
+  }
   MatRef ref() const { return MatRef{rows(), lde.height, lde.width, stride()}; }
 };
 

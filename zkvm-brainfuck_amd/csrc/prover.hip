@@ -22,6 +22,7 @@
 #include "poseidon2.h"
 #include "quotient.h"
 #include "tracegen.h"
+#include "verifier.h"
 
 namespace bfz {
 
@@ -213,11 +214,23 @@ Plan make_plan() {
 }
 }  // namespace
 
-// plan != nullptr and a height it shards: this rank's residue-class shard of the LDE (plus the
-// next-row shard when want_next and G >= 4) from the interpolant's coefficients, kept in cm.coef.
+// Columns each chip reads at the next row (verifier.cpp: next_row_columns), computed once.
+static const NextCols& chip_next_cols(int chip) {
+  static const auto all = [] {
+    std::array<NextCols, NUM_CHIPS> a;
+    for (int c = 0; c < NUM_CHIPS; c++) a[c] = next_row_columns(c);
+    return a;
+  }();
+  return all[chip];
+}
+
+// plan != nullptr and a height it shards: this rank's residue-class shard of the LDE from the
+// interpolant's coefficients (kept in cm.coef), plus -- for G >= 4 -- the shard of the next-row
+// residue class for the columns in next_cols (the quotient reads only those at row i + 2).
 static void lde_into(CMat& cm, const uint32_t* evals, size_t n, int w, uint32_t domain_shift,
                      hipStream_t st, EvTimer* tm, StageTimes* times, const Plan* plan = nullptr,
-                     bool want_next = false) {
+                     const std::vector<int>* next_cols = nullptr) {
+  for (int c = 0; c < 64; c++) cm.nmap[c] = (uint8_t)c;
   cm.n = n;
   cm.log_n = log2i(n);
   cm.shift = domain_shift;
@@ -234,10 +247,12 @@ static void lde_into(CMat& cm, const uint32_t* evals, size_t n, int w, uint32_t 
     cm.lde.buf.reset(cm.blk * (size_t)w);
     lde_coefficients(evals, n, w, cm.coef.p, st);
     coset_residue(cm.coef.p, n, w, lde_shift, plan->lg, plan->r, cm.lde.buf.p, st);
-    if (want_next && plan->G >= 4) {
-      cm.nxt_row0 = (size_t)plan->k2 * cm.blk;
-      cm.nxt.reset(cm.blk * (size_t)w);
-      coset_residue(cm.coef.p, n, w, lde_shift, plan->lg, plan->r2, cm.nxt.p, st);
+    cm.nxt_row0 = (size_t)plan->k2 * cm.blk;  // = row0 for G = 2
+    if (next_cols && !next_cols->empty() && plan->G >= 4) {
+      cm.nxt.reset(cm.blk * next_cols->size());
+      coset_residue_cols(cm.coef.p, n, *next_cols, lde_shift, plan->lg, plan->r2, cm.nxt.p, st);
+      cm.nmap.fill(0);  // columns not read at the next row: any valid column
+      for (size_t y = 0; y < next_cols->size(); y++) cm.nmap[(*next_cols)[y]] = (uint8_t)y;
     }
     return;
   }
@@ -391,7 +406,7 @@ void commit_main_impl(MainData& md, ProofScope& ps) {
   md.mainr.mats.resize(nc);
   for (int k = 0; k < nc; k++)
     lde_into(md.mainr.mats[k], dt.evals[md.order[k]].p, md.hn[k], CHIP_INFO[md.chip[k]].main_w, ONE,
-             st, &ps.ev, ps.tms, &plan, /*want_next=*/true);
+             st, &ps.ev, ps.tms, &plan, &chip_next_cols(md.chip[k]).main);
   md.mainr.commit(st);
   if (ps.ev.on) ps.ev.end(e0, st, &ps.tms->main_commit);
 }
@@ -509,7 +524,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     const uint32_t* prep = pi >= 0 ? pk.prep_evals[pi].p : nullptr;
     if (k == 0) htrace().mark("perm_rows launch");
     perm_trace(c, dt.evals[order[k]].p, prep, hn[k], pc, pe.p, cums_d.p + k, st);
-    lde_into(permr.mats[k], pe.p, hn[k], 4 * pw, ONE, st, &ev, tms, &plan, /*want_next=*/true);
+    lde_into(permr.mats[k], pe.p, hn[k], 4 * pw, ONE, st, &ev, tms, &plan, &chip_next_cols(c).perm);
   }
   permr.commit(st);
   std::vector<EF> cums(nc);
@@ -560,8 +575,10 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     const CMat& pm = permr.mats[k];
     if (k == 0) htrace().mark("quotient launch");
     if (mm.sharded) {  // this rank's points only; next rows from the next-residue shards
-      const QuotRows in{mm.rows(), mm.next_rows(), pm.rows(), pm.next_rows(), prep_lde,
-                        mm.stride(), mm.row0, mm.blk};
+      QuotRows in{mm.rows(), mm.next_rows(), pm.rows(), pm.next_rows(), prep_lde,
+                  mm.stride(), mm.row0, mm.blk, {}, {}};
+      std::copy(mm.nmap.begin(), mm.nmap.end(), in.nmain);
+      std::copy(pm.nmap.begin(), pm.nmap.end(), in.nperm);
       quotient_rows(c, in, logn + 1, qp, qv[k].p, st);
     } else {
       quotient(c, mm.lde.buf.p, prep_lde, pm.lde.buf.p, logn + 1, qp, qv[k].p, st);
@@ -869,14 +886,26 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   const int nrounds = Lmax - LOG_BLOWUP;
   DBuf<EF> betas(std::max(nrounds, 1));
   size_t len = (size_t)1 << Lmax;
+  // Every sharded round costs one subtree-root all-gather: rounds stay sharded only while
+  // h >= FRI_SHARD_MIN and the shorter tail (a few hundred thousand permutations) runs on every
+  // rank after one all-gather of the layer.
+  // (BFZ_FRI_SHARD_MIN overrides it: the tests shard small proofs' rounds too)
+  static const size_t FRI_SHARD_MIN = [] {
+    const char* e = std::getenv("BFZ_FRI_SHARD_MIN");
+    return e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)1 << 18;
+  }();
+  auto fri_sharded = [&](size_t h) { return plan.sharded(h) && h >= FRI_SHARD_MIN; };
+  auto gather = [&](DBuf<EF>& v, size_t len) {  // a row-sharded vector of len values, in place
+    DBuf<EF> all(len);
+    HIP_CHECK(hipStreamSynchronize(st));
+    shard->allgather(v.p, plan.blk(len) * sizeof(EF), all.p);
+    v = std::move(all);
+  };
   for (int rd = 0; len > ((size_t)1 << LOG_BLOWUP); rd++) {
     const size_t h = len / 2;
     FriLayer& cur = layers.back();
-    if (cur.local && !plan.sharded(h)) {
-      DBuf<EF> all(len);
-      HIP_CHECK(hipStreamSynchronize(st));
-      shard->allgather(cur.v.p, plan.blk(len) * sizeof(EF), all.p);
-      cur.v = std::move(all);
+    if (cur.local && !fri_sharded(h)) {
+      gather(cur.v, len);
       cur.e0 = 0;
       cur.local = false;
     }
@@ -885,9 +914,10 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     trees.emplace_back();
     MerkleTree& t = trees.back();
     merkle_from_rows8(t, (const uint32_t*)(cur.v.p - 2 * i0), h, st, /*fetch_root=*/false,
-                      RootChallenge{dstate.p, betas.p + rd});
+                      RootChallenge{dstate.p, betas.p + rd}, /*allow_shard=*/loc);
     DBuf<EF> next(cnt);
     const int lgh = log2i(h);
+    if (!loc && ro.count(lgh) && plan.sharded(h)) gather(ro.at(lgh), h);  // replicated tail
     const EF* add = ro.count(lgh) ? ro.at(lgh).p : nullptr;  // same range as next
     fri_fold_range(cur.v.p, next.p, h, i0, cnt, betas.p + rd, add, st);
     layers.push_back({std::move(next), i0, loc});

@@ -27,11 +27,13 @@ void quotient(int chip, const uint32_t* mainc, const uint32_t* prepc, const uint
 // pointer is indexed by the GLOBAL position: column c of main/perm at ptr[c * stride + t]
 // (a shard buffer passes its base minus its first position), prep at prep[c * N + t] (full).
 // main_l/perm_l serve the points' own rows, main_n/perm_n their next rows (i + 2); in the
-// unsharded form both are the full LDE.  qout is the full 8 x n chunk buffer; only the
+// unsharded form both are the full LDE (identity column maps); a sharded proof's next-row
+// shards hold only the columns the chip reads at the next row.  qout is the full 8 x n chunk buffer; only the
 // range's entries are written.
 struct QuotRows {
   const uint32_t *main_l, *main_n, *perm_l, *perm_n, *prep;
   size_t stride, t0, count;
+  uint8_t nmain[64], nperm[64];  // column c's next row: main_n / perm_n column nmain[c] / nperm[c]
 };
 void quotient_rows(int chip, const QuotRows& in, int logN, const QuotParams& qp, uint32_t* qout,
                    hipStream_t st);

@@ -104,7 +104,7 @@ __global__ __launch_bounds__(256, 3) void k_quotient(QuotRows in, int logN, Quot
 #pragma unroll
   for (int c = 0; c < MW; c++) {
     L[c] = in.main_l[(size_t)c * in.stride + t];
-    Nx[c] = in.main_n[(size_t)c * in.stride + tn];
+    Nx[c] = in.main_n[(size_t)in.nmain[c] * in.stride + tn];
   }
 #pragma unroll
   for (int c = 0; c < PWD; c++) {
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256, 3) void k_quotient(QuotRows in, int logN, Quot
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       pl[e].c[k] = in.perm_l[(size_t)(4 * e + k) * in.stride + t];
-      pn[e].c[k] = in.perm_n[(size_t)(4 * e + k) * in.stride + tn];
+      pn[e].c[k] = in.perm_n[(size_t)in.nperm[4 * e + k] * in.stride + tn];
     }
 
   const uint32_t x = quot_point(i, (uint32_t)n, qp.shift, twf);
@@ -166,7 +166,8 @@ static const uint32_t* sel_inv_table(int logN, const QuotParams& qp, hipStream_t
 void quotient(int chip, const uint32_t* mainc, const uint32_t* prepc, const uint32_t* permc,
               int logN, const QuotParams& qp, uint32_t* qout, hipStream_t st) {
   const size_t N = (size_t)1 << logN;
-  QuotRows in{mainc, mainc, permc, permc, prepc, N, 0, N};
+  QuotRows in{mainc, mainc, permc, permc, prepc, N, 0, N, {}, {}};
+  for (int c = 0; c < 64; c++) in.nmain[c] = in.nperm[c] = (uint8_t)c;
   quotient_rows(chip, in, logN, qp, qout, st);
 }
 

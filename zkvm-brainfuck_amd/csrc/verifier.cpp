@@ -412,4 +412,47 @@ bool verify_shard(const std::string& src, const uint32_t vk_commit[8], const Sha
   }
 }
 
+// Columns a chip's constraints read at the next row (quotient.rs:41-42), found by perturbing
+// one next-row value at a time in a random evaluation of fold_any (a column the constraints do
+// not read cannot change the folded value; one that they read changes it except with
+// probability ~1/p).  The sharded prover computes next-row shards only for these columns.
+NextCols next_row_columns(int chip) {
+  const ChipInfo& ci = CHIP_INFO[chip];
+  uint64_t seed = 0x9E3779B97F4A7C15ull * (uint64_t)(chip + 1);
+  auto rnd = [&] {
+    seed = seed * 6364136223846793005ull + 1442695040888963407ull;
+    return to_mont((uint32_t)((seed >> 33) % P));
+  };
+  auto rnd_ef = [&] { return EF{{rnd(), rnd(), rnd(), rnd()}}; };
+  auto vec = [&](size_t n) {
+    std::vector<EF> v(n);
+    for (EF& e : v) e = rnd_ef();
+    return v;
+  };
+  const size_t pw = (size_t)perm_width(chip);  // fold_any takes the perm values as EF columns
+  std::vector<EF> pl = vec(ci.prep_w), pn = vec(ci.prep_w), ml = vec(ci.main_w), mn = vec(ci.main_w),
+                  perml = vec(pw), permn = vec(pw);
+  EF pb[8];
+  for (EF& e : pb) e = rnd_ef();
+  const EF pa = rnd_ef(), cs = rnd_ef(), f = rnd_ef(), l = rnd_ef(), t = rnd_ef(), al = rnd_ef();
+  auto fold = [&] { return fold_any(chip, pl, pn, ml, mn, perml, permn, pa, pb, cs, f, l, t, al); };
+  const EF base = fold();
+  NextCols nc;
+  for (int pass = 0; pass < 2; pass++) {
+    std::vector<EF>& v = pass ? permn : mn;
+    for (size_t c = 0; c < v.size(); c++) {
+      const EF keep = v[c];
+      v[c] = ef_add(v[c], ef_one());
+      if (!ef_eq(fold(), base)) {
+        if (pass)
+          for (int k = 0; k < 4; k++) nc.perm.push_back(4 * (int)c + k);  // flatten_to_base
+        else
+          nc.main.push_back((int)c);
+      }
+      v[c] = keep;
+    }
+  }
+  return nc;
+}
+
 }  // namespace bfz

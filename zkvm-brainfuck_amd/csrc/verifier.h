@@ -6,6 +6,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "proof.h"
 
@@ -15,6 +16,12 @@ struct VerifyOptions {
   int num_queries = 84;
   bool observe_openings = true;  // PCS transcript variant (decision D1)
 };
+
+// Main and permutation (base) columns a chip's constraints read at the next row.
+struct NextCols {
+  std::vector<int> main, perm;
+};
+NextCols next_row_columns(int chip);
 
 bool verify_shard(const std::string& program_src, const uint32_t vk_commit[8], const ShardProof& pf,
                   const VerifyOptions& opt, std::string* why);
