@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void k_inv_denoms(EF z, int logH, size_t t0, s
 #ifndef BFZ_OPEN_R
 #define BFZ_OPEN_R 8
 #endif
-constexpr int OPEN_T = 256, OPEN_R = BFZ_OPEN_R, OPEN_CH = OPEN_T * OPEN_R, OPEN_CB = 32;
+constexpr int OPEN_T = 256, OPEN_R = BFZ_OPEN_R, OPEN_CH = OPEN_T * OPEN_R;
 
 __device__ __forceinline__ EF wave_sum(EF v) {
 #pragma unroll
@@ -68,20 +68,14 @@ __device__ __forceinline__ EF wave_sum(EF v) {
   return v;
 }
 
-// Sum over the 16 lanes of a DPP row (every lane of the row ends with the total).
-__device__ __forceinline__ uint32_t row_sum16(uint32_t v) {
-  v = madd(v, dpp<DPP_ROR1>(v));
-  v = madd(v, dpp<DPP_ROR2>(v));
-  v = madd(v, dpp<DPP_ROR4>(v));
-  return madd(v, dpp<DPP_ROR8>(v));
-}
-
 // Barycentric opening of one matrix at one or two points (NP):
 // partial[(chunk * w + c) * NP + k] = sum_{t in chunk} W_k,t col_c[t],  W_k,t = -x_t invd_k[t].
 // A thread owns OPEN_R rows and keeps their weights for both points in registers, so every
-// matrix element is read once for both points.  Per column the lane sums go through the
-// 16-lane DPP rows only; the 16 row sums of the block meet in LDS once per OPEN_CB columns.
-// Loads run two columns ahead (16 per thread in flight) to cover HBM latency.
+// matrix element is read once for both points.  Four column buffers form a ring (three columns
+// in flight while one is consumed).  Each thread's reduced partial of a column goes to LDS and
+// the block adds up every 4-column group cooperatively (PER threads per sum, one shuffle tree)
+// instead of a DPP row-sum chain per column and coefficient (same-box A/B: the per-column DPP
+// sums and a 2-deep prefetch were slower; so was a 4-deep prefetch with the DPP sums).
 // TAB = false: barycentric weights W_k,t = -x_t invd_k[t] over the low coset (mat = the LDE).
 // TAB = true: W_k,t = invd_k[t] read as a weight table (coefficient form: mat = a range of
 // coefficients, the table = powers of the point), logH/twf unused.
@@ -91,8 +85,6 @@ __device__ __forceinline__ void open_tile(const uint32_t* __restrict__ mat, size
                                           const EF* __restrict__ invd_b,
                                           const uint32_t* __restrict__ twf,
                                           EF* __restrict__ partial, unsigned chunk) {
-  constexpr int NROW = OPEN_T / 16;
-  __shared__ EF sh[NP][NROW][OPEN_CB];
   const size_t c0 = (size_t)chunk * OPEN_CH + threadIdx.x;
   const int nr = c0 >= n ? 0 : (int)min((size_t)OPEN_R, (n - c0 + OPEN_T - 1) / OPEN_T);
   EF W[NP][OPEN_R];
@@ -109,47 +101,50 @@ __device__ __forceinline__ void open_tile(const uint32_t* __restrict__ mat, size
     for (int k = 0; k < NP; k++)
       W[k][r] = r < nr ? ef_neg(ef_mul_base((k ? invd_b : invd_a)[t], x)) : ef_zero();
   }
-  const int row16 = threadIdx.x >> 4, lane16 = threadIdx.x & 15;
-  // two column buffers alternate: while one is consumed the other is in flight, and the
-  // consumed one is refilled two columns ahead
-  uint32_t va[OPEN_R], vb[OPEN_R];
   auto load = [&](int c, uint32_t (&v)[OPEN_R]) {
     const uint32_t* col = mat + (size_t)c * height + c0;
 #pragma unroll
     for (int r = 0; r < OPEN_R; r++) v[r] = r < nr ? col[(size_t)r * OPEN_T] : 0u;
   };
-  auto consume = [&](int cl, const uint32_t (&v)[OPEN_R]) {
+  // four column buffers in a ring: three columns stay in flight while one is consumed
+  uint32_t vr[4][OPEN_R];
 #pragma unroll
-    for (int k = 0; k < NP; k++) {
-      LazyEF lz;
-      lz.init();
+  for (int j = 0; j < 4; j++)
+    if (j < w) load(j, vr[j]);
+  __shared__ uint32_t red[NP * 4 * 4 * OPEN_T];  // [(k * 4 + col) * 4 + coef][thread]
+  constexpr int NSUM = NP * 16, PER = OPEN_T / NSUM;  // sums per group, threads per sum
+  for (int c = 0; c < w; c += 4) {
 #pragma unroll
-      for (int r = 0; r < OPEN_R; r++) lz.add(W[k][r], v[r]);
-      EF acc = lz.get();
+    for (int j = 0; j < 4; j++) {
+      if (c + j < w) {
 #pragma unroll
-      for (int e = 0; e < 4; e++) acc.c[e] = row_sum16(acc.c[e]);
-      if (lane16 == 0) sh[k][row16][cl] = acc;
-    }
-  };
-  load(0, va);
-  if (w > 1) load(1, vb);
-  for (int cb = 0; cb < w; cb += OPEN_CB) {
-    const int cw = min(OPEN_CB, w - cb);
-    for (int c = 0; c < cw; c += 2) {  // OPEN_CB is even: cb + c is even, va holds it
-      consume(c, va);
-      if (cb + c + 2 < w) load(cb + c + 2, va);
-      if (c + 1 < cw) {
-        consume(c + 1, vb);
-        if (cb + c + 3 < w) load(cb + c + 3, vb);
+        for (int k = 0; k < NP; k++) {
+          LazyEF lz;
+          lz.init();
+#pragma unroll
+          for (int r = 0; r < OPEN_R; r++) lz.add(W[k][r], vr[j][r]);
+          const EF acc = lz.get();
+#pragma unroll
+          for (int e = 0; e < 4; e++) red[((k * 4 + j) * 4 + e) * OPEN_T + threadIdx.x] = acc.c[e];
+        }
+        if (c + j + 4 < w) load(c + j + 4, vr[j]);
       }
     }
     __syncthreads();
-    if (threadIdx.x < (unsigned)(NP * cw)) {
-      const int k = threadIdx.x / cw, c = threadIdx.x % cw;
-      EF a = sh[k][0][c];
+    {  // sum q = (k * 4 + j) * 4 + e is added up by the PER threads q * PER .. q * PER + PER - 1
+      const int q = threadIdx.x / PER, part = threadIdx.x % PER;
+      const uint32_t* src = red + q * OPEN_T;
+      uint64_t a64 = 0;
+#pragma unroll 8
+      for (int i = part; i < OPEN_T; i += PER) a64 += src[i];  // < 32 p < 2^36
+      constexpr uint64_t C32 = (1u << 25) - 2;  // 2^32 mod p
+      a64 = (a64 >> 32) * C32 + (uint32_t)a64;  // < 2^32 + 2^30
+      a64 = (a64 >> 32) * C32 + (uint32_t)a64;  // < 2^32 + 2^25
+      uint32_t v = (uint32_t)(a64 >= 2ull * P ? a64 - 2ull * P : a64 >= P ? a64 - P : a64);
 #pragma unroll
-      for (int q = 1; q < NROW; q++) a = ef_add(a, sh[k][q][c]);
-      partial[((size_t)chunk * w + cb + c) * NP + k] = a;
+      for (int off = 1; off < PER; off <<= 1) v = madd(v, __shfl_xor(v, off, 64));
+      const int k = q / 16, j = (q / 4) % 4, e = q % 4;
+      if (part == 0 && c + j < w) partial[((size_t)chunk * w + c + j) * NP + k].c[e] = v;
     }
     __syncthreads();
   }
