@@ -159,6 +159,9 @@ def cpu_baseline():
     return {"value": round(secs * 1000.0, 1), "unit": "ms per 2^22-row core proof",
             "cores": threads, "kind": "port",
             "nproc": os.cpu_count(), "affinity_cpus": avail, "cpu_model": cpu_model(),
+            "threads_note": ("OMP_NUM_THREADS caps the pool: the GPU pool sets it to this job's "
+                             "CPU share (16 cores per GPU) although nproc shows the whole host"
+                             if threads < avail else "every CPU this process may use"),
             "sample": f"whole headline workload: oracle prove of FIBO_X4 stdin [255] (3,767,729 "
                       f"cycles, Cpu 2^22 rows, executor included) = {secs:.2f} s on {threads} "
                       f"OpenMP threads"}
