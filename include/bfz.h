@@ -167,10 +167,13 @@ int bfz_record_prove(const bfz_pk* pk, const bfz_record* rec, uint8_t** proof, s
 void bfz_record_free(bfz_record* rec);
 
 /* One proof sharded over `world` GPUs (one process per GPU, every rank calls this with the
- * same record): each rank hashes its subtree of every large Merkle tree (the commits and the
- * FRI commit phase, crates/stark/src/prover.rs:209-236,460-470); the ranks exchange subtree
- * roots and query openings through the callbacks (torch.distributed / RCCL on the host
- * side).  Every rank returns the same proof, byte-identical to bfz_record_prove's.  The
+ * same record): each rank computes its residue-class row shard of every large LDE, hashes its
+ * subtree of every large Merkle tree, evaluates the quotient at its points and computes its
+ * slice of the openings, reduced openings and large FRI rounds (the commits, quotient and
+ * open of crates/stark/src/prover.rs:209-236,344-470); the ranks exchange subtree roots,
+ * quotient values, opened-value slices, one FRI layer and the query openings through the
+ * callbacks (torch.distributed / RCCL on the host side).  Every rank returns the same proof,
+ * byte-identical to bfz_record_prove's.  The
  * callbacks return 0 on success.  Their buffers (send / recv / data) are DEVICE pointers on the
  * rank's GPU (the library's stream is synchronized before each call and the data must be in
  * place when the callback returns): ncclAllGather / ncclAllReduce run on them directly. */
