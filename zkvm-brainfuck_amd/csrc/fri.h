@@ -45,7 +45,7 @@ struct OpenDesc {
   uint64_t height;
   int w, logH;
   const kb::EF* invd_a;
-  const kb::EF* invd_b;
+  const kb::EF* invd_b;  // nullptr: derived from invd_a (w_n^-1 folded into scale_b, see k_reduce)
   kb::EF scale_a, scale_b;
   kb::EF* out_a;
   kb::EF* out_b;
@@ -64,10 +64,13 @@ void open_matrix(const uint32_t* mat, size_t height, int w, const kb::EF* invd_a
 void reduce_height(const RedCol* cols, const RedMat* mats, int nmats, size_t H,
                    const kb::EF* invd_a, const kb::EF* invd_b, const kb::EF& ya, const kb::EF& yb,
                    bool has_b, kb::EF* ro, hipStream_t st);
-// The same over the positions [t0, t0 + count) only; pointers indexed by the global position.
-void reduce_range(const RedCol* cols, const RedMat* mats, int nmats, size_t t0, size_t count,
-                  const kb::EF* invd_a, const kb::EF* invd_b, const kb::EF& ya, const kb::EF& yb,
-                  bool has_b, kb::EF* ro, hipStream_t st);
+// The same over the positions [t0, t0 + count) of a height-`height` LDE only; pointers indexed
+// by the global position.  invd_b == nullptr with has_b: the second point is zeta w_n and its
+// denominators are read from invd_a at the position of natural index i - 2 -- the caller has
+// folded w_n^-1 into every RedMat::kb and into yb.
+void reduce_range(const RedCol* cols, const RedMat* mats, int nmats, size_t height, size_t t0,
+                  size_t count, const kb::EF* invd_a, const kb::EF* invd_b, const kb::EF& ya,
+                  const kb::EF& yb, bool has_b, kb::EF* ro, hipStream_t st);
 void fri_fold(const kb::EF* in, kb::EF* out, size_t h, const kb::EF& beta, const kb::EF* add,
               hipStream_t st);
 uint32_t grind(const GrindState& gs, int bits, hipStream_t st);

@@ -25,6 +25,12 @@ __device__ __forceinline__ uint32_t coset_point(uint32_t t, int logH, const uint
   return mmul(to_mont_c(3), w);
 }
 
+// Position of natural index bitrev(t) - 2 in a bit-reversed vector of 2^logH values.
+__device__ __forceinline__ size_t prev2_pos(size_t t, int logH) {
+  const uint32_t mask = (uint32_t)(((size_t)1 << logH) - 1);
+  return dbitrev((dbitrev((uint32_t)t, logH) - 2u) & mask, logH);
+}
+
 constexpr int INV_CHUNK = 8;
 
 // out[t - t0] = 1 / (x_t - z) for t in [t0, t0 + count)
@@ -98,8 +104,14 @@ __device__ __forceinline__ void open_tile(const uint32_t* __restrict__ mat, size
     }
     const uint32_t x = r < nr ? coset_point((uint32_t)t, logH, twf) : 0u;
 #pragma unroll
-    for (int k = 0; k < NP; k++)
-      W[k][r] = r < nr ? ef_neg(ef_mul_base((k ? invd_b : invd_a)[t], x)) : ef_zero();
+    for (int k = 0; k < NP; k++) {
+      // invd_b == nullptr: the second point is z w_n and 1 / (x_t - z w_n) =
+      // w_n^-1 / (x_t' - z) with t' the position of natural index i - 2 (the caller folds
+      // w_n^-1 into scale_b), so the zeta table serves both points
+      const size_t tk = k && !invd_b ? prev2_pos(t, logH) : t;
+      const EF* tab = k && invd_b ? invd_b : invd_a;
+      W[k][r] = r < nr ? ef_neg(ef_mul_base(tab[tk], x)) : ef_zero();
+    }
   }
   auto load = [&](int c, uint32_t (&v)[OPEN_R]) {
     const uint32_t* col = mat + (size_t)c * height + c0;
@@ -219,12 +231,18 @@ __global__ __launch_bounds__(256) void k_open_final_batch(const OpenDesc* __rest
 }
 
 // ------------------------------------------------------------------ reduced openings
+#ifndef BFZ_RED_STEP
+#define BFZ_RED_STEP 16
+#endif
+constexpr int RED_STEP = BFZ_RED_STEP;
 // Positions [t0, t1) (a shard's range; every pointer indexed by the global position).
+// invd_b == nullptr (has_b): the second point's denominators come from the zeta table at the
+// position of natural index i - 2 (see open_tile); the caller folds w_n^-1 into kb and yb.
 __global__ __launch_bounds__(256) void k_reduce(const RedCol* __restrict__ cols,
                                                 const RedMat* __restrict__ mats, int nmats,
                                                 size_t t0, size_t t1, const EF* __restrict__ invd_a,
                                                 const EF* __restrict__ invd_b, EF ya, EF yb,
-                                                int has_b, EF* __restrict__ ro) {
+                                                int has_b, int logH, EF* __restrict__ ro) {
   for (size_t t = t0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < t1;
        t += (size_t)gridDim.x * blockDim.x) {
     EF sa = ef_zero(), sb = ef_zero();
@@ -234,12 +252,20 @@ __global__ __launch_bounds__(256) void k_reduce(const RedCol* __restrict__ cols,
       acc.init();
       const int end = rm.first + rm.count;
       int c = rm.first;
-      for (; c + 8 <= end; c += 8) {  // eight column loads in flight per step
+      for (; c + RED_STEP <= end; c += RED_STEP) {  // RED_STEP column loads in flight per step
+        uint32_t v[RED_STEP];
+#pragma unroll
+        for (int k = 0; k < RED_STEP; k++) v[k] = cols[c + k].col[t];
+#pragma unroll
+        for (int k = 0; k < RED_STEP; k++) acc.add(cols[c + k].ca, v[k]);
+      }
+      if (RED_STEP > 8 && c + 8 <= end) {
         uint32_t v[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) v[k] = cols[c + k].col[t];
 #pragma unroll
         for (int k = 0; k < 8; k++) acc.add(cols[c + k].ca, v[k]);
+        c += 8;
       }
       if (c + 4 <= end) {
         uint32_t v[4];
@@ -255,7 +281,8 @@ __global__ __launch_bounds__(256) void k_reduce(const RedCol* __restrict__ cols,
       if (rm.has_b) sb = ef_add(sb, ef_mul(s, rm.kb));
     }
     EF r = ef_mul(ef_sub(sa, ya), invd_a[t]);
-    if (has_b) r = ef_add(r, ef_mul(ef_sub(sb, yb), invd_b[t]));
+    if (has_b)
+      r = ef_add(r, ef_mul(ef_sub(sb, yb), invd_b ? invd_b[t] : invd_a[prev2_pos(t, logH)]));
     ro[t] = r;  // one launch covers every matrix of the height
   }
 }
@@ -465,15 +492,15 @@ void open_batch(std::vector<OpenDesc>& ds, int np, hipStream_t st) {
 void reduce_height(const RedCol* cols, const RedMat* mats, int nmats, size_t H, const EF* invd_a,
                    const EF* invd_b, const EF& ya, const EF& yb, bool has_b, EF* ro,
                    hipStream_t st) {
-  reduce_range(cols, mats, nmats, 0, H, invd_a, invd_b, ya, yb, has_b, ro, st);
+  reduce_range(cols, mats, nmats, H, 0, H, invd_a, invd_b, ya, yb, has_b, ro, st);
 }
 
-void reduce_range(const RedCol* cols, const RedMat* mats, int nmats, size_t t0, size_t count,
-                  const EF* invd_a, const EF* invd_b, const EF& ya, const EF& yb, bool has_b,
-                  EF* ro, hipStream_t st) {
+void reduce_range(const RedCol* cols, const RedMat* mats, int nmats, size_t height, size_t t0,
+                  size_t count, const EF* invd_a, const EF* invd_b, const EF& ya, const EF& yb,
+                  bool has_b, EF* ro, hipStream_t st) {
   const unsigned grid = std::min<unsigned>(ceil_div(count, 256), 8192);
   hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(256), 0, st, cols, mats, nmats, t0, t0 + count,
-                     invd_a, invd_b, ya, yb, has_b ? 1 : 0, ro);
+                     invd_a, invd_b, ya, yb, has_b ? 1 : 0, log2i(height), ro);
   KCHECK();
 }
 

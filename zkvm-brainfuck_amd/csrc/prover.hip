@@ -677,7 +677,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
       d.a = DBuf<EF>::borrow(invd_zeta.p, H);
     }
     const EF znext = ef_mul_base(zeta, two_adic_gen(lh - LOG_BLOWUP));
-    if (two) {
+    if (two && plan.on()) {  // single GPU: read from the zeta table (prev2_pos, fri.hip)
       d.b.reset(cnt);
       inv_denoms_range(znext, lh, t0, cnt, d.b.p, st);
     }
@@ -738,9 +738,10 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
       o.w = m.lde.width;
       o.logH = lh;
       o.invd_a = d.full_a();
-      o.invd_b = two ? d.full_b() : o.invd_a;
+      o.invd_b = two ? d.full_b() : o.invd_a;  // nullptr: derived from the zeta table
       o.scale_a = scale[0];
       o.scale_b = two ? scale[1] : scale[0];
+      if (two && !o.invd_b) o.scale_b = ef_mul_base(o.scale_b, minv(two_adic_gen(m.log_n)));
       o.out_a = out_a;
       o.out_b = two ? out_b : out_a;
       (two ? open2 : open1).push_back(o);
@@ -835,10 +836,14 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
         if (mp[r][i].npts == 2) {
           rm.has_b = 1;
           rm.kb = ef_pow(fri_alpha, (uint64_t)w);
+          // single GPU: the second point's denominators come from the zeta table times w_n^-1
+          // (reduce_range), folded in here and into yb below
+          if (!plan.on()) rm.kb = ef_mul_base(rm.kb, minv(two_adic_gen(m.log_n)));
         }
         rmats.push_back(rm);
       }
     if (cols.empty()) continue;
+    if (has_b && !plan.on()) yb = ef_mul_base(yb, minv(two_adic_gen(lh - LOG_BLOWUP)));
     red_jobs.push_back({lh, red_cols.size(), red_mats.size(), (int)rmats.size(), ya, yb, has_b});
     red_cols.insert(red_cols.end(), cols.begin(), cols.end());
     red_mats.insert(red_mats.end(), rmats.begin(), rmats.end());
@@ -854,7 +859,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     const size_t t0 = sh ? plan.row0(H) : 0, cnt = sh ? plan.blk(H) : H;
     DBuf<EF> r(cnt);
     const Invd& d = invd.at(j.lh);
-    reduce_range(red_cols_d.p + j.col0, red_mats_d.p + j.mat0, j.nmats, t0, cnt, d.pa(),
+    reduce_range(red_cols_d.p + j.col0, red_mats_d.p + j.mat0, j.nmats, H, t0, cnt, d.pa(),
                  j.has_b ? d.pb() : nullptr, j.ya, j.yb, j.has_b, r.p - t0, st);
     ro.emplace(j.lh, std::move(r));
   }
