@@ -60,3 +60,21 @@ def test_coefficient_slices_sum_to_the_opening():
     parts = [sum(c[j] * pow(z, j, P) for j in range(k * n // G, (k + 1) * n // G)) % P
              for k in range(G)]
     assert sum(parts) % P == full
+
+
+@pytest.mark.parametrize("logh", [1, 2, 3, 5])
+def test_second_point_denominators_from_the_zeta_table(logh):
+    """fri.hip prev2_pos: on an LDE of height H = 2n over 3 H_2n (bit-reversed positions),
+    1 / (x_t - z w_n) = w_n^-1 / (x_t' - z) where t' holds natural index bitrev(t) - 2."""
+    H = 1 << logh
+    wH = _gen(logh)
+    wn = pow(wH, 2, P)
+    z = 123456789
+    for t in range(H):
+        i = _brev(t, logh)
+        x = 3 * pow(wH, i, P) % P
+        t2 = _brev((i - 2) % H, logh)
+        x2 = 3 * pow(wH, _brev(t2, logh), P) % P
+        lhs = pow((x - z * wn) % P, P - 2, P)
+        rhs = pow(wn, P - 2, P) * pow((x2 - z) % P, P - 2, P) % P
+        assert lhs == rhs
