@@ -55,24 +55,15 @@ struct OpenDesc {
 // Every descriptor of ds is opened at np (1 or 2) points: one partial-sum launch over all of
 // their row chunks, one final launch over all of their columns.
 void open_batch(std::vector<OpenDesc>& ds, int np, hipStream_t st);
-// out_dev[c] = value at z of column c of a committed LDE (height = 2n), via the low coset.
-void open_matrix(const uint32_t* mat, size_t height, int w, const kb::EF* invd_a,
-                 const kb::EF& scale_a, kb::EF* out_a, const kb::EF* invd_b,
-                 const kb::EF& scale_b, kb::EF* out_b, hipStream_t st);
 // ro[t] = (sum_c ca_c v_c[t] - ya) invd_a[t] + (sum_m kb_m sum_(c in m) ca_c v_c[t] - yb) invd_b[t]
-// cols / mats: device descriptor arrays of one height (RedMat::first indexes cols).
-void reduce_height(const RedCol* cols, const RedMat* mats, int nmats, size_t H,
-                   const kb::EF* invd_a, const kb::EF* invd_b, const kb::EF& ya, const kb::EF& yb,
-                   bool has_b, kb::EF* ro, hipStream_t st);
-// The same over the positions [t0, t0 + count) of a height-`height` LDE only; pointers indexed
-// by the global position.  invd_b == nullptr with has_b: the second point is zeta w_n and its
+// for the positions [t0, t0 + count) of a height-`height` LDE (all of it, or a shard's range);
+// cols / mats: device descriptor arrays of one height (RedMat::first indexes cols); every
+// pointer is indexed by the global position.  invd_b == nullptr with has_b: the second point is zeta w_n and its
 // denominators are read from invd_a at the position of natural index i - 2 -- the caller has
 // folded w_n^-1 into every RedMat::kb and into yb.
 void reduce_range(const RedCol* cols, const RedMat* mats, int nmats, size_t height, size_t t0,
                   size_t count, const kb::EF* invd_a, const kb::EF* invd_b, const kb::EF& ya,
                   const kb::EF& yb, bool has_b, kb::EF* ro, hipStream_t st);
-void fri_fold(const kb::EF* in, kb::EF* out, size_t h, const kb::EF& beta, const kb::EF* add,
-              hipStream_t st);
 uint32_t grind(const GrindState& gs, int bits, hipStream_t st);
 // One FRI commit-phase transcript step on the device (DuplexChallenger with an empty input
 // buffer): observe the 8-word root, duplex, sample an EF (pops out[7], out[6], out[5], out[4]).

@@ -301,22 +301,6 @@ __global__ __launch_bounds__(256) void k_pow_table(EF z, size_t j0, size_t count
 }
 
 // ------------------------------------------------------------------ FRI fold
-__global__ __launch_bounds__(256) void k_fri_fold(const EF* __restrict__ in, EF* __restrict__ out,
-                                                  size_t h, int logh, EF half_beta,
-                                                  const uint32_t* __restrict__ twi,
-                                                  const EF* __restrict__ add) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= h) return;
-  // g_inv^rev(i) with g = w_(2h): twi[h + j] = w_(2h)^-j
-  const uint32_t g = twi[h + dbitrev((uint32_t)i, logh)];
-  const EF p = ef_mul_base(half_beta, g);
-  const uint32_t halfv = to_mont_c((P + 1) / 2);
-  const EF lo = in[2 * i], hi = in[2 * i + 1];
-  EF r = ef_add(ef_mul(ef_add_base(p, halfv), lo), ef_mul(ef_sub(ef_base(halfv), p), hi));
-  if (add) r = ef_add(r, add[i]);
-  out[i] = r;
-}
-
 // Outputs [i0, i0 + count) of a fold of 2h values to h; in/out/add hold that range only
 // (in: 2 count values, from 2 i0).
 __global__ __launch_bounds__(256) void k_fri_fold_dev(const EF* __restrict__ in,
@@ -433,30 +417,6 @@ void open_coefficients(const uint32_t* coef, size_t col_stride, int w, size_t co
   KCHECK();
 }
 
-void open_matrix(const uint32_t* mat, size_t height, int w, const EF* invd_a, const EF& scale_a,
-                 EF* out_a, const EF* invd_b, const EF& scale_b, EF* out_b, hipStream_t st) {
-  const size_t n = height / 2;  // low coset = first half of the bit-reversed LDE
-  const int logH = log2i(height);
-  const int nchunks = (int)ceil_div(n, OPEN_CH);
-  const int np = invd_b ? 2 : 1;
-  DBuf<EF> partial((size_t)nchunks * w * np);
-  const uint32_t* twf = (const uint32_t*)twiddles().fwd.p;
-  if (np == 2) {
-    hipLaunchKernelGGL(k_open_partial<2>, dim3(nchunks), dim3(OPEN_T), 0, st, mat, height, w, n,
-                       logH, invd_a, invd_b, twf, partial.p);
-    KCHECK();
-    hipLaunchKernelGGL(k_open_final<2>, dim3(w), dim3(256), 0, st, (const EF*)partial.p, nchunks,
-                       w, scale_a, scale_b, out_a, out_b);
-  } else {
-    hipLaunchKernelGGL(k_open_partial<1>, dim3(nchunks), dim3(OPEN_T), 0, st, mat, height, w, n,
-                       logH, invd_a, invd_a, twf, partial.p);
-    KCHECK();
-    hipLaunchKernelGGL(k_open_final<1>, dim3(w), dim3(256), 0, st, (const EF*)partial.p, nchunks,
-                       w, scale_a, scale_a, out_a, out_a);
-  }
-  KCHECK();
-}
-
 void open_batch(std::vector<OpenDesc>& ds, int np, hipStream_t st) {
   if (ds.empty()) return;
   uint32_t chunks = 0, cols = 0;
@@ -489,27 +449,12 @@ void open_batch(std::vector<OpenDesc>& ds, int np, hipStream_t st) {
   KCHECK();
 }
 
-void reduce_height(const RedCol* cols, const RedMat* mats, int nmats, size_t H, const EF* invd_a,
-                   const EF* invd_b, const EF& ya, const EF& yb, bool has_b, EF* ro,
-                   hipStream_t st) {
-  reduce_range(cols, mats, nmats, H, 0, H, invd_a, invd_b, ya, yb, has_b, ro, st);
-}
-
 void reduce_range(const RedCol* cols, const RedMat* mats, int nmats, size_t height, size_t t0,
                   size_t count, const EF* invd_a, const EF* invd_b, const EF& ya, const EF& yb,
                   bool has_b, EF* ro, hipStream_t st) {
   const unsigned grid = std::min<unsigned>(ceil_div(count, 256), 8192);
   hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(256), 0, st, cols, mats, nmats, t0, t0 + count,
                      invd_a, invd_b, ya, yb, has_b ? 1 : 0, log2i(height), ro);
-  KCHECK();
-}
-
-void fri_fold(const EF* in, EF* out, size_t h, const EF& beta, const EF* add, hipStream_t st) {
-  const int logh = log2i(h);
-  twiddles().ensure(logh + 1);
-  const EF half_beta = ef_mul_base(beta, to_mont_c((P + 1) / 2));
-  hipLaunchKernelGGL(k_fri_fold, dim3(ceil_div(h, 256)), dim3(256), 0, st, in, out, h, logh,
-                     half_beta, (const uint32_t*)twiddles().inv.p, add);
   KCHECK();
 }
 
