@@ -21,6 +21,11 @@ void ntt_passes(const uint32_t* src, uint32_t* dst, size_t src_stride, size_t ds
 // rows = evaluations of the interpolant on shift * H_2n (shift = GENERATOR / domain shift).
 void coset_lde(const uint32_t* evals, size_t n, int w, uint32_t shift, uint32_t* lde,
                hipStream_t st);
+// The same with the input columns at stride src_stride, and only_half = 0 / 1: write only
+// LDE rows [0, n) / [n, 2n) of each column (the other half is left untouched -- a quotient
+// chunk's own domain is that half, so the caller has its values already; -1: both halves).
+void coset_lde_ex(const uint32_t* evals, size_t src_stride, size_t n, int w, uint32_t shift,
+                  uint32_t* lde, int only_half, hipStream_t st);
 
 // Sharded LDE.  lde_coefficients: coef = n * (coefficients of the interpolant
 // over H_n), natural order (the iDFT alone).  coset_residue: the rank shard of the coset LDE

@@ -333,7 +333,7 @@ template <int L>
 __global__ __launch_bounds__(1 << (MidPlan<L>::b2 + MidPlan<L>::c2 - 4)) void k_lde_mid(
     const uint32_t* __restrict__ src, size_t src_stride, uint32_t* __restrict__ lde, size_t n,
     const uint32_t* __restrict__ tw_inv, const uint32_t* __restrict__ tw_fwd,
-    const uint32_t* __restrict__ pw, int B, MidPowers mp) {
+    const uint32_t* __restrict__ pw, int B, MidPowers mp, int only_half) {
   constexpr int s0 = MidPlan<L>::b1, b = MidPlan<L>::b2, c = MidPlan<L>::c2;
   extern __shared__ uint32_t lds[];
   const int tid = threadIdx.x;
@@ -383,6 +383,7 @@ __global__ __launch_bounds__(1 << (MidPlan<L>::b2 + MidPlan<L>::c2 - 4)) void k_
     const uint32_t S0 = mmul(pw[k0 & mask], pw[nb + (k0 >> B)]);
     const uint32_t T0 = mmul(pw[2 * nb + (k0 & mask)], pw[3 * nb + (k0 >> B)]);
     for (int half = 0; half < 2; half++) {
+      if (only_half >= 0 && half != only_half) continue;  // uniform across the block
       const uint32_t P0 = half ? T0 : S0;
 #pragma unroll
       for (int i = 0; i < 16; i++) x[i] = mmul(coef[i], mmul(P0, half ? mp.hi[i] : mp.lo[i]));
@@ -419,7 +420,8 @@ __global__ __launch_bounds__(1 << (MidPlan<L>::b2 + MidPlan<L>::c2 - 4)) void k_
 // lo_k = c_k * s^k / n ; hi_k = c_k * t^k / n  with s^k = SL[k & m] * SH[k >> B] (1/n in SH)
 __global__ __launch_bounds__(256) void k_scale_split(const uint32_t* __restrict__ coef,
                                                      uint32_t* __restrict__ lde, size_t n, int B,
-                                                     const uint32_t* __restrict__ pw) {
+                                                     const uint32_t* __restrict__ pw,
+                                                     int only_half) {
   const uint32_t* c = coef + (size_t)blockIdx.y * n;
   uint32_t* o = lde + (size_t)blockIdx.y * 2 * n;
   const size_t mask = ((size_t)1 << B) - 1;
@@ -432,8 +434,8 @@ __global__ __launch_bounds__(256) void k_scale_split(const uint32_t* __restrict_
        k += (size_t)gridDim.x * blockDim.x) {
     const uint32_t v = c[k];
     const size_t kl = k & mask, kh = k >> B;
-    o[k] = mmul(v, mmul(SL[kl], SH[kh]));
-    o[n + k] = mmul(v, mmul(TL[kl], TH[kh]));
+    if (only_half != 1) o[k] = mmul(v, mmul(SL[kl], SH[kh]));
+    if (only_half != 0) o[n + k] = mmul(v, mmul(TL[kl], TH[kh]));
   }
 }
 
@@ -647,7 +649,16 @@ const uint32_t* scale_tables(uint32_t shift, int L, int B) {
 
 void coset_lde(const uint32_t* evals, size_t n, int w, uint32_t shift, uint32_t* lde,
                hipStream_t st) {
+  coset_lde_ex(evals, n, n, w, shift, lde, -1, st);
+}
+
+void coset_lde_ex(const uint32_t* evals, size_t src_stride, size_t n, int w, uint32_t shift,
+                  uint32_t* lde, int only_half, hipStream_t st) {
   const int L = log2i(n);
+  // the DFT of one half: its w columns of n at stride 2n; both halves: 2w columns at stride n
+  uint32_t* dft_base = only_half >= 0 ? lde + (size_t)only_half * n : lde;
+  const size_t dft_stride = only_half >= 0 ? 2 * n : n;
+  const int dft_cols = only_half >= 0 ? w : 2 * w;
   if (L > R16_TILE_LOG) {  // iDFT pass 1 -> fused middle -> DFT last pass (3 HBM passes)
     Twiddles& T = twiddles();
     T.ensure(L);
@@ -656,7 +667,7 @@ void coset_lde(const uint32_t* evals, size_t n, int w, uint32_t shift, uint32_t*
     const R16Pass& p1 = plan[0];
     const R16Pass& p2 = plan[1];
     DBuf<uint32_t> coef(n * (size_t)w);
-    r16_launch(p1, evals, n, coef.p, n, w, L, false, st);
+    r16_launch(p1, evals, src_stride, coef.p, n, w, L, false, st);
     const int B = (L + 1) / 2;
     const uint32_t* pw = scale_tables(shift, L, B);
     MidPowers mp;
@@ -678,7 +689,8 @@ void coset_lde(const uint32_t* evals, size_t n, int w, uint32_t shift, uint32_t*
   case LL:                                                                                       \
     static_assert(MidPlan<LL>::b2 >= 4, "plan");                                                 \
     hipLaunchKernelGGL(k_lde_mid<LL>, grid, dim3(threads), ldsz * 4, st, (const uint32_t*)coef.p, \
-                       n, lde, n, (const uint32_t*)T.inv.p, (const uint32_t*)T.fwd.p, pw, B, mp); \
+                       n, lde, n, (const uint32_t*)T.inv.p, (const uint32_t*)T.fwd.p, pw, B, mp, \
+                       only_half);                                                               \
     break;
     switch (L) {
       BFZ_MID(14) BFZ_MID(15) BFZ_MID(16) BFZ_MID(17) BFZ_MID(18) BFZ_MID(19) BFZ_MID(20) BFZ_MID(21)
@@ -687,18 +699,18 @@ void coset_lde(const uint32_t* evals, size_t n, int w, uint32_t shift, uint32_t*
     }
 #undef BFZ_MID
     KCHECK();
-    if (probe.on) probe.end(ev0, st, 12.0 * (double)n * w);  // read n, write 2n
-    r16_launch(p1, lde, n, lde, n, 2 * w, L, true, st);
+    if (probe.on) probe.end(ev0, st, (only_half >= 0 ? 8.0 : 12.0) * (double)n * w);
+    r16_launch(p1, dft_base, dft_stride, dft_base, dft_stride, dft_cols, L, true, st);
     return;
   }
   DBuf<uint32_t> coef(n * (size_t)w);
-  ntt_passes(evals, coef.p, n, n, w, L, /*dif=*/false, st);
+  ntt_passes(evals, coef.p, src_stride, n, w, L, /*dif=*/false, st);
   const int B = (L + 1) / 2;
   const uint32_t* pw = scale_tables(shift, L, B);
   dim3 grid(std::min<unsigned>(ceil_div(n, 256), 4096), w);
-  hipLaunchKernelGGL(k_scale_split, grid, dim3(256), 0, st, coef.p, lde, n, B, pw);
+  hipLaunchKernelGGL(k_scale_split, grid, dim3(256), 0, st, coef.p, lde, n, B, pw, only_half);
   KCHECK();
-  ntt_passes(lde, lde, n, n, 2 * w, L, /*dif=*/true, st);
+  ntt_passes(dft_base, dft_base, dft_stride, dft_stride, dft_cols, L, /*dif=*/true, st);
   // coef goes back to the pool here; every consumer is ordered on the same stream.
 }
 

@@ -570,19 +570,43 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     qp.shift = three;
     const int pi = pk.idx_of_chip[c];
     const uint32_t* prep_lde = pi >= 0 ? pk.prep.mats[pi].lde.buf.p : nullptr;
-    qv[k].reset(8 * n);
     const CMat& mm = mainr.mats[k];
     const CMat& pm = permr.mats[k];
     if (k == 0) htrace().mark("quotient launch");
-    if (mm.sharded) {  // this rank's points only; next rows from the next-residue shards
-      QuotRows in{mm.rows(), mm.next_rows(), pm.rows(), pm.next_rows(), prep_lde,
-                  mm.stride(), mm.row0, mm.blk, {}, {}};
-      std::copy(mm.nmap.begin(), mm.nmap.end(), in.nmain);
-      std::copy(pm.nmap.begin(), pm.nmap.end(), in.nperm);
-      quotient_rows(c, in, logn + 1, qp, qv[k].p, st);
-    } else {
-      quotient(c, mm.lde.buf.p, prep_lde, pm.lde.buf.p, logn + 1, qp, qv[k].p, st);
+    if (!mm.sharded) {
+      // Chunk cc's domain 3 w_2n^cc H_n is one half of its LDE domain 3 H_2n: the kernel writes
+      // each chunk straight into that half of the chunk's LDE buffer (rows [cc n, (cc+1) n))
+      // and only the other half is computed below (coset_lde_ex).
+      const uint32_t w2n = two_adic_gen(logn + 1);
+      for (int cc = 0; cc < 2; cc++) {
+        CMat& qm = quotr.mats[2 * k + cc];
+        qm.n = n;
+        qm.log_n = logn;
+        qm.shift = mmul(three, cc ? w2n : ONE);  // split_domains: shift * g^cc
+        qm.lde.height = 2 * n;
+        qm.lde.width = 4;
+        qm.lde.buf.reset(8 * n);
+        qm.sharded = false;
+        qm.blk = 2 * n;
+        qm.row0 = 0;
+        qm.coef.free();
+        qm.nxt.free();
+        for (int j = 0; j < 64; j++) qm.nmap[j] = (uint8_t)j;
+      }
+      const size_t N = 2 * n;
+      QuotRows in{mm.lde.buf.p, mm.lde.buf.p, pm.lde.buf.p, pm.lde.buf.p, prep_lde, N, 0, N, {}, {}};
+      for (int j = 0; j < 64; j++) in.nmain[j] = in.nperm[j] = (uint8_t)j;
+      quotient_into(c, in, logn + 1, qp,
+                    QuotOut{{quotr.mats[2 * k].lde.buf.p, quotr.mats[2 * k + 1].lde.buf.p + n}, N}, st);
+      continue;
     }
+    // sharded: this rank's points only; next rows from the next-residue shards
+    qv[k].reset(8 * n);
+    QuotRows in{mm.rows(), mm.next_rows(), pm.rows(), pm.next_rows(), prep_lde,
+                mm.stride(), mm.row0, mm.blk, {}, {}};
+    std::copy(mm.nmap.begin(), mm.nmap.end(), in.nmain);
+    std::copy(pm.nmap.begin(), pm.nmap.end(), in.nperm);
+    quotient_rows(c, in, logn + 1, qp, qv[k].p, st);
   }
   if (plan.on()) gather_quotients(mainr, hn, qv, plan, *shard, st);
   for (int k = 0; k < nc; k++) {  // the next-row shards are done with
@@ -592,6 +616,21 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   for (int k = 0; k < nc; k++) {
     const size_t n = hn[k];
     const uint32_t w2n = two_adic_gen(log2i(n) + 1);
+    if (!mainr.mats[k].sharded) {  // the other half of each chunk LDE
+      for (int cc = 0; cc < 2; cc++) {
+        CMat& qm = quotr.mats[2 * k + cc];
+        const uint32_t lde_shift = mmul(to_mont(3), minv(qm.shift));  // GENERATOR / shift
+        hipEvent_t b = ev.on ? ev.begin(st) : nullptr;
+        coset_lde_ex(qm.lde.buf.p + (size_t)cc * n, 2 * n, n, 4, lde_shift, qm.lde.buf.p, 1 - cc, st);
+        if (ev.on) {
+          ev.end(b, st, &tms->lde_ms);
+          tms->lde_bytes += 8.0 * (double)n * 4;  // read n, write n
+          tms->lde_elem_stages += 2.0 * (double)n * qm.log_n * 4;
+          tms->lde_calls++;
+        }
+      }
+      continue;
+    }
     for (int cc = 0; cc < 2; cc++) {
       const uint32_t dshift = mmul(to_mont(3), cc ? w2n : ONE);  // split_domains: shift * g^cc
       lde_into(quotr.mats[2 * k + cc], qv[k].p + (size_t)4 * cc * n, n, 4, dshift, st, &ev, tms,

@@ -37,5 +37,14 @@ struct QuotRows {
 };
 void quotient_rows(int chip, const QuotRows& in, int logN, const QuotParams& qp, uint32_t* qout,
                    hipStream_t st);
+// Output placement: chunk k's coefficient column e at chunk[k] + e * stride (row = position
+// within the chunk).  qout above is {qout, qout + 4n}, stride n; the single-GPU prover writes
+// each chunk straight into its own half of the chunk's LDE buffer ({lde0, lde1 + n}, stride 2n).
+struct QuotOut {
+  uint32_t* chunk[2];
+  size_t stride;
+};
+void quotient_into(int chip, const QuotRows& in, int logN, const QuotParams& qp, const QuotOut& out,
+                   hipStream_t st);
 
 }  // namespace bfz

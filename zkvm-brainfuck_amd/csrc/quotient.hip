@@ -89,7 +89,7 @@ template <int CHIP>
 __global__ __launch_bounds__(256, 3) void k_quotient(QuotRows in, int logN, QuotParams qp,
                                                   const uint32_t* __restrict__ twf,
                                                   const uint32_t* __restrict__ sel_inv,
-                                                  uint32_t* __restrict__ qout) {
+                                                  QuotOut qo) {
   constexpr int MW = QMAIN_W[CHIP];
   constexpr int PWD = QPREP_W[CHIP] > 0 ? QPREP_W[CHIP] : 1;
   constexpr int PMW = QPERM_W[CHIP];
@@ -136,14 +136,14 @@ __global__ __launch_bounds__(256, 3) void k_quotient(QuotRows in, int logN, Quot
   const EF q = ef_mul_base(acc.value(), zh_inv);
   const size_t chunk = t >> (logN - 1), pos = t & (n - 1);
 #pragma unroll
-  for (int e = 0; e < 4; e++) qout[(chunk * 4 + e) * n + pos] = q.c[e];
+  for (int e = 0; e < 4; e++) qo.chunk[chunk][e * qo.stride + pos] = q.c[e];
 }
 
 template <int CHIP>
 static void launch_q(const QuotRows& in, int logN, const QuotParams& qp, const uint32_t* sel,
-                     uint32_t* qout, hipStream_t st) {
+                     const QuotOut& qo, hipStream_t st) {
   hipLaunchKernelGGL(k_quotient<CHIP>, dim3(ceil_div(in.count, 256)), dim3(256), 0, st, in, logN,
-                     qp, (const uint32_t*)twiddles().fwd.p, sel, qout);
+                     qp, (const uint32_t*)twiddles().fwd.p, sel, qo);
   KCHECK();
 }
 
@@ -172,6 +172,12 @@ void quotient(int chip, const uint32_t* mainc, const uint32_t* prepc, const uint
 }
 
 void quotient_rows(int chip, const QuotRows& in, int logN, const QuotParams& qp, uint32_t* qout,
+                   hipStream_t st) {
+  const size_t n = (size_t)1 << (logN - 1);
+  quotient_into(chip, in, logN, qp, QuotOut{{qout, qout + 4 * n}, n}, st);
+}
+
+void quotient_into(int chip, const QuotRows& in, int logN, const QuotParams& qp, const QuotOut& qout,
                    hipStream_t st) {
   twiddles().ensure(logN);
   const uint32_t* sel = sel_inv_table(logN, qp, st);
