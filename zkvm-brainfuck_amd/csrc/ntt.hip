@@ -103,6 +103,9 @@ constexpr SmallRoots SMALL = make_small_roots();
 #endif
 constexpr int R16_TILE_LOG = BFZ_TILE_LOG;  // 2^14 elements per tile: 1024 threads x 16
 // Second-pass tiles take 2^c adjacent columns (2^c * 4 B coalesced runs); c <= MID_CMAX.
+#ifndef BFZ_TILE_DIRECT
+#define BFZ_TILE_DIRECT 1
+#endif
 #ifndef BFZ_MID_CMAX
 #define BFZ_MID_CMAX 5
 #endif
@@ -266,14 +269,19 @@ __global__ __launch_bounds__(1 << (B - 4)) void k_ntt_tile(const uint32_t* __res
   const uint32_t* S = src + (size_t)blockIdx.y * src_stride + base;
   uint32_t* D = dst + (size_t)blockIdx.y * dst_stride + base;
   const int tpad = tid + (tid >> 4);
-#pragma unroll
-  for (int i = 0; i < 16; i++) lds[i * (T + T / 16) + tpad] = S[i * T + tid];
-  uint32_t x[16];
+  // A DIT's last window (g0 = B - 4) holds elements tid + i T: those go straight from registers
+  // to HBM (one coalesced 256-byte segment per wave instruction; -2.4% per pass).  The DIF's
+  // first window would read the same way, but measured slower than LDS staging (+4.5%,
+  // profiles/r02/ntt_lab_variants.txt), so a DIF pass keeps it.
   // BFZ_NTT_REPS (diagnostic builds only, scripts/ubench_ntt.cpp): 0 = data movement alone,
   // 2 = the stages twice, to split a pass's time into its memory and compute parts.
 #ifndef BFZ_NTT_REPS
 #define BFZ_NTT_REPS 1
 #endif
+  constexpr bool DIRECT = BFZ_TILE_DIRECT && BFZ_NTT_REPS == 1;
+  uint32_t x[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) lds[i * (T + T / 16) + tpad] = S[i * T + tid];
 #pragma nounroll
   for (int rep = 0; rep < BFZ_NTT_REPS; rep++) {
   int done_lo = 0, done_hi = B;
@@ -283,6 +291,7 @@ __global__ __launch_bounds__(1 << (B - 4)) void k_ntt_tile(const uint32_t* __res
     const uint32_t m_low = tid & ((1 << g0) - 1);
     const uint32_t m_base = m_low | ((uint32_t)(tid >> g0) << (g0 + 4));
     const uint32_t pb = m_base + (m_base >> 4);
+    const bool direct_out = DIRECT && !DIF && w == NW - 1;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 16; i++) x[i] = lds[pb + (i << g0) + ((i << g0) >> 4)];
@@ -298,13 +307,20 @@ __global__ __launch_bounds__(1 << (B - 4)) void k_ntt_tile(const uint32_t* __res
       r16_window<DIF, true>(x, g0, kk_lo, kk_hi, 0, m_low, 0, tw);
     else
       r16_window<DIF, false, true>(x, g0, kk_lo, kk_hi, 0, m_low, 0, tw);
+    if (direct_out) {
 #pragma unroll
-    for (int i = 0; i < 16; i++) lds[pb + (i << g0) + ((i << g0) >> 4)] = x[i];
+      for (int i = 0; i < 16; i++) D[i * T + tid] = x[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; i++) lds[pb + (i << g0) + ((i << g0) >> 4)] = x[i];
+    }
   }
   }
-  __syncthreads();
+  if (DIF || !DIRECT) {
+    __syncthreads();
 #pragma unroll
-  for (int i = 0; i < 16; i++) D[i * T + tid] = lds[i * (T + T / 16) + tpad];
+    for (int i = 0; i < 16; i++) D[i * T + tid] = lds[i * (T + T / 16) + tpad];
+  }
 }
 
 // Fused middle of a two-pass coset LDE (L > 14).  One tile = 2^b points at stride 2^s0 x 2^c
