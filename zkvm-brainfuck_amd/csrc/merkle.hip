@@ -9,6 +9,12 @@
 #include "merkle.h"
 #include "poseidon2.h"
 
+// Throughput Poseidon2 kernels: optional occupancy floor for A/B builds
+// (e.g. -DBFZ_P2_KATTR='__attribute__((amdgpu_waves_per_eu(8, 8)))').
+#ifndef BFZ_P2_KATTR
+#define BFZ_P2_KATTR
+#endif
+
 namespace bfz {
 
 using namespace kb;
@@ -39,7 +45,7 @@ __device__ __forceinline__ void sponge_cols(uint32_t st[16], const ColList& cl, 
 }
 
 // Rows [r0, r0 + count) (a shard's range; the whole matrix when unsharded).
-__global__ __launch_bounds__(256) void k_hash_leaves(ColList cl, size_t r0, size_t count,
+__global__ __launch_bounds__(256) BFZ_P2_KATTR void k_hash_leaves(ColList cl, size_t r0, size_t count,
                                                      uint32_t* __restrict__ out) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
@@ -102,7 +108,7 @@ __device__ __forceinline__ void store8(uint32_t* p, const uint32_t st[16]) {
 }
 
 // Nodes [j0, j0 + count) of a layer.
-__global__ __launch_bounds__(256) void k_compress(const uint32_t* __restrict__ prev, size_t j0,
+__global__ __launch_bounds__(256) BFZ_P2_KATTR void k_compress(const uint32_t* __restrict__ prev, size_t j0,
                                                   size_t count, uint32_t* __restrict__ out,
                                                   ColList inj) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -227,7 +233,7 @@ __global__ __launch_bounds__(256) void k_permute_batch(uint32_t* __restrict__ s,
   for (int k = 0; k < 16; k++) s[16 * i + k] = st[k];
 }
 
-__global__ __launch_bounds__(256) void k_hash_rows8(const uint32_t* __restrict__ rows, size_t r0,
+__global__ __launch_bounds__(256) BFZ_P2_KATTR void k_hash_rows8(const uint32_t* __restrict__ rows, size_t r0,
                                                     size_t count, uint32_t* __restrict__ out) {
   const size_t i = r0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= r0 + count) return;

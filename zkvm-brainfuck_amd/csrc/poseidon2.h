@@ -106,6 +106,12 @@ KB_HD void mds_light64(uint64_t s[16]) {
 //    |t_i| < 7p/8; the result is sum + d_i x_i in Montgomery form.  The next round's constant
 //    rides on t_0's reduction (the terminal external round's on every element after the last
 //    internal round).
+#ifndef BFZ_P2_PRE_RC
+#define BFZ_P2_PRE_RC 1
+#endif
+#ifndef BFZ_P2_SUM_CHAINS
+#define BFZ_P2_SUM_CHAINS 2
+#endif
 constexpr int32_t centred(uint32_t x) { return x > P / 2 ? (int32_t)(x - P) : (int32_t)x; }
 struct P2Signed {
   int32_t rc_init[4][16];  // centred rc R^2 (R^2-form constants)
@@ -127,6 +133,78 @@ constexpr P2Signed make_p2_signed() {
   return t;
 }
 constexpr P2Signed P2S = make_p2_signed();
+
+// Round constants moved in front of the MDS-light (BFZ_P2_PRE_RC): the MDS layer M is linear
+// and invertible, so M y + rc = M (y + K) with K = M^-1 rc (mod p).  K rides on the 64-bit
+// addend of the S-box's last product (x^3 = m a + K, one v_mad_i64_i32 either way; |K| < p/2)
+// or of the initial s * C32, and the separate 64-bit "+ rc" before each reduction is gone.
+// M^-1 = (I4 (x) M4^-1)(I - J/5): M = (I + J (x) I4)(I4 (x) M4) with J the 4 x 4 all-ones
+// block matrix, (I + J)^-1 = I - J/5 since J^2 = 4J.
+struct P2Pre {
+  int32_t init0[16];     // M^-1 rc_init[0], added to s * C32
+  int32_t init[4][16];   // round r's S-box addend: M^-1 rc_init[r+1]; r = 3: M^-1 (rc_int[0] e0)
+  int32_t term[4][16];   // M^-1 rc_term[r+1]; r = 3: none
+};
+constexpr uint32_t cmul_mod(uint32_t a, uint32_t b) { return (uint32_t)((uint64_t)a * b % P); }
+constexpr void m4_inverse(uint32_t inv[4][4]) {
+  constexpr uint32_t m4[4][4] = {{2, 3, 1, 1}, {1, 2, 3, 1}, {1, 1, 2, 3}, {3, 1, 1, 2}};
+  uint32_t a[4][8] = {};
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 4; j++) {
+      a[i][j] = m4[i][j];
+      a[i][4 + j] = i == j;
+    }
+  for (int c = 0; c < 4; c++) {
+    int piv = c;
+    while (a[piv][c] == 0) piv++;
+    for (int j = 0; j < 8; j++) {
+      const uint32_t t = a[c][j];
+      a[c][j] = a[piv][j];
+      a[piv][j] = t;
+    }
+    const uint32_t iv = cpow(a[c][c], P - 2);
+    for (int j = 0; j < 8; j++) a[c][j] = cmul_mod(a[c][j], iv);
+    for (int i = 0; i < 4; i++)
+      if (i != c && a[i][c]) {
+        const uint32_t f = a[i][c];
+        for (int j = 0; j < 8; j++) a[i][j] = (a[i][j] + P - cmul_mod(f, a[c][j])) % P;
+      }
+  }
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 4; j++) inv[i][j] = a[i][4 + j];
+}
+// canonical residues in, centred M^-1 v out
+constexpr void mds_light_inverse(const uint32_t v[16], int32_t out[16]) {
+  uint32_t inv[4][4] = {};
+  m4_inverse(inv);
+  const uint32_t inv5 = cpow(5, P - 2);
+  uint32_t w[16] = {};
+  for (int k = 0; k < 4; k++) {
+    uint64_t sum = 0;
+    for (int b = 0; b < 4; b++) sum += v[4 * b + k];
+    const uint32_t s5 = cmul_mod((uint32_t)(sum % P), inv5);
+    for (int b = 0; b < 4; b++) w[4 * b + k] = (v[4 * b + k] + P - s5) % P;
+  }
+  for (int b = 0; b < 4; b++)
+    for (int i = 0; i < 4; i++) {
+      uint64_t acc = 0;
+      for (int j = 0; j < 4; j++) acc += (uint64_t)inv[i][j] * w[4 * b + j] % P;
+      out[4 * b + i] = centred((uint32_t)(acc % P));
+    }
+}
+constexpr P2Pre make_p2_pre() {
+  P2Pre t{};
+  mds_light_inverse(P2.ext_init_r2[0], t.init0);
+  for (int r = 0; r < 3; r++) {
+    mds_light_inverse(P2.ext_init_r2[r + 1], t.init[r]);
+    mds_light_inverse(P2.ext_term_r2[r + 1], t.term[r]);
+  }
+  uint32_t e0[16] = {};
+  e0[0] = to_mont_c(P2.internal[0]);  // rc_int[0] in R^2 form
+  mds_light_inverse(e0, t.init[3]);
+  return t;
+}
+constexpr P2Pre P2PRE = make_p2_pre();
 
 // The diagonal entries d_i R include powers of two, and a sum of int32 terms into 64 bits
 // sign-extends each term; the compiler would turn d * t + acc into 64-bit shifts and
@@ -203,9 +281,35 @@ KB_HD void external_rounds_s(const int32_t a[16], int64_t y[16], const int32_t (
     mds_light64(u);
   }
 }
+// The same with the constants already in front of the MDS layers (P2Pre): round r's S-box
+// output gets K[r] (the M^-1 image of the constant the reduction after its MDS would add).
+KB_HD void external_rounds_pre(const int32_t a[16], int64_t y[16], const int32_t (&K)[4][16]) {
+  uint64_t* u = reinterpret_cast<uint64_t*>(y);
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const int32_t x = r ? mred_s(y[i]) : a[i];
+      const int64_t c3 = (int64_t)mred_s((int64_t)x * x) * x + K[r][i];
+      y[i] = fold_s(c3);
+    }
+    mds_light64(u);
+  }
+}
 KB_HD void poseidon2_permute(uint32_t s[16]) {
   int64_t y[16];
   int32_t t[16];
+#if BFZ_P2_PRE_RC
+  // initial MDS-light on x R^2 + M^-1 rc_0 (s C32 < 2^56, rows sum to 35: < 2^61.2)
+#pragma unroll
+  for (int i = 0; i < 16; i++) y[i] = (int64_t)((uint64_t)s[i] * C32) + P2PRE.init0[i];
+  mds_light64(reinterpret_cast<uint64_t*>(y));
+#pragma unroll
+  for (int i = 0; i < 16; i++) t[i] = mred_s(y[i]);
+  external_rounds_pre(t, y, P2PRE.init);
+#pragma unroll
+  for (int i = 0; i < 16; i++) t[i] = mred_s(y[i]);  // rc_int[0] already in y[0]
+#else
   // initial MDS-light on x R^2 (s C32 < 2^56, rows sum to 35: < 2^61.2)
 #pragma unroll
   for (int i = 0; i < 16; i++) y[i] = (int64_t)((uint64_t)s[i] * C32);
@@ -215,9 +319,22 @@ KB_HD void poseidon2_permute(uint32_t s[16]) {
   external_rounds_s(t, y, P2S.rc_init);
 #pragma unroll
   for (int i = 0; i < 16; i++) t[i] = mred_s(i == 0 ? y[i] + P2S.rc_int[0] : y[i]);
+#endif
 #pragma unroll
   for (int r = 0; r < 13; r++) {
     const int32_t c = mred_s(cube_s(t[0]));
+#if BFZ_P2_SUM_CHAINS == 2
+    // two multiply-add chains of 8 that start from a product, not from a sign-extended
+    // element (ashr + mov + 64-bit add per chain otherwise)
+    int64_t part[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      part[k] = (int64_t)P2M.one[8 * k] * (k ? t[8] : c);
+#pragma unroll
+      for (int i = 8 * k + 1; i < 8 * k + 8; i++) part[k] = (int64_t)P2M.one[i] * t[i] + part[k];
+    }
+    const int32_t sp = mred_s(part[0] + part[1]);
+#else
     int64_t part[4];  // four independent multiply-add chains
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -226,6 +343,7 @@ KB_HD void poseidon2_permute(uint32_t s[16]) {
       for (int i = 4 * k + 1; i < 4 * k + 4; i++) part[k] = (int64_t)P2M.one[i] * t[i] + part[k];
     }
     const int32_t sp = mred_s((part[0] + part[1]) + (part[2] + part[3]));
+#endif
     if (r < 12) {
       const int64_t q = opaque64((int64_t)P2M.k * sp);  // one product, not one per element
       t[0] = mred_s((int64_t)P2M.d[0] * c + (q + P2S.rc_int[r + 1]));
@@ -238,7 +356,11 @@ KB_HD void poseidon2_permute(uint32_t s[16]) {
       for (int i = 1; i < 16; i++) t[i] = mred_s((int64_t)P2M.d[i] * t[i] + (q + P2S.rc_term[0][i]));
     }
   }
+#if BFZ_P2_PRE_RC
+  external_rounds_pre(t, y, P2PRE.term);
+#else
   external_rounds_s(t, y, P2S.rc_term);
+#endif
 #pragma unroll
   for (int i = 0; i < 16; i++) {
     const uint32_t r = (uint32_t)mred_s(y[i]);
