@@ -32,15 +32,15 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # min, 64-bit adds) count as 2.  scripts/ubench_valu.hip measures 75 T for v_sub/v_xor.
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 # Full-rate-equivalent VALU lane-ops of one Poseidon2 permutation in k_permute_batch
-# (gfx950 ISA instruction mix, profiles/r01/poseidon2_isa_mix.txt).
-P2_UNITS_PER_PERM = 5548
+# (gfx950 ISA instruction mix, profiles/r02/poseidon2_isa_mix.txt).
+P2_UNITS_PER_PERM = 5205
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02", "pmc_summary.json")
 
 
 # VALU units (full-rate lane-ops) per radix-2 element-stage of a 2^22 coset LDE, from the gfx950
 # ISA of k_ntt_tile<false,14> + k_lde_mid<22> + k_ntt_tile<true,14> (scripts/ntt_isa.py ->
 # profiles/r02/ntt_isa_mix.txt).  Smaller chips' LDEs use the same kernels' shapes within ~5%.
-NTT_UNITS_PER_ELEM_STAGE = 7.064
+NTT_UNITS_PER_ELEM_STAGE = 7.006
 
 
 def ntt_traffic():
