@@ -253,6 +253,22 @@ def sharded_latency(dist, pk, rec, rank, world, device, ref_proof, steps=3):
         return {"error": f"{type(e).__name__}: {e}"}
 
 
+def sustained(step, seconds, sync):
+    """Proofs back to back for about `seconds` after the timed steps (same record, same
+    stream): the steady-state rate over many proofs, and a GPU phase long enough for a
+    utilisation sampler polling every few seconds to see the device busy."""
+    sync()
+    t0 = time.perf_counter()
+    k = 0
+    while time.perf_counter() - t0 < seconds:
+        step()
+        k += 1
+    sync()
+    wall = time.perf_counter() - t0
+    return {"proofs": k, "seconds": round(wall, 3), "ms_per_proof": round(wall * 1e3 / max(k, 1), 3),
+            "what": "back-to-back proofs of the same record after the timed steps (one rank)"}
+
+
 def timed_steps(step, steps, dist=None, sync=lambda: None):
     """Runs `step` exactly `steps` times between barrier + device synchronize on both sides
     and returns ms per step, the max over ranks (every rank proves its own replica; the
@@ -336,6 +352,9 @@ def main():
                          "sharded: one proof split across all ranks (strong scaling); "
                          "pcs: column-sharded commit + FRI of a synthetic trace (BASELINE "
                          "configs 4/5, strong scaling)")
+    ap.add_argument("--sustain-s", type=float, default=8.0,
+                    help="replicas mode: seconds of back-to-back proofs after the timed steps "
+                         "(0 = skip)")
     ap.add_argument("--log-n", type=int, default=24, help="pcs mode: trace rows = 2^log_n")
     ap.add_argument("--cols", type=int, default=64, help="pcs mode: trace columns")
     args = ap.parse_args()
@@ -411,6 +430,9 @@ def main():
 
     ms = timed_steps(lambda: one(), args.steps, dist, sync=lambda: _lib.check(L.bfz_synchronize()))
     extra = {}
+    if not sharded and args.sustain_s > 0:
+        extra["sustained"] = sustained(lambda: one(), args.sustain_s,
+                                       sync=lambda: _lib.check(L.bfz_synchronize()))
     if world > 1 and not sharded and not args.no_extra:  # every rank takes part
         extra["sharded_proof"] = sharded_latency(dist, pk, rec, rank, world, device, proof)
 
@@ -445,6 +467,8 @@ def main():
             "poseidon2": poseidon2_roofline(tm),
             "proof_bytes": len(proof),
         }
+        if "sustained" in extra:
+            line["sustained"] = extra["sustained"]
         if world > 1 and not sharded and not args.no_extra and "sharded_proof" in extra:
             line["sharded_proof"] = extra["sharded_proof"]
         if world == 1 and not args.no_extra:

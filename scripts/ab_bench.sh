@@ -10,7 +10,7 @@ for rep in 1 2; do
   for so in "$@"; do
     v=$(basename $so .so)
     cp "$so" zkvm-brainfuck_amd/libbfz.so
-    timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extra > gpurun_out/ab_${v}_$rep.json 2>gpurun_out/ab_${v}_$rep.err || { cp /tmp/libbfz_orig.so zkvm-brainfuck_amd/libbfz.so; exit 1; }
+    timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extra --sustain-s 0 > gpurun_out/ab_${v}_$rep.json 2>gpurun_out/ab_${v}_$rep.err || { cp /tmp/libbfz_orig.so zkvm-brainfuck_amd/libbfz.so; exit 1; }
     python3 -c "import json;d=json.load(open('gpurun_out/ab_${v}_$rep.json'));s=d['stages_ms'];print('$v', d['value'], 'ntt', s['ntt_kernel_ms'], 'open', s['open_ms'], 'fri', s['fri_ms'], 'quot', s['quotient_ms'], 'p2', s['p2_kernel_ms'])"
   done
 done

@@ -11,9 +11,9 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 timeout -k 10 400 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
-  -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-extra > gpurun_out/prof.log 2>&1 && \
+  -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-extra --sustain-s 0 > gpurun_out/prof.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/kt -o run \
-  -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extra > gpurun_out/kt.log 2>&1 && \
+  -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extra --sustain-s 0 > gpurun_out/kt.log 2>&1 && \
 python3 scripts/timeline.py gpurun_out/kt/run_kernel_trace.csv > gpurun_out/timeline.txt && \
 bash scripts/gpu_pmc.sh > gpurun_out/pmc.out 2>&1 && \
 bash scripts/gpu_sq.sh > gpurun_out/sq.out 2>&1 && \
