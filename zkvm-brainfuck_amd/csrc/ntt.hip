@@ -255,7 +255,13 @@ __global__ __launch_bounds__(1024) void k_ntt_r16(const uint32_t* __restrict__ s
 template <int G0>
 __device__ __forceinline__ constexpr int tile_off(int i) { return (i << G0) + ((i << G0) >> 4); }
 
-template <bool DIF, int B>
+// DIN (DIT only): the first window (g0 = 0) holds the 16 consecutive words tid*16 + i, read
+// straight from HBM as four 16-byte loads (no LDS staging, one barrier fewer); the launch picks
+// it when the source rows are 16-byte aligned.
+#ifndef BFZ_TILE_DIRECT_IN
+#define BFZ_TILE_DIRECT_IN 1
+#endif
+template <bool DIF, int B, bool DIN = false>
 __global__ __launch_bounds__(1 << (B - 4)) void k_ntt_tile(const uint32_t* __restrict__ src,
                                                            uint32_t* __restrict__ dst,
                                                            size_t src_stride, size_t dst_stride,
@@ -279,9 +285,19 @@ __global__ __launch_bounds__(1 << (B - 4)) void k_ntt_tile(const uint32_t* __res
 #define BFZ_NTT_REPS 1
 #endif
   constexpr bool DIRECT = BFZ_TILE_DIRECT && BFZ_NTT_REPS == 1;
+  static_assert(!DIN || (!DIF && BFZ_NTT_REPS == 1), "direct first window: DIT passes only");
   uint32_t x[16];
+  if constexpr (DIN) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(S + (tid << 4));
 #pragma unroll
-  for (int i = 0; i < 16; i++) lds[i * (T + T / 16) + tpad] = S[i * T + tid];
+    for (int q = 0; q < 4; q++) {
+      const uint4 v = s4[q];
+      x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; i++) lds[i * (T + T / 16) + tpad] = S[i * T + tid];
+  }
 #pragma nounroll
   for (int rep = 0; rep < BFZ_NTT_REPS; rep++) {
   int done_lo = 0, done_hi = B;
@@ -292,9 +308,11 @@ __global__ __launch_bounds__(1 << (B - 4)) void k_ntt_tile(const uint32_t* __res
     const uint32_t m_base = m_low | ((uint32_t)(tid >> g0) << (g0 + 4));
     const uint32_t pb = m_base + (m_base >> 4);
     const bool direct_out = DIRECT && !DIF && w == NW - 1;
-    __syncthreads();
+    if (!DIN || w > 0) {
+      __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 16; i++) x[i] = lds[pb + (i << g0) + ((i << g0) >> 4)];
+      for (int i = 0; i < 16; i++) x[i] = lds[pb + (i << g0) + ((i << g0) >> 4)];
+    }
     int kk_lo = 0, kk_hi = 4;
     if (DIF) {
       kk_hi = done_hi - g0 < 4 ? done_hi - g0 : 4;
@@ -534,6 +552,8 @@ static void r16_attrs() {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<false, R16_TILE_LOG>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<false, R16_TILE_LOG, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   done = true;
 }
 
@@ -541,6 +561,13 @@ template <bool DIF, int B>
 static void tile_launch(dim3 grid, const uint32_t* in, size_t is, uint32_t* dst, size_t ds,
                         const uint32_t* tw, hipStream_t st) {
   const size_t lds = ((size_t)1 << B) + ((size_t)1 << (B - 4));
+  if constexpr (!DIF && BFZ_TILE_DIRECT_IN && BFZ_NTT_REPS == 1) {
+    if (((uintptr_t)in & 15) == 0 && (is & 3) == 0) {
+      hipLaunchKernelGGL((k_ntt_tile<false, B, true>), grid, dim3(1 << (B - 4)), lds * 4, st, in,
+                         dst, is, ds, tw);
+      return;
+    }
+  }
   hipLaunchKernelGGL((k_ntt_tile<DIF, B>), grid, dim3(1 << (B - 4)), lds * 4, st, in, dst, is, ds,
                      tw);
 }
