@@ -33,7 +33,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 # Full-rate-equivalent VALU lane-ops of one Poseidon2 permutation in k_permute_batch
 # (gfx950 ISA instruction mix, profiles/r02/poseidon2_isa_mix.txt).
-P2_UNITS_PER_PERM = 5205
+P2_UNITS_PER_PERM = 5133
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02", "pmc_summary.json")
 
 

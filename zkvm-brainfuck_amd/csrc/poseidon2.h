@@ -109,6 +109,9 @@ KB_HD void mds_light64(uint64_t s[16]) {
 #ifndef BFZ_P2_PRE_RC
 #define BFZ_P2_PRE_RC 1
 #endif
+#ifndef BFZ_P2_LAZY_DIAG
+#define BFZ_P2_LAZY_DIAG 1
+#endif
 #ifndef BFZ_P2_SUM_CHAINS
 #define BFZ_P2_SUM_CHAINS 2
 #endif
@@ -216,12 +219,14 @@ struct P2Mul {
   int32_t d[16];
   int32_t k;
   int32_t one[16];
+  int32_t dd[16];  // centred d_i R^2 (a plain value times it is R^2-form)
 };
 constexpr P2Mul make_p2_mul() {
   P2Mul m{};
   for (int i = 0; i < 16; i++) {
     m.d[i] = P2S.d[i];
     m.one[i] = 1;
+    m.dd[i] = centred(to_mont_c(P2.diag[i]));
   }
   m.k = P2S.k;
   return m;
@@ -256,6 +261,18 @@ KB_HD int32_t mred_s(int64_t y) {
 #else  // host (transcript, verifier): the same residue as hi(y) - hi(m' p), m' = -m
   const uint32_t mh = (uint32_t)(((int64_t)(int32_t)(0u - (uint32_t)m) * (int64_t)P) >> 32);
   return (int32_t)((uint32_t)((uint64_t)y >> 32) - mh);
+#endif
+}
+// (a << sh) + b in one v_lshl_add_u64 (the compiler turns a small-constant multiple of a
+// 64-bit value into v_mad_u64_u32 pairs and moves otherwise)
+template <int SH>
+KB_HD int64_t lshl_add64(int64_t a, int64_t b) {
+#ifdef __HIP_DEVICE_COMPILE__
+  int64_t r;
+  asm("v_lshl_add_u64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "n"(SH), "v"(b));
+  return r;
+#else
+  return (int64_t)(((uint64_t)a << SH) + (uint64_t)b);
 #endif
 }
 // a = x R, |a| < p  ->  x^3 R^2 (mod p), |.| < p^2
@@ -320,6 +337,52 @@ KB_HD void poseidon2_permute(uint32_t s[16]) {
 #pragma unroll
   for (int i = 0; i < 16; i++) t[i] = mred_s(i == 0 ? y[i] + P2S.rc_int[0] : y[i]);
 #endif
+#if BFZ_P2_LAZY_DIAG
+  // Elements 1, 2, 4, 5 (d = 1, 2, 3, 4) stay unreduced 64-bit R-form values through rounds
+  // 0..11: u <- d u + T_R with T_R = reduce(q) the R-form round sum (|T_R| < p/2 + 2^28), a
+  // 64-bit shift-add instead of multiply + reduction.  Growth: |u_5| < 4^12 2^30.2 + 4^12 p/6
+  // < 2^54.7, so every sum stays below 2^58 (mred_s needs < 2^62).  Round 12 reduces them to
+  // plain values x = reduce(u) and applies d_i R^2 x + q + rc, the other elements' form.
+  int64_t u1 = t[1], u2 = t[2], u4 = t[4], u5 = t[5];
+#pragma unroll
+  for (int r = 0; r < 13; r++) {
+    const int32_t c = mred_s(cube_s(t[0]));
+    int64_t part[2];
+    part[0] = (int64_t)P2M.one[0] * c;
+    part[0] = (int64_t)P2M.one[3] * t[3] + part[0];
+    part[0] = (int64_t)P2M.one[6] * t[6] + part[0];
+    part[0] = (int64_t)P2M.one[7] * t[7] + part[0];
+    part[0] = part[0] + u1;
+    part[0] = part[0] + u2;
+    part[1] = (int64_t)P2M.one[8] * t[8];
+#pragma unroll
+    for (int i = 9; i < 16; i++) part[1] = (int64_t)P2M.one[i] * t[i] + part[1];
+    part[1] = part[1] + u4;
+    part[1] = part[1] + u5;
+    const int32_t sp = mred_s(part[0] + part[1]);
+    const int64_t q = opaque64((int64_t)P2M.k * sp);
+    if (r < 12) {
+      const int64_t tr = (int64_t)mred_s(q);
+      t[0] = mred_s((int64_t)P2M.d[0] * c + (q + P2S.rc_int[r + 1]));
+#pragma unroll
+      for (int i = 3; i < 16; i++)
+        if (i != 4 && i != 5) t[i] = mred_s((int64_t)P2M.d[i] * t[i] + q);
+      u1 = lshl_add64<0>(u1, tr);
+      u2 = lshl_add64<1>(u2, tr);
+      u4 = lshl_add64<0>(lshl_add64<1>(u4, u4), tr);
+      u5 = lshl_add64<2>(u5, tr);
+    } else {
+      t[0] = mred_s((int64_t)P2M.d[0] * c + (q + P2S.rc_term[0][0]));
+#pragma unroll
+      for (int i = 3; i < 16; i++)
+        if (i != 4 && i != 5) t[i] = mred_s((int64_t)P2M.d[i] * t[i] + (q + P2S.rc_term[0][i]));
+      t[1] = mred_s((int64_t)P2M.dd[1] * mred_s(u1) + (q + P2S.rc_term[0][1]));
+      t[2] = mred_s((int64_t)P2M.dd[2] * mred_s(u2) + (q + P2S.rc_term[0][2]));
+      t[4] = mred_s((int64_t)P2M.dd[4] * mred_s(u4) + (q + P2S.rc_term[0][4]));
+      t[5] = mred_s((int64_t)P2M.dd[5] * mred_s(u5) + (q + P2S.rc_term[0][5]));
+    }
+  }
+#else
 #pragma unroll
   for (int r = 0; r < 13; r++) {
     const int32_t c = mred_s(cube_s(t[0]));
@@ -356,6 +419,7 @@ KB_HD void poseidon2_permute(uint32_t s[16]) {
       for (int i = 1; i < 16; i++) t[i] = mred_s((int64_t)P2M.d[i] * t[i] + (q + P2S.rc_term[0][i]));
     }
   }
+#endif
 #if BFZ_P2_PRE_RC
   external_rounds_pre(t, y, P2PRE.term);
 #else
