@@ -45,6 +45,22 @@ def test_poseidon2_batch_parity():
         assert np.array_equal(got, exp)
 
 
+def test_poseidon2_extreme_states_parity():
+    """The lazy forms' bounds (signed state, unreduced 64-bit internal diagonal elements,
+    poseidon2.h) at the edges: device words (Montgomery form) 0, 1, p - 1, (p +- 1)/2 and
+    alternating extremes, then 2^18 random states."""
+    edge = [np.zeros(16), np.full(16, P - 1), np.ones(16), np.tile([P - 1, 0], 8),
+            np.tile([0, P - 1], 8), np.full(16, (P - 1) // 2), np.full(16, (P + 1) // 2),
+            np.arange(P - 16, P), np.tile([P - 1, 1], 8)]
+    rng = np.random.default_rng(7)
+    words = np.concatenate([np.array(edge, dtype=np.uint64),
+                            rng.integers(0, P, size=(1 << 18, 16), dtype=np.uint64)]).astype(np.uint32)
+    dev = words.reshape(-1).copy()
+    _lib.check(_lib.lib().bfz_poseidon2_permute(dev.ctypes.data_as(P32), len(words)))
+    exp = O.poseidon2(unmont(words).reshape(-1)).reshape(-1, 16)
+    assert np.array_equal(unmont(dev).reshape(-1, 16), exp)
+
+
 def test_poseidon2_lane_mode_parity():
     """16-lanes-per-state permutation (DPP cross-lane MDS) == oracle."""
     rng = np.random.default_rng(3)
