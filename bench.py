@@ -38,9 +38,9 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02", "pmc_summary.json")
 
 
 # VALU units (full-rate lane-ops) per radix-2 element-stage of a 2^22 coset LDE, from the gfx950
-# ISA of k_ntt_tile<false,14> + k_lde_mid<22> + k_ntt_tile<true,14> (scripts/ntt_isa.py ->
+# ISA of k_ntt_tile<false,14,true> + k_lde_mid<22> + k_ntt_tile<true,14> (scripts/ntt_isa.py ->
 # profiles/r02/ntt_isa_mix.txt).  Smaller chips' LDEs use the same kernels' shapes within ~5%.
-NTT_UNITS_PER_ELEM_STAGE = 7.006
+NTT_UNITS_PER_ELEM_STAGE = 7.023
 
 
 def ntt_traffic():

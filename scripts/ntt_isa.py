@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """VALU cost of a 2^L coset LDE per radix-2 element-stage, from the gfx950 ISA of the three
 kernels one LDE launches (ntt.hip coset_lde, L > 14):
-  k_ntt_tile<false,14>  iDFT stages 0..13 over n elements          (16 elements / thread)
+  k_ntt_tile<false,14,true>  iDFT stages 0..13 over n elements     (16 elements / thread)
   k_lde_mid<L>          iDFT stages 14..L-1, coset scale, DFT stages L-1..14 of both halves
                         (16 input elements / thread, 32 outputs)
   k_ntt_tile<true,14>   DFT stages 13..0 over the 2n outputs        (16 elements / thread)
@@ -24,7 +24,9 @@ def main():
     L = int(sys.argv[1]) if len(sys.argv) > 1 else 22
     txt = isa_mix.compile_asm(os.path.join(ROOT, "zkvm-brainfuck_amd", "csrc", "ntt.hip"))
     names = isa_mix.kernels(txt)
-    tile_dit = [k for k in names if k.startswith("_ZN3bfz10k_ntt_tileILb0ELi14E")][0]
+    # the DIT pass the LDE launches reads its first window straight from HBM (DIN = true)
+    dit = [k for k in names if k.startswith("_ZN3bfz10k_ntt_tileILb0ELi14ELb1E")]
+    tile_dit = (dit or [k for k in names if k.startswith("_ZN3bfz10k_ntt_tileILb0ELi14E")])[0]
     tile_dif = [k for k in names if k.startswith("_ZN3bfz10k_ntt_tileILb1ELi14E")][0]
     mid = [k for k in names if k.startswith(f"_ZN3bfz9k_lde_midILi{L}E")][0]
     b2 = L - 14
