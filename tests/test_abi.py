@@ -151,6 +151,59 @@ def test_verifier_rejects_out_of_range_log_degree_and_round_count():
         c.verify(sdk.BfProofWithPublicValues(proof=_tampered(pf, short_commit), stdin=b""), vk)
 
 
+def test_verifier_fuzz_rejects_every_mutation():
+    """(f)3 as a fuzz target: 300 seeded mutations of a valid proof (bit flips, words set to
+    0 / 1 / p-1 / p / 2^31 / 2^32-1 / random, inserted words, truncations, header words) are
+    each rejected with an error -- no crash, no accepted variant (the local-only chips' unopened
+    next values included, see verifier.cpp)."""
+    import random
+    prog = guests.HELLO
+    pf = O.prove(prog, [])
+    vk = _vk(prog)
+    c = sdk.ProverClient()
+    rng = random.Random(2024)
+    specials = [0, 1, 0x7F000000, 0x7F000001, 0x80000000, 0xFFFFFFFF]
+    tried = 0
+    while tried < 300:
+        b = bytearray(pf)
+        kind = rng.randrange(5)
+        if kind == 0:
+            b[rng.randrange(len(b))] ^= 1 << rng.randrange(8)
+        elif kind == 1:
+            o = rng.randrange(len(b) // 4) * 4
+            b[o:o + 4] = struct.pack("<I", rng.choice(specials + [rng.getrandbits(32)]))
+        elif kind == 2:
+            b = b[:rng.randrange(len(b))]
+        elif kind == 3:
+            o = rng.randrange(len(b) // 4) * 4
+            b[o:o] = struct.pack("<I", rng.getrandbits(32))
+        else:
+            o = rng.randrange(min(len(b) // 4, 256)) * 4
+            b[o:o + 4] = struct.pack("<I", rng.choice(specials + [2, 0x10000, rng.getrandbits(32)]))
+        if bytes(b) == pf:
+            continue
+        tried += 1
+        with pytest.raises(_lib.BfzError):
+            c.verify(sdk.BfProofWithPublicValues(proof=bytes(b), stdin=b""), vk)
+
+
+def test_verifier_rejects_nonzero_next_of_local_only_chips():
+    """Normal form: the reference prover writes zero next values for local-only chips
+    (prover.rs:484-487); they are not opened, so only the normal-form check catches them."""
+    prog = guests.HELLO
+    pf = O.prove(prog, [])
+    m = BR.parse_bfz1(pf)
+    local = [i for i, o in enumerate(m["opened"]) if not any(any(x) for x in o["main_next"])]
+    assert local, "hello has local-only chips (AddSub, Jump, IO)"
+
+    def poke(mm):
+        mm["opened"][local[0]]["main_next"][0][0] = 1
+
+    with pytest.raises(_lib.BfzError, match="local-only chip"):
+        sdk.ProverClient().verify(
+            sdk.BfProofWithPublicValues(proof=_tampered(pf, poke), stdin=b""), _vk(prog))
+
+
 def test_pcs_variant_switch_is_consistent():
     """Decision D1: with the opened values kept out of the transcript, the
     oracle's proof differs, and each verifier accepts exactly the proofs of its own variant."""

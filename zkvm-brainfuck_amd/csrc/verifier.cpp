@@ -209,6 +209,16 @@ bool verify_shard(const std::string& src, const uint32_t vk_commit[8], const Sha
           c.perml.size() != 4 * (size_t)perm_width(ch) || c.permn.size() != c.perml.size() ||
           c.pl.size() != pw || c.pn.size() != pw || c.q[0].size() != 4 || c.q[1].size() != 4)
         throw std::runtime_error("opened-value shape mismatch");
+      // A local-only chip's next values are not opened by the PCS (verifier.rs:109-135), so
+      // the reference verifier would accept any words there; its prover writes zeros
+      // (prover.rs:484-487, 499-502).  Requiring the zeros keeps accepted proofs
+      // non-malleable (tests/test_abi.py fuzz) and rejects nothing an honest prover emits.
+      if (CHIP_INFO[ch].local_only) {
+        for (const std::vector<EF>* v : {&c.pn, &c.mn})
+          for (const EF& e : *v)
+            if (e.c[0] | e.c[1] | e.c[2] | e.c[3])
+              throw std::runtime_error("local-only chip with non-zero next values");
+      }
     }
     // BfProver::verify: Cpu chip present, log degree bound
     int cpu_i = -1;
