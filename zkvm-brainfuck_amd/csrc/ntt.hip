@@ -80,11 +80,11 @@ constexpr uint32_t root_pow2(int k) {  // w_(2^k), canonical
   return g;
 }
 struct SmallRoots {
-  uint32_t f[16], i[16];  // [2^k + l] = w_(2^(k+1))^(+-l), k = 0..3 (Montgomery)
+  uint32_t f[32], i[32];  // [2^k + l] = w_(2^(k+1))^(+-l), k = 0..4 (Montgomery)
 };
 constexpr SmallRoots make_small_roots() {
   SmallRoots r{};
-  for (int k = 0; k < 4; k++) {
+  for (int k = 0; k < 5; k++) {
     const uint32_t w = root_pow2(k + 1), wi = cpow(w, P - 2);
     uint32_t a = 1, b = 1;
     for (int l = 0; l < (1 << k); l++) {
@@ -127,34 +127,36 @@ __device__ __forceinline__ int lds_pad(int idx, int c) { return c < 5 ? idx + (i
 // TW_LOAD: read every twiddle of the stage from the table (tile kernels: s0 = lo_g = 0, the
 // table slice below 2^14 is L2-resident) instead of multiplying one loaded base by the small
 // roots -- a load replaces a Montgomery product.
-template <bool DIF, bool CONST_TW, bool TW_LOAD = false>
-__device__ __forceinline__ void r16_window(uint32_t (&x)[16], int g0, int kk_lo, int kk_hi, int s0,
+// R = 5 (tile kernels, BFZ_TILE_R): 32 elements per thread, windows of 5 stages.
+template <bool DIF, bool CONST_TW, bool TW_LOAD = false, int R = 4>
+__device__ __forceinline__ void r16_window(uint32_t (&x)[1 << R], int g0, int kk_lo, int kk_hi, int s0,
                                            uint32_t m_low, uint32_t lo_g, const uint32_t* __restrict__ tw) {
   // performs stages t = g0 + kk for kk in [kk_lo, kk_hi), ascending (DIT) or descending (DIF)
+  constexpr int E = 1 << R, H = E / 2;
 #pragma unroll
-  for (int q = 0; q < 4; q++) {
-    const int kk = DIF ? 3 - q : q;
+  for (int q = 0; q < R; q++) {
+    const int kk = DIF ? R - 1 - q : q;
     if (kk < kk_lo || kk >= kk_hi) continue;
-    uint32_t tws[8];
+    uint32_t tws[H];
     if (CONST_TW) {
 #pragma unroll
-      for (int l = 0; l < 8; l++)
+      for (int l = 0; l < H; l++)
         if (l < (1 << kk)) tws[l] = DIF ? SMALL.f[(1 << kk) + l] : SMALL.i[(1 << kk) + l];
     } else if (TW_LOAD) {  // one table load per twiddle instead of a load and a multiply
       const uint32_t* tt = tw + (1u << (s0 + g0 + kk)) + ((size_t)m_low << s0) + lo_g;
 #pragma unroll
-      for (int l = 0; l < 8; l++)
+      for (int l = 0; l < H; l++)
         if (l < (1 << kk)) tws[l] = tt[(size_t)l << (g0 + s0)];
     } else {
       const int t = g0 + kk;
       const uint32_t wb = tw[(1u << (s0 + t)) + (m_low << s0) + lo_g];
 #pragma unroll
-      for (int l = 0; l < 8; l++)
+      for (int l = 0; l < H; l++)
         if (l < (1 << kk))
           tws[l] = l == 0 ? wb : mmul(wb, DIF ? SMALL.f[(1 << kk) + l] : SMALL.i[(1 << kk) + l]);
     }
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
+    for (int i = 0; i < E; i++) {
       if (i & (1 << kk)) continue;
       const int j = i | (1 << kk);
       const int l = i & ((1 << kk) - 1);
@@ -166,7 +168,7 @@ __device__ __forceinline__ void r16_window(uint32_t (&x)[16], int g0, int kk_lo,
         x[j] = unit ? msub(u, v) : mmul_s((int32_t)(u - v), w);
       } else {
         const uint32_t vw = unit ? umin(v, v - P) : mmul(v, w);
-        const bool lazy = kk < 3 && ((i >> (kk + 1)) & 1);
+        const bool lazy = kk < R - 1 && ((i >> (kk + 1)) & 1);
         const uint32_t s_ = u + vw, d = u - vw;
         x[i] = lazy ? s_ : umin(s_, s_ - P);
         x[j] = lazy ? d + P : umin(d, d + P);
@@ -261,21 +263,34 @@ __device__ __forceinline__ constexpr int tile_off(int i) { return (i << G0) + ((
 #ifndef BFZ_TILE_DIRECT_IN
 #define BFZ_TILE_DIRECT_IN 1
 #endif
-template <bool DIF, int B, bool DIN = false>
-__global__ __launch_bounds__(1 << (B - 4)) void k_ntt_tile(const uint32_t* __restrict__ src,
+// R (BFZ_TILE_R): 2^R elements per thread and R stages per register window; R = 5 takes a
+// 2^14 tile in three windows (5 + 5 + 4 stages) and two LDS exchanges instead of four windows
+// (4 + 4 + 4 + 2) and three exchanges, at 512 threads and 32 elements per thread.
+#ifndef BFZ_TILE_R
+#define BFZ_TILE_R 4
+#endif
+#ifndef BFZ_TILE_R_DIT
+#define BFZ_TILE_R_DIT BFZ_TILE_R
+#endif
+#ifndef BFZ_TILE_R_DIF
+#define BFZ_TILE_R_DIF BFZ_TILE_R
+#endif
+template <bool DIF, int B, bool DIN = false, int R = 4>
+__global__ __launch_bounds__(1 << (B - R)) void k_ntt_tile(const uint32_t* __restrict__ src,
                                                            uint32_t* __restrict__ dst,
                                                            size_t src_stride, size_t dst_stride,
                                                            const uint32_t* __restrict__ tw) {
   static_assert(B >= 8 && B <= R16_TILE_LOG, "tile");
-  constexpr int T = 1 << (B - 4);
-  constexpr int NW = (B + 3) / 4;
+  constexpr int E = 1 << R;  // elements per thread
+  constexpr int T = 1 << (B - R);
+  constexpr int NW = (B + R - 1) / R;
   extern __shared__ uint32_t lds[];
   const int tid = threadIdx.x;
   const size_t base = (size_t)blockIdx.x << B;
   const uint32_t* S = src + (size_t)blockIdx.y * src_stride + base;
   uint32_t* D = dst + (size_t)blockIdx.y * dst_stride + base;
-  const int tpad = tid + (tid >> 4);
-  // A DIT's last window (g0 = B - 4) holds elements tid + i T: those go straight from registers
+  const int tpad = tid + (tid >> R);
+  // A DIT's last window (g0 = B - R) holds elements tid + i T: those go straight from registers
   // to HBM (one coalesced 256-byte segment per wave instruction; -2.4% per pass).  The DIF's
   // first window would read the same way, but measured slower than LDS staging (+4.5%,
   // profiles/r02/ntt_lab_variants.txt), so a DIF pass keeps it.
@@ -286,58 +301,58 @@ __global__ __launch_bounds__(1 << (B - 4)) void k_ntt_tile(const uint32_t* __res
 #endif
   constexpr bool DIRECT = BFZ_TILE_DIRECT && BFZ_NTT_REPS == 1;
   static_assert(!DIN || (!DIF && BFZ_NTT_REPS == 1), "direct first window: DIT passes only");
-  uint32_t x[16];
+  uint32_t x[E];
   if constexpr (DIN) {
-    const uint4* s4 = reinterpret_cast<const uint4*>(S + (tid << 4));
+    const uint4* s4 = reinterpret_cast<const uint4*>(S + (tid << R));
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
+    for (int q = 0; q < E / 4; q++) {
       const uint4 v = s4[q];
       x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
     }
   } else {
 #pragma unroll
-    for (int i = 0; i < 16; i++) lds[i * (T + T / 16) + tpad] = S[i * T + tid];
+    for (int i = 0; i < E; i++) lds[i * (T + T / E) + tpad] = S[i * T + tid];
   }
 #pragma nounroll
   for (int rep = 0; rep < BFZ_NTT_REPS; rep++) {
   int done_lo = 0, done_hi = B;
 #pragma unroll
   for (int w = 0; w < NW; w++) {
-    const int g0 = DIF ? (B - 4 - 4 * w > 0 ? B - 4 - 4 * w : 0) : (4 * w < B - 4 ? 4 * w : B - 4);
+    const int g0 = DIF ? (B - R - R * w > 0 ? B - R - R * w : 0) : (R * w < B - R ? R * w : B - R);
     const uint32_t m_low = tid & ((1 << g0) - 1);
-    const uint32_t m_base = m_low | ((uint32_t)(tid >> g0) << (g0 + 4));
-    const uint32_t pb = m_base + (m_base >> 4);
+    const uint32_t m_base = m_low | ((uint32_t)(tid >> g0) << (g0 + R));
+    const uint32_t pb = m_base + (m_base >> R);
     const bool direct_out = DIRECT && !DIF && w == NW - 1;
     if (!DIN || w > 0) {
       __syncthreads();
 #pragma unroll
-      for (int i = 0; i < 16; i++) x[i] = lds[pb + (i << g0) + ((i << g0) >> 4)];
+      for (int i = 0; i < E; i++) x[i] = lds[pb + (i << g0) + ((i << g0) >> R)];
     }
-    int kk_lo = 0, kk_hi = 4;
+    int kk_lo = 0, kk_hi = R;
     if (DIF) {
-      kk_hi = done_hi - g0 < 4 ? done_hi - g0 : 4;
+      kk_hi = done_hi - g0 < R ? done_hi - g0 : R;
       done_hi = g0;
     } else {
       kk_lo = done_lo - g0 > 0 ? done_lo - g0 : 0;
-      done_lo = g0 + 4;
+      done_lo = g0 + R;
     }
     if (g0 == 0)
-      r16_window<DIF, true>(x, g0, kk_lo, kk_hi, 0, m_low, 0, tw);
+      r16_window<DIF, true, false, R>(x, g0, kk_lo, kk_hi, 0, m_low, 0, tw);
     else
-      r16_window<DIF, false, true>(x, g0, kk_lo, kk_hi, 0, m_low, 0, tw);
+      r16_window<DIF, false, true, R>(x, g0, kk_lo, kk_hi, 0, m_low, 0, tw);
     if (direct_out) {
 #pragma unroll
-      for (int i = 0; i < 16; i++) D[i * T + tid] = x[i];
+      for (int i = 0; i < E; i++) D[i * T + tid] = x[i];
     } else {
 #pragma unroll
-      for (int i = 0; i < 16; i++) lds[pb + (i << g0) + ((i << g0) >> 4)] = x[i];
+      for (int i = 0; i < E; i++) lds[pb + (i << g0) + ((i << g0) >> R)] = x[i];
     }
   }
   }
   if (DIF || !DIRECT) {
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 16; i++) D[i * T + tid] = lds[i * (T + T / 16) + tpad];
+    for (int i = 0; i < E; i++) D[i * T + tid] = lds[i * (T + T / E) + tpad];
   }
 }
 
@@ -548,11 +563,11 @@ static void r16_attrs() {
                         (const void*)&k_lde_mid<23>};
   for (const void* f : mids)
     HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<true, R16_TILE_LOG>),
+  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<true, R16_TILE_LOG, false, BFZ_TILE_R_DIF>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<false, R16_TILE_LOG>),
+  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<false, R16_TILE_LOG, false, BFZ_TILE_R_DIT>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<false, R16_TILE_LOG, true>),
+  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<false, R16_TILE_LOG, true, BFZ_TILE_R_DIT>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   done = true;
 }
@@ -560,15 +575,18 @@ static void r16_attrs() {
 template <bool DIF, int B>
 static void tile_launch(dim3 grid, const uint32_t* in, size_t is, uint32_t* dst, size_t ds,
                         const uint32_t* tw, hipStream_t st) {
-  const size_t lds = ((size_t)1 << B) + ((size_t)1 << (B - 4));
+  // the full-size tile takes BFZ_TILE_R; smaller tiles (short columns) stay radix-16
+  constexpr int R = B == R16_TILE_LOG ? (DIF ? BFZ_TILE_R_DIF : BFZ_TILE_R_DIT) : 4;
+  const size_t lds = ((size_t)1 << B) + ((size_t)1 << (B - R));
+  const dim3 block(1 << (B - R));
   if constexpr (!DIF && BFZ_TILE_DIRECT_IN && BFZ_NTT_REPS == 1) {
     if (((uintptr_t)in & 15) == 0 && (is & 3) == 0) {
-      hipLaunchKernelGGL((k_ntt_tile<false, B, true>), grid, dim3(1 << (B - 4)), lds * 4, st, in,
-                         dst, is, ds, tw);
+      hipLaunchKernelGGL((k_ntt_tile<false, B, true, R>), grid, block, lds * 4, st, in, dst, is,
+                         ds, tw);
       return;
     }
   }
-  hipLaunchKernelGGL((k_ntt_tile<DIF, B>), grid, dim3(1 << (B - 4)), lds * 4, st, in, dst, is, ds,
+  hipLaunchKernelGGL((k_ntt_tile<DIF, B, false, R>), grid, block, lds * 4, st, in, dst, is, ds,
                      tw);
 }
 
