@@ -2,7 +2,9 @@
 #include "gpu.h"
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -74,10 +76,69 @@ void upload_async(void* dst, const void* src, size_t bytes, hipStream_t st) {
 // through two pinned buffers, each filled by several host threads while the DMA of the other
 // is in flight, so the copy runs near the PCIe rate instead of the runtime's synchronous
 // pageable path.  Returns when the data is on the device.
+// Host-to-pinned staging copies split over a persistent set of threads (spawning 8 threads per
+// 32 MB chunk cost about as much as the chunk's DMA).  The pool lives for the process; its
+// threads sleep between copies.
+namespace {
+class CopyPool {
+ public:
+  explicit CopyPool(int nthreads) : nt_(nthreads) {
+    for (int i = 1; i < nt_; i++) th_.emplace_back([this, i] { loop(i); });
+  }
+  // dst[0..n) = src[0..n), the caller's thread taking share 0
+  void copy(uint8_t* dst, const uint8_t* src, size_t n) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      dst_ = dst;
+      src_ = src;
+      n_ = n;
+      per_ = (n + nt_ - 1) / nt_;
+      pending_ = nt_ - 1;
+      gen_++;
+    }
+    cv_.notify_all();
+    part(0);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [this] { return pending_ == 0; });
+  }
+
+ private:
+  void part(int i) {
+    const size_t a = (size_t)i * per_;
+    if (a < n_) std::memcpy(dst_ + a, src_ + a, std::min(per_, n_ - a));
+  }
+  void loop(int i) {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+      }
+      part(i);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--pending_ == 0) done_.notify_all();
+    }
+  }
+  const int nt_;
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  uint8_t* dst_ = nullptr;
+  const uint8_t* src_ = nullptr;
+  size_t n_ = 0, per_ = 0;
+  int pending_ = 0;
+  uint64_t gen_ = 0;
+};
+}  // namespace
+
 void upload_bulk(void* dst, const void* src, size_t bytes, hipStream_t st) {
   if (!bytes) return;
   constexpr size_t CHUNK = (size_t)32 << 20;
-  constexpr int NTHR = 8;
+#ifndef BFZ_UPLOAD_THREADS
+#define BFZ_UPLOAD_THREADS 8
+#endif
+  constexpr int NTHR = BFZ_UPLOAD_THREADS;
   struct Bulk {
     uint8_t* buf[2] = {nullptr, nullptr};
     hipEvent_t done[2];
@@ -90,6 +151,7 @@ void upload_bulk(void* dst, const void* src, size_t bytes, hipStream_t st) {
     }
     return x;
   }();
+  static CopyPool* pool = new CopyPool(NTHR);  // never destroyed: its threads end with the process
   if (bytes <= ((size_t)1 << 20)) {  // small: one staged copy
     const uint8_t* s = static_cast<const uint8_t*>(src);
     HIP_CHECK(hipEventSynchronize(b->done[0]));
@@ -105,15 +167,7 @@ void upload_bulk(void* dst, const void* src, size_t bytes, hipStream_t st) {
   for (size_t off = 0; off < bytes; off += CHUNK, k ^= 1) {
     const size_t n = std::min(CHUNK, bytes - off);
     HIP_CHECK(hipEventSynchronize(b->done[k]));  // buffer k's previous DMA has finished
-    std::vector<std::thread> th;
-    const size_t per = (n + NTHR - 1) / NTHR;
-    for (int t = 0; t < NTHR; t++) {
-      const size_t a = t * per;
-      if (a >= n) break;
-      const size_t len = std::min(per, n - a);
-      th.emplace_back([=] { std::memcpy(b->buf[k] + a, s + off + a, len); });
-    }
-    for (auto& t : th) t.join();
+    pool->copy(b->buf[k], s + off, n);
     HIP_CHECK(hipMemcpyAsync(d + off, b->buf[k], n, hipMemcpyHostToDevice, st));
     HIP_CHECK(hipEventRecord(b->done[k], st));
   }
