@@ -244,26 +244,7 @@ def _events(elf, stdin, executor):
     return _lib.take_bytes(p, ln.value)
 
 
-def _random_program(rng, size):
-    """A random balanced Brainfuck program that halts: loops always start with a '-' ... ']'
-    body that decrements the cell it tests, over a bounded tape excursion."""
-    out = []
-    for _ in range(size):
-        r = rng.random()
-        if r < 0.25:
-            out.append("+" * rng.integers(1, 6))
-        elif r < 0.35:
-            out.append("-")
-        elif r < 0.55:
-            out.append(">" if rng.random() < 0.6 else "<")
-        elif r < 0.65:
-            out.append(".")
-        elif r < 0.7:
-            out.append(",")
-        else:
-            k = int(rng.integers(1, 4))
-            out.append("[-" + ">" * k + "+" + "<" * k + "]")
-    return "".join(out)
+from bfgen import random_program as _random_program  # noqa: E402
 
 
 @pytest.mark.parametrize("prog,stdin", [(p, s) for _, p, s in guests.REFERENCE_PROGRAMS]

@@ -271,6 +271,36 @@ def test_fibo17_end_to_end_sdk(client):
     client.verify(proof, vk)
 
 
+def test_random_programs_bytes_match_oracle(client):
+    """Whole-proof parity beyond the reference programs: 16 seeded random halting programs
+    (I/O, memory excursions, nested loops; some chips empty) give the oracle's bytes, and both
+    verifiers accept them."""
+    from bfgen import random_program
+    rng = np.random.default_rng(11)
+    for k in range(16):
+        prog = random_program(rng, int(rng.integers(3, 120)), allow_negative=False)
+        stdin = [int(x) for x in rng.integers(0, 256, size=prog.count(","))]
+        pk, vk = client.setup(prog)
+        pf = client.prove(pk, stdin).run()
+        assert pf.proof == O.prove(prog, stdin), (k, prog)
+        client.verify(pf, vk)
+        assert O.verify(prog, pf.proof), (k, prog)
+
+
+def test_pointer_below_zero_matches_reference_behaviour(client):
+    """The reference executor wraps the memory pointer (u32, executor.rs:137-138) but its
+    MemoryInstrs AIR range-checks it as a field word (air.rs:37-61): a program stepping below
+    cell 0 executes and 'proves', and every verifier rejects the proof.  bfz reproduces that
+    byte for byte (no early error the reference would not raise)."""
+    prog, stdin = "<+.>,[->+<]>.", [7]
+    pk, vk = client.setup(prog)
+    pf = client.prove(pk, stdin).run()
+    assert pf.proof == O.prove(prog, stdin)
+    assert not O.verify(prog, pf.proof)
+    with pytest.raises(_lib.BfzError, match="OOD evaluation mismatch on chip MemoryInstrs"):
+        client.verify(pf, vk)
+
+
 def test_fibo255_2pow20_parity(client):
     """fibonacci trace 2^20 rows (BASELINE config 3): full pipeline, bit-exact vs oracle."""
     pk, vk = client.setup(guests.FIBO)
