@@ -62,8 +62,14 @@ __device__ __forceinline__ void batch_frac(const uint32_t (&pr)[PWD], const uint
   }
 }
 
+// Optional occupancy floor for A/B builds (the Cpu instance holds ~246 VGPRs: 2 waves/SIMD),
+// e.g. -DBFZ_PERM_KATTR='__attribute__((amdgpu_waves_per_eu(3)))'.
+#ifndef BFZ_PERM_KATTR
+#define BFZ_PERM_KATTR
+#endif
+
 template <int CHIP>
-__global__ __launch_bounds__(256) void k_perm_rows(const uint32_t* __restrict__ mainc,
+__global__ __launch_bounds__(256) BFZ_PERM_KATTR void k_perm_rows(const uint32_t* __restrict__ mainc,
                                                    const uint32_t* __restrict__ prepc, size_t n,
                                                    PermChallenges ch, uint32_t* __restrict__ perm,
                                                    EF* __restrict__ rowsum) {
