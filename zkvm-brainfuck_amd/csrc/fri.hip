@@ -449,10 +449,13 @@ void open_batch(std::vector<OpenDesc>& ds, int np, hipStream_t st) {
   KCHECK();
 }
 
+#ifndef BFZ_RED_GRID  // k_reduce's grid-stride cap in workgroups (A/B builds)
+#define BFZ_RED_GRID 32768
+#endif
 void reduce_range(const RedCol* cols, const RedMat* mats, int nmats, size_t height, size_t t0,
                   size_t count, const EF* invd_a, const EF* invd_b, const EF& ya, const EF& yb,
                   bool has_b, EF* ro, hipStream_t st) {
-  const unsigned grid = std::min<unsigned>(ceil_div(count, 256), 8192);
+  const unsigned grid = std::min<unsigned>(ceil_div(count, 256), BFZ_RED_GRID);
   hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(256), 0, st, cols, mats, nmats, t0, t0 + count,
                      invd_a, invd_b, ya, yb, has_b ? 1 : 0, log2i(height), ro);
   KCHECK();
