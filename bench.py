@@ -226,6 +226,40 @@ def drop_in_path(pk, prog, stdin, ref_proof, steps=3):
                     f"{nbytes / 1e9:.2f} GB) incl. upload + transpose + proof"}
 
 
+def events_path(pk, prog, stdin, ref_proof, steps=3):
+    """The Rust HipProver::prove path: the reference record's event vectors (Executor::run's
+    ExecutionRecord, in the bfz_*_event layout, pageable host memory) -> bfz_record_from_events
+    (upload, memory events sorted, validation) -> bfz_record_prove (device trace generation +
+    proof).  The executor runs before the timed region, as it does before MachineProver::prove
+    (utils/prove.rs:38-44)."""
+    import ctypes
+    import time as _t
+    from bfz import _lib as _l, events as _e
+    rec = _e.ExecutionRecordArrays.from_executor(prog, stdin)
+
+    def one():
+        drec = _e.record_from_events(pk, rec)
+        ptr = ctypes.POINTER(ctypes.c_uint8)()
+        plen = ctypes.c_size_t()
+        _l.check(_l.lib().bfz_record_prove(ctypes.c_void_p(pk.handle), ctypes.c_void_p(drec.handle),
+                                           ctypes.byref(ptr), ctypes.byref(plen), None))
+        return _l.take_bytes(ptr, plen.value)
+
+    one()  # warm
+    times = []
+    for _ in range(steps):
+        t0 = _t.perf_counter()
+        pf = one()
+        times.append((_t.perf_counter() - t0) * 1e3)
+    assert pf == ref_proof, "events-path proof differs from the record path"
+    nbytes = sum(int(getattr(rec, k).nbytes) for k in ("cpu", "add", "sub", "jump", "io",
+                                                       "memory_instr", "memory"))
+    return {"ms": round(min(times), 3), "event_bytes": nbytes,
+            "what": "bfz_record_from_events (the reference ExecutionRecord's events from pageable "
+                    f"host memory, {nbytes / 1e6:.0f} MB) + bfz_record_prove: the Rust "
+                    "HipProver::prove path, upload included"}
+
+
 def sharded_latency(dist, pk, rec, rank, world, device, ref_proof, steps=3):
     """Latency of ONE proof split over all ranks (bfz_record_prove_sharded: every rank hashes
     its subtree of each large Merkle tree; the subtree roots are all-gathered and the query
@@ -473,6 +507,7 @@ def main():
             line["sharded_proof"] = extra["sharded_proof"]
         if world == 1 and not args.no_extra:
             line["end_to_end"] = end_to_end(client, pk, prog, stdin)
+            line["events_path"] = events_path(pk, prog, stdin, proof)
             line["drop_in_path"] = drop_in_path(pk, prog, stdin, proof)
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is timed at N=1 only
             try:

@@ -1,40 +1,53 @@
 //! `HipProver`: the reference's `MachineProver` trait (crates/stark/src/prover.rs:27-150)
-//! implemented over libbfz, the MI355X core prover.  Every method maps to one C ABI call:
+//! implemented over libbfz, the MI355X core prover.  Every method maps to C ABI calls:
 //!
-//! | trait method (reference)                     | libbfz                                   |
-//! |----------------------------------------------|------------------------------------------|
-//! | `setup` (prover.rs:49, machine.rs:154-224)   | `bfz_setup` (cached per program)          |
-//! | `commit` (prover.rs:209-236)                 | `bfz_main_commit` -> `bfz_main_data`      |
-//! | `observe_into` (prover.rs:595-601)           | native Rust (same as StarkProvingKey)     |
-//! | `open` (prover.rs:242-553)                   | `bfz_open` + `bfz_proof_to_bincode`       |
-//! | `prove` (prover.rs:560-582)                  | generate_dependencies + commit + open     |
+//! | trait method (reference)                        | libbfz                                      |
+//! |-------------------------------------------------|---------------------------------------------|
+//! | `setup` (prover.rs:49, machine.rs:154-224)      | host `StarkMachine::setup` + `pk_to_device`  |
+//! | `pk_to_device` (prover.rs:52,201-203)           | `bfz_pk_from_host` (checked against commit) |
+//! | `pk_to_host` (prover.rs:55,205-207)             | the host key kept beside the handle         |
+//! | `commit` (prover.rs:209-236)                    | `bfz_main_commit` -> `bfz_main_data`         |
+//! | `observe_into` (prover.rs:595-601)              | native Rust (same as StarkProvingKey)       |
+//! | `open` (prover.rs:242-553)                      | `bfz_open` + `bfz_proof_to_bincode`          |
+//! | `prove` (prover.rs:560-582)                     | `bfz_record_from_events` + record commit + open |
+//!
+//! `prove` overrides the default: instead of `generate_dependencies` + `generate_traces` on the
+//! host and a 1 GB trace upload, the record's event vectors (~50 B per cycle) go to the device,
+//! where every chip trace and the byte-lookup multiplicities are generated.
 //!
 //! The proof comes back as the reference's own bincode `ShardProof<KoalaBearPoseidon2>` bytes
 //! (bfz_proof_to_bincode, `FIELD_MONTGOMERY`), so `bincode::deserialize` yields the exact type
 //! `StarkMachine::verify` takes: no hand-written decoder on the Rust side.
 //!
-//! Not compiled here: the binding mirrors `zkvm-brainfuck_amd/bfz/sdk.py`
-//! (`CoreProver.commit / observe_into / open / prove`), which the GPU tests exercise.
+//! Selection: this crate does not depend on bf-prover (bf-prover depends on it behind its `hip`
+//! feature, which points `DefaultProverComponents::CoreProver` here; see
+//! crates/reference-patch/ and INTEGRATION.md).
+//!
+//! Not compiled here (no Rust toolchain in this image): the binding mirrors
+//! `zkvm-brainfuck_amd/bfz/sdk.py` (`BfProver`, `CoreProver`), which the GPU tests exercise.
 use std::ffi::CString;
 use std::os::raw::c_int;
 
+use bf_core_executor::events::MemoryRecordEnum;
 use bf_core_executor::{ExecutionRecord, Opcode, Program};
 use bf_core_machine::brainfuck::BfAir;
-use bf_prover::components::BfProverComponents;
 use bf_stark::koala_bear_poseidon2::KoalaBearPoseidon2;
 use bf_stark::{
     Challenger, Com, DebugConstraintBuilder, MachineProof, MachineProver, MachineProvingKey,
-    MachineRecord, ShardMainData, ShardProof, StarkGenericConfig, StarkMachine, StarkProvingKey,
+    ShardMainData, ShardProof, StarkGenericConfig, StarkMachine, StarkProvingKey,
     StarkVerifyingKey,
 };
 use bfz_sys as sys;
+use hashbrown::HashMap;
+use p3_air::Air;
 use p3_challenger::CanObserve;
-use p3_field::{FieldAlgebra, PrimeField32};
+use p3_field::FieldAlgebra;
 use p3_koala_bear::KoalaBear;
 use p3_matrix::{dense::RowMajorMatrix, Matrix};
+use p3_maybe_rayon::prelude::*;
 
 type SC = KoalaBearPoseidon2;
-type Air = BfAir<KoalaBear>;
+type A = BfAir<KoalaBear>;
 
 /// BfAir::chips() order (crates/core/machine/src/brainfuck/mod.rs:53-81) = chip id in the ABI.
 pub const CHIPS: [&str; 8] =
@@ -67,6 +80,10 @@ pub fn program_source(p: &Program) -> String {
 fn words<T>(v: &[T]) -> &[u32] {
     assert_eq!(core::mem::size_of::<T>(), 4);
     unsafe { core::slice::from_raw_parts(v.as_ptr() as *const u32, v.len()) }
+}
+fn field_words(w: &[u32]) -> Vec<KoalaBear> {
+    assert_eq!(core::mem::size_of::<KoalaBear>(), 4);
+    w.iter().map(|&x| unsafe { core::mem::transmute::<u32, KoalaBear>(x) }).collect()
 }
 
 #[derive(Debug, Clone, Copy)]
@@ -114,8 +131,16 @@ impl Drop for HipMainData {
     }
 }
 
+/// An `ExecutionRecord`'s events resident in HBM (bfz_record), freed on drop.
+struct HipRecord(*mut sys::bfz_record);
+impl Drop for HipRecord {
+    fn drop(&mut self) {
+        unsafe { sys::bfz_record_free(self.0) }
+    }
+}
+
 pub struct HipProver {
-    machine: StarkMachine<SC, Air>,
+    machine: StarkMachine<SC, A>,
 }
 
 fn to_c(ch: &Challenger<SC>) -> sys::bfz_challenger {
@@ -129,36 +154,201 @@ fn to_c(ch: &Challenger<SC>) -> sys::bfz_challenger {
     c
 }
 
-impl MachineProver<SC, Air> for HipProver {
+fn from_c(c: &sys::bfz_challenger, ch: &mut Challenger<SC>) {
+    let st = field_words(&c.sponge_state);
+    ch.sponge_state.copy_from_slice(&st);
+    ch.input_buffer = field_words(&c.input_buffer[..c.n_input as usize]);
+    ch.output_buffer = field_words(&c.output_buffer[..c.n_output as usize]);
+}
+
+fn access(a: &Option<MemoryRecordEnum>) -> sys::bfz_memory_access {
+    match a {
+        None => sys::bfz_memory_access::default(),
+        Some(MemoryRecordEnum::Read(r)) => sys::bfz_memory_access {
+            kind: 1,
+            value: r.value,
+            prev_value: 0,
+            _pad: 0,
+            timestamp: r.timestamp,
+            prev_timestamp: r.prev_timestamp,
+        },
+        Some(MemoryRecordEnum::Write(w)) => sys::bfz_memory_access {
+            kind: 2,
+            value: w.value,
+            prev_value: w.prev_value,
+            _pad: 0,
+            timestamp: w.timestamp,
+            prev_timestamp: w.prev_timestamp,
+        },
+    }
+}
+
+/// The record's event vectors (record.rs:15-34) in the bfz_*_event layouts.
+struct EventArrays {
+    cpu: Vec<sys::bfz_cpu_event>,
+    add: Vec<sys::bfz_alu_event>,
+    sub: Vec<sys::bfz_alu_event>,
+    jump: Vec<sys::bfz_jump_event>,
+    io: Vec<sys::bfz_io_event>,
+    memory_instr: Vec<sys::bfz_mem_instr_event>,
+    memory: Vec<sys::bfz_memory_event>,
+}
+
+impl EventArrays {
+    fn new(r: &ExecutionRecord) -> Self {
+        let alu = |e: &bf_core_executor::events::AluEvent| sys::bfz_alu_event {
+            pc: e.pc,
+            opcode: e.opcode as u8,
+            next_mv: e.next_mv,
+            mv: e.mv,
+            _pad: 0,
+        };
+        Self {
+            cpu: r
+                .cpu_events
+                .par_iter()
+                .map(|e| sys::bfz_cpu_event {
+                    clk: e.clk,
+                    pc: e.pc,
+                    next_pc: e.next_pc,
+                    mp: e.mp,
+                    next_mp: e.next_mp,
+                    mv: e.mv,
+                    next_mv: e.next_mv,
+                    _pad: [0; 2],
+                    mv_access: access(&e.mv_access),
+                    next_mv_access: access(&e.next_mv_access),
+                })
+                .collect(),
+            add: r.add_events.par_iter().map(alu).collect(),
+            sub: r.sub_events.par_iter().map(alu).collect(),
+            jump: r
+                .jump_events
+                .par_iter()
+                .map(|e| sys::bfz_jump_event {
+                    pc: e.pc,
+                    next_pc: e.next_pc,
+                    opcode: e.opcode as u8,
+                    _pad: [0; 3],
+                    dst: e.dst,
+                    mv: e.mv,
+                    _pad2: [0; 3],
+                })
+                .collect(),
+            io: r
+                .io_events
+                .iter()
+                .map(|e| sys::bfz_io_event {
+                    pc: e.pc,
+                    opcode: e.opcode as u8,
+                    _pad: [0; 3],
+                    mp: e.mp,
+                    mv: e.mv,
+                    _pad2: [0; 3],
+                })
+                .collect(),
+            memory_instr: r
+                .memory_instr_events
+                .par_iter()
+                .map(|e| sys::bfz_mem_instr_event {
+                    clk: e.clk,
+                    pc: e.pc,
+                    opcode: e.opcode as u8,
+                    _pad: [0; 3],
+                    mp: e.mp,
+                    next_mp: e.next_mp,
+                })
+                .collect(),
+            // HashMap-drain order (executor.rs:74); libbfz sorts it into the normal form
+            memory: r
+                .cpu_memory_access
+                .iter()
+                .map(|e| sys::bfz_memory_event {
+                    addr: e.addr,
+                    initial_timestamp: e.initial_mem_access.timestamp,
+                    final_timestamp: e.final_mem_access.timestamp,
+                    initial_value: e.initial_mem_access.value,
+                    final_value: e.final_mem_access.value,
+                    _pad: [0; 2],
+                })
+                .collect(),
+        }
+    }
+
+    fn as_c(&self) -> sys::bfz_events {
+        sys::bfz_events {
+            cpu: self.cpu.as_ptr(),
+            n_cpu: self.cpu.len(),
+            add: self.add.as_ptr(),
+            n_add: self.add.len(),
+            sub: self.sub.as_ptr(),
+            n_sub: self.sub.len(),
+            jump: self.jump.as_ptr(),
+            n_jump: self.jump.len(),
+            io: self.io.as_ptr(),
+            n_io: self.io.len(),
+            memory_instr: self.memory_instr.as_ptr(),
+            n_memory_instr: self.memory_instr.len(),
+            memory: self.memory.as_ptr(),
+            n_memory: self.memory.len(),
+        }
+    }
+}
+
+impl HipProver {
+    /// BFZ1 proof bytes -> the reference's ShardProof (utils/prove.rs:46 wire format).
+    fn shard_proof(bfz1: &[u8]) -> Result<ShardProof<SC>, HipProverError> {
+        let (mut b, mut blen) = (core::ptr::null_mut(), 0usize);
+        sys::check(unsafe {
+            sys::bfz_proof_to_bincode(bfz1.as_ptr(), bfz1.len(), FIELD_MONTGOMERY, &mut b, &mut blen)
+        });
+        let bytes = unsafe { sys::take_bytes(b, blen) };
+        bincode::deserialize(&bytes).map_err(|_| HipProverError)
+    }
+}
+
+impl MachineProver<SC, A> for HipProver {
     type DeviceMatrix = RowMajorMatrix<KoalaBear>;
     type DeviceProverData = HipMainData;
     type DeviceProvingKey = HipProvingKey;
     type Error = HipProverError;
 
-    fn new(machine: StarkMachine<SC, Air>) -> Self {
+    fn new(machine: StarkMachine<SC, A>) -> Self {
         let device = std::env::var("BFZ_DEVICE").ok().and_then(|d| d.parse().ok()).unwrap_or(0);
         sys::check(unsafe { sys::bfz_init(device) });
         Self { machine }
     }
 
-    fn machine(&self) -> &StarkMachine<SC, Air> {
+    fn machine(&self) -> &StarkMachine<SC, A> {
         &self.machine
     }
 
     fn setup(&self, program: &Program) -> (HipProvingKey, StarkVerifyingKey<SC>) {
+        // the host key is what BfProver::setup keeps (pk_to_host, crates/prover/src/lib.rs:51);
+        // the device key is made from it exactly as BfProver::prove does (lib.rs:76)
         let (host, vk) = self.machine.setup(program);
-        let src = CString::new(program_source(program)).unwrap();
-        let mut dev = core::ptr::null_mut();
-        let mut root = [0u32; 8];
-        sys::check(unsafe { sys::bfz_setup(src.as_ptr(), &mut dev, root.as_mut_ptr()) });
-        // the device and host preprocessed commitments agree (both are MerkleTreeMmcs roots)
-        assert_eq!(words(host.commit.as_ref()), &root[..], "preprocessed commit mismatch");
-        (HipProvingKey { host, dev }, vk)
+        (self.pk_to_device(&host), vk)
     }
 
-    fn pk_to_device(&self, _pk: &StarkProvingKey<SC>) -> HipProvingKey {
-        // keys are made by setup(program): libbfz builds the preprocessed LDEs from the program
-        unimplemented!("HipProver: create device keys with setup()")
+    fn pk_to_device(&self, pk: &StarkProvingKey<SC>) -> HipProvingKey {
+        // StarkProvingKey::traces in the key's order; chip_ordering maps each name to its index
+        let mut chips = vec![-1 as c_int; pk.traces.len()];
+        for (name, &i) in pk.chip_ordering.iter() {
+            chips[i] = chip_id(name);
+        }
+        assert!(chips.iter().all(|&c| c >= 0), "pk_to_device: chip_ordering does not cover the traces");
+        let ptrs: Vec<*const u32> = pk.traces.iter().map(|t| words(&t.values).as_ptr()).collect();
+        let hs: Vec<usize> = pk.traces.iter().map(|t| t.height()).collect();
+        let ws: Vec<usize> = pk.traces.iter().map(|t| t.width()).collect();
+        let commit = words(pk.commit.as_ref());
+        let mut dev = core::ptr::null_mut();
+        // libbfz recovers the program from the Program trace, checks both traces against it and
+        // the device commitment against pk.commit (a mismatch is an error, not a silent re-key)
+        sys::check(unsafe {
+            sys::bfz_pk_from_host(chips.as_ptr(), ptrs.as_ptr(), hs.as_ptr(), ws.as_ptr(),
+                                  chips.len(), commit.as_ptr(), &mut dev)
+        });
+        HipProvingKey { host: pk.clone(), dev }
     }
 
     fn pk_to_host(&self, pk: &HipProvingKey) -> StarkProvingKey<SC> {
@@ -195,17 +385,13 @@ impl MachineProver<SC, Air> for HipProver {
         data: ShardMainData<SC, RowMajorMatrix<KoalaBear>, HipMainData>,
         challenger: &mut Challenger<SC>,
     ) -> Result<ShardProof<SC>, HipProverError> {
-        let ch = to_c(challenger);
+        let mut ch = to_c(challenger);
         let (mut p, mut len) = (core::ptr::null_mut(), 0usize);
-        sys::check(unsafe { sys::bfz_open(pk.dev, data.main_data.0, &ch, &mut p, &mut len) });
+        sys::check(unsafe { sys::bfz_open(pk.dev, data.main_data.0, &mut ch, &mut p, &mut len) });
+        // bfz_open advances the challenger through the whole opening, as the trait's open does
+        from_c(&ch, challenger);
         let bfz1 = unsafe { sys::take_bytes(p, len) };
-        let (mut b, mut blen) = (core::ptr::null_mut(), 0usize);
-        sys::check(unsafe {
-            sys::bfz_proof_to_bincode(bfz1.as_ptr(), bfz1.len(), FIELD_MONTGOMERY, &mut b, &mut blen)
-        });
-        let bytes = unsafe { sys::take_bytes(b, blen) };
-        // the reference's own wire format (utils/prove.rs:46): deserialize straight into the type
-        bincode::deserialize(&bytes).map_err(|_| HipProverError)
+        Self::shard_proof(&bfz1)
     }
 
     fn prove(
@@ -215,21 +401,38 @@ impl MachineProver<SC, Air> for HipProver {
         challenger: &mut Challenger<SC>,
     ) -> Result<MachineProof<SC>, HipProverError>
     where
-        Air: for<'a> p3_air::Air<DebugConstraintBuilder<'a, KoalaBear, <SC as StarkGenericConfig>::Challenge>>,
+        A: for<'a> Air<DebugConstraintBuilder<'a, KoalaBear, <SC as StarkGenericConfig>::Challenge>>,
     {
-        self.machine().generate_dependencies(record, None); // prover.rs:570
-        pk.observe_into(challenger);
-        let traces = self.generate_traces(record);
-        let data = self.commit(traces);
+        // prover.rs:560-582 with the trace generation moved to the device: the byte-lookup
+        // multiplicities (generate_dependencies, prover.rs:570) are computed there from the same
+        // events; the host record gets them too only where the debug builder reads them
+        #[cfg(feature = "debug")]
+        self.machine().generate_dependencies(record, None);
+        pk.observe_into(challenger); // prover.rs:572
+        let events = EventArrays::new(record);
+        let c_events = events.as_c();
+        let mut rec = core::ptr::null_mut();
+        sys::check(unsafe { sys::bfz_record_from_events(pk.dev, &c_events, &mut rec) });
+        let rec = HipRecord(rec);
+        drop(events); // the events are in HBM now
+        let mut data = core::ptr::null_mut();
+        let mut root = [0u32; 8];
+        sys::check(unsafe {
+            sys::bfz_record_main_commit(pk.dev, rec.0, &mut data, root.as_mut_ptr())
+        });
+        let main_commit: Com<SC> = unsafe { core::mem::transmute_copy(&root) };
+        // open reads the device data only: no host traces, chip ordering fixed by libbfz
+        let data = ShardMainData::new(Vec::new(), main_commit, HipMainData(data), HashMap::new());
         let shard_proof = self.open(pk, data, &mut challenger.clone())?; // prover.rs:578
+        drop(rec);
         Ok(MachineProof { shard_proof })
     }
 }
 
 impl HipProver {
     /// Pipelined proofs of one program over many inputs (bfz_prove_batch): execution and event
-    /// upload of job k+1 run under the GPU proof of job k.  Returns the reference's bincode
-    /// ShardProof bytes per input.
+    /// upload of job k+1 run under the GPU proof of job k.  Returns the reference's ShardProof
+    /// per input.
     pub fn prove_batch(&self, pk: &HipProvingKey, stdins: &[Vec<u8>]) -> Vec<ShardProof<SC>> {
         let ptrs: Vec<*const u8> = stdins.iter().map(|s| s.as_ptr()).collect();
         let lens: Vec<usize> = stdins.iter().map(|s| s.len()).collect();
@@ -241,21 +444,17 @@ impl HipProver {
         });
         outs.into_iter()
             .zip(olens)
-            .map(|(p, n)| {
-                let bfz1 = unsafe { sys::take_bytes(p, n) };
-                let (mut b, mut blen) = (core::ptr::null_mut(), 0usize);
-                sys::check(unsafe {
-                    sys::bfz_proof_to_bincode(bfz1.as_ptr(), bfz1.len(), FIELD_MONTGOMERY, &mut b,
-                                              &mut blen)
-                });
-                bincode::deserialize(&unsafe { sys::take_bytes(b, blen) }).expect("bincode")
-            })
+            .map(|(p, n)| Self::shard_proof(&unsafe { sys::take_bytes(p, n) }).expect("bincode"))
             .collect()
     }
-}
 
-/// crates/prover/src/components.rs:11-20: select the HIP core prover.
-pub struct HipProverComponents;
-impl BfProverComponents for HipProverComponents {
-    type CoreProver = HipProver;
+    /// bfz_setup on the program text directly (a device key without the host StarkProvingKey;
+    /// cached per program in libbfz).
+    pub fn setup_device_only(&self, program: &Program) -> (*mut sys::bfz_pk, [u32; 8]) {
+        let src = CString::new(program_source(program)).unwrap();
+        let mut dev = core::ptr::null_mut();
+        let mut root = [0u32; 8];
+        sys::check(unsafe { sys::bfz_setup(src.as_ptr(), &mut dev, root.as_mut_ptr()) });
+        (dev, root)
+    }
 }

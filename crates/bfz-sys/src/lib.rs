@@ -61,6 +61,107 @@ pub struct bfz_batch_stats {
     pub exec_threads: c_int,
 }
 
+/// `Option<MemoryRecordEnum>` (events/memory.rs:31-79): kind 0 = None, 1 = Read, 2 = Write.
+#[repr(C)]
+#[derive(Clone, Copy, Default, Debug)]
+pub struct bfz_memory_access {
+    pub kind: u8,
+    pub value: u8,
+    pub prev_value: u8,
+    pub _pad: u8,
+    pub timestamp: u32,
+    pub prev_timestamp: u32,
+}
+/// `CpuEvent` (events/cpu.rs).
+#[repr(C)]
+#[derive(Clone, Copy, Default, Debug)]
+pub struct bfz_cpu_event {
+    pub clk: u32,
+    pub pc: u32,
+    pub next_pc: u32,
+    pub mp: u32,
+    pub next_mp: u32,
+    pub mv: u8,
+    pub next_mv: u8,
+    pub _pad: [u8; 2],
+    pub mv_access: bfz_memory_access,
+    pub next_mv_access: bfz_memory_access,
+}
+/// `AluEvent` (events/instr.rs).
+#[repr(C)]
+#[derive(Clone, Copy, Default, Debug)]
+pub struct bfz_alu_event {
+    pub pc: u32,
+    pub opcode: u8,
+    pub next_mv: u8,
+    pub mv: u8,
+    pub _pad: u8,
+}
+/// `JumpEvent`.
+#[repr(C)]
+#[derive(Clone, Copy, Default, Debug)]
+pub struct bfz_jump_event {
+    pub pc: u32,
+    pub next_pc: u32,
+    pub opcode: u8,
+    pub _pad: [u8; 3],
+    pub dst: u32,
+    pub mv: u8,
+    pub _pad2: [u8; 3],
+}
+/// `MemInstrEvent`.
+#[repr(C)]
+#[derive(Clone, Copy, Default, Debug)]
+pub struct bfz_mem_instr_event {
+    pub clk: u32,
+    pub pc: u32,
+    pub opcode: u8,
+    pub _pad: [u8; 3],
+    pub mp: u32,
+    pub next_mp: u32,
+}
+/// `IoEvent`.
+#[repr(C)]
+#[derive(Clone, Copy, Default, Debug)]
+pub struct bfz_io_event {
+    pub pc: u32,
+    pub opcode: u8,
+    pub _pad: [u8; 3],
+    pub mp: u32,
+    pub mv: u8,
+    pub _pad2: [u8; 3],
+}
+/// `MemoryEvent` (addr, initial_mem_access, final_mem_access).
+#[repr(C)]
+#[derive(Clone, Copy, Default, Debug)]
+pub struct bfz_memory_event {
+    pub addr: u32,
+    pub initial_timestamp: u32,
+    pub final_timestamp: u32,
+    pub initial_value: u8,
+    pub final_value: u8,
+    pub _pad: [u8; 2],
+}
+/// The `ExecutionRecord` event vectors (record.rs:15-34) as pointer + length pairs.
+#[repr(C)]
+#[derive(Clone, Copy, Debug)]
+pub struct bfz_events {
+    pub cpu: *const bfz_cpu_event,
+    pub n_cpu: usize,
+    pub add: *const bfz_alu_event,
+    pub n_add: usize,
+    pub sub: *const bfz_alu_event,
+    pub n_sub: usize,
+    pub jump: *const bfz_jump_event,
+    pub n_jump: usize,
+    pub io: *const bfz_io_event,
+    pub n_io: usize,
+    pub memory_instr: *const bfz_mem_instr_event,
+    pub n_memory_instr: usize,
+    pub memory: *const bfz_memory_event,
+    pub n_memory: usize,
+}
+
 pub type bfz_allgather_fn =
     Option<unsafe extern "C" fn(ctx: *mut c_void, send: *const c_void, bytes: usize, recv: *mut c_void) -> c_int>;
 pub type bfz_allreduce_u32_fn = Option<unsafe extern "C" fn(ctx: *mut c_void, data: *mut u32, n: usize) -> c_int>;
@@ -86,6 +187,10 @@ extern "C" {
 
     pub fn bfz_setup(elf: *const c_char, pk: *mut *mut bfz_pk, vk_commit: *mut u32) -> c_int;
     pub fn bfz_pk_free(pk: *mut bfz_pk);
+    pub fn bfz_pk_from_host(chips: *const c_int, traces: *const *const u32, heights: *const usize,
+                            widths: *const usize, n: usize, commit: *const u32,
+                            pk: *mut *mut bfz_pk) -> c_int;
+    pub fn bfz_pk_commit(pk: *const bfz_pk, commit: *mut u32) -> c_int;
 
     pub fn bfz_main_commit(pk: *const bfz_pk, chips: *const c_int, traces: *const *const u32,
                            heights: *const usize, widths: *const usize, nchips: usize,
@@ -93,7 +198,7 @@ extern "C" {
     pub fn bfz_record_main_commit(pk: *const bfz_pk, rec: *const bfz_record,
                                   out: *mut *mut bfz_main_data, root: *mut u32) -> c_int;
     pub fn bfz_challenger_observe_pk(pk: *const bfz_pk, ch: *mut bfz_challenger) -> c_int;
-    pub fn bfz_open(pk: *const bfz_pk, data: *mut bfz_main_data, ch: *const bfz_challenger,
+    pub fn bfz_open(pk: *const bfz_pk, data: *mut bfz_main_data, ch: *mut bfz_challenger,
                     proof: *mut *mut u8, proof_len: *mut usize) -> c_int;
     pub fn bfz_main_data_free(data: *mut bfz_main_data);
 
@@ -113,6 +218,8 @@ extern "C" {
     pub fn bfz_record_prove(pk: *const bfz_pk, rec: *const bfz_record, proof: *mut *mut u8,
                             proof_len: *mut usize, timings: *mut bfz_timings) -> c_int;
     pub fn bfz_record_free(rec: *mut bfz_record);
+    pub fn bfz_record_from_events(pk: *const bfz_pk, events: *const bfz_events,
+                                  rec: *mut *mut bfz_record) -> c_int;
     pub fn bfz_record_prove_sharded(pk: *const bfz_pk, rec: *const bfz_record, rank: c_int,
                                     world: c_int, allgather: bfz_allgather_fn,
                                     allreduce_sum: bfz_allreduce_u32_fn, ctx: *mut c_void,

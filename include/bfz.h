@@ -108,6 +108,21 @@ int bfz_trace_device(const char* elf, const uint8_t* stdin_data, size_t nin, int
 int bfz_setup(const char* elf, bfz_pk** pk, uint32_t vk_commit[8]);
 void bfz_pk_free(bfz_pk* pk);
 
+/* MachineProver::pk_to_device (crates/stark/src/prover.rs:52,201-203): the device key of a
+ * StarkProvingKey kept on the host.  BfProver::setup keeps only pk_to_host(pk)
+ * (crates/prover/src/lib.rs:51) and BfProver::prove rebuilds the device key from it on every
+ * proof (:76).  Arguments are the key's preprocessed traces (StarkProvingKey::traces,
+ * machine.rs:49-60, in the key's order): chips[i] the chip id (BfAir::chips() order) of
+ * traces[i], a row-major Montgomery heights[i] x widths[i] matrix, and the key's commit.
+ * The program is recovered from the Program chip's preprocessed trace (pc, opcode, op_a bytes;
+ * program/mod.rs:66-94); both traces must be exactly that program's (machine.rs:154-224), and
+ * the device commitment of them must equal commit, or the call fails.  The device key is the
+ * per-program setup cache's (a cache hit costs the trace comparison only). */
+int bfz_pk_from_host(const int* chips, const uint32_t* const* traces, const size_t* heights,
+                     const size_t* widths, size_t n, const uint32_t commit[8], bfz_pk** pk);
+/* The preprocessed commitment of a device key (StarkProvingKey::commit / vk.commit). */
+int bfz_pk_commit(const bfz_pk* pk, uint32_t commit[8]);
+
 /* The split MachineProver surface, for a Rust HipProver:
  *   bfz_main_commit         MachineProver::commit (crates/stark/src/prover.rs:209-236): host
  *                           row-major main traces (as bfz_prove_traces) -> LDE + MerkleTreeMmcs
@@ -117,9 +132,13 @@ void bfz_pk_free(bfz_pk* pk);
  *   bfz_record_main_commit  the same from a device-resident record (traces generated on device).
  *   bfz_challenger_observe_pk  MachineProvingKey::observe_into (prover.rs:595-601).
  *   bfz_open                MachineProver::open (prover.rs:242-553) on the challenger state
- *                           after observe_into; ch is not modified (the reference opens on a
- *                           clone, prover.rs:578).  Output = the same BFZ1 proof bfz_prove*
- *                           returns.  The main data stays valid (it may be opened again).
+ *                           after observe_into.  Like the trait method (which takes the
+ *                           challenger &mut), ch is advanced: on success it holds the state
+ *                           after the whole opening (PCS open, FRI commit phase, grind, query
+ *                           sampling).  MachineProver::prove opens on a clone (prover.rs:578):
+ *                           pass a copy to keep the caller's state.  Output = the same BFZ1
+ *                           proof bfz_prove* returns.  The main data stays valid (it may be
+ *                           opened again).
  *   bfz_main_data_free      drops ShardMainData (frees its HBM). */
 int bfz_main_commit(const bfz_pk* pk, const int* chips, const uint32_t* const* traces,
                     const size_t* heights, const size_t* widths, size_t nchips, bfz_main_data** out,
@@ -127,7 +146,7 @@ int bfz_main_commit(const bfz_pk* pk, const int* chips, const uint32_t* const* t
 int bfz_record_main_commit(const bfz_pk* pk, const bfz_record* rec, bfz_main_data** out,
                            uint32_t root[8]);
 int bfz_challenger_observe_pk(const bfz_pk* pk, bfz_challenger* ch);
-int bfz_open(const bfz_pk* pk, bfz_main_data* data, const bfz_challenger* ch, uint8_t** proof,
+int bfz_open(const bfz_pk* pk, bfz_main_data* data, bfz_challenger* ch, uint8_t** proof,
              size_t* proof_len);
 void bfz_main_data_free(bfz_main_data* data);
 
@@ -165,6 +184,65 @@ int bfz_record_new(const bfz_pk* pk, const uint8_t* stdin_data, size_t nin, bfz_
 int bfz_record_prove(const bfz_pk* pk, const bfz_record* rec, uint8_t** proof, size_t* proof_len,
                      bfz_timings* timings);
 void bfz_record_free(bfz_record* rec);
+
+/* The reference's ExecutionRecord (crates/core/executor/src/record.rs:15-34) as plain arrays,
+ * one C struct per event type of crates/core/executor/src/events (explicit padding, no
+ * compiler-inserted gaps; opcodes are the Opcode discriminants of opcode.rs:13-30).
+ * bfz_memory_access is Option<MemoryRecordEnum> (events/memory.rs:31-79): kind 0 = None,
+ * 1 = Read (prev_value unused), 2 = Write. */
+typedef struct {
+  uint8_t kind, value, prev_value, _pad;
+  uint32_t timestamp, prev_timestamp;
+} bfz_memory_access;
+typedef struct { /* CpuEvent, events/cpu.rs */
+  uint32_t clk, pc, next_pc, mp, next_mp;
+  uint8_t mv, next_mv, _pad[2];
+  bfz_memory_access mv_access, next_mv_access;
+} bfz_cpu_event;
+typedef struct { /* AluEvent, events/instr.rs */
+  uint32_t pc;
+  uint8_t opcode, next_mv, mv, _pad;
+} bfz_alu_event;
+typedef struct { /* JumpEvent */
+  uint32_t pc, next_pc;
+  uint8_t opcode, _pad[3];
+  uint32_t dst;
+  uint8_t mv, _pad2[3];
+} bfz_jump_event;
+typedef struct { /* MemInstrEvent */
+  uint32_t clk, pc;
+  uint8_t opcode, _pad[3];
+  uint32_t mp, next_mp;
+} bfz_mem_instr_event;
+typedef struct { /* IoEvent */
+  uint32_t pc;
+  uint8_t opcode, _pad[3];
+  uint32_t mp;
+  uint8_t mv, _pad2[3];
+} bfz_io_event;
+typedef struct { /* MemoryEvent: addr, initial_mem_access, final_mem_access (events/memory.rs:6-13) */
+  uint32_t addr, initial_timestamp, final_timestamp;
+  uint8_t initial_value, final_value, _pad[2];
+} bfz_memory_event;
+typedef struct {
+  const bfz_cpu_event* cpu;                 size_t n_cpu;          /* cpu_events */
+  const bfz_alu_event* add;                 size_t n_add;          /* add_events */
+  const bfz_alu_event* sub;                 size_t n_sub;          /* sub_events */
+  const bfz_jump_event* jump;               size_t n_jump;         /* jump_events */
+  const bfz_io_event* io;                   size_t n_io;           /* io_events */
+  const bfz_mem_instr_event* memory_instr;  size_t n_memory_instr; /* memory_instr_events */
+  const bfz_memory_event* memory;           size_t n_memory;       /* cpu_memory_access */
+} bfz_events;
+/* A device record from the reference's own events (the record utils::prove hands to
+ * MachineProver::prove, crates/core/machine/src/utils/prove.rs:38-44): the arrays go to HBM
+ * (add_events then sub_events as one AddSub stream, alu/mod.rs:72), the memory events are put
+ * in the normal form (sorted by address; the reference drains a HashMap, executor.rs:74), and
+ * bfz_record_prove / bfz_record_main_commit then generate every chip trace and the byte-lookup
+ * multiplicities on the device (generate_dependencies + generate_traces, prover.rs:58-81,
+ * machine.rs:228-248).  The program is pk's.  Events are validated (pc inside the program,
+ * opcodes, access kinds, unique memory addresses, at least one cycle) before any kernel reads
+ * them.  Host pointers (pageable is fine). */
+int bfz_record_from_events(const bfz_pk* pk, const bfz_events* events, bfz_record** rec);
 
 /* One proof sharded over `world` GPUs (one process per GPU, every rank calls this with the
  * same record): each rank computes its residue-class row shard of every large LDE, hashes its

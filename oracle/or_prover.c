@@ -772,6 +772,12 @@ int or_verify_proof(const or_program* prog, const uint8_t* proof, size_t len) {
       ef t = ef_mul(ef_sub(betas[s], ef_from_fp(xs0)), ef_sub(ev[1], ev[0]));
       folded = ef_add(ev[0], ef_mul_fp(t, fp_inv(fp_sub(xs1, xs0))));
     }
+    /* a height-2 input (a 1-row trace) joins after the last fold, as in the commit phase above
+     * (decision D11) */
+    {
+      int lfin = log_max_h - (int)ns;
+      if (lfin >= 0 && lfin < 32 && have[lfin]) { folded = ef_add(folded, ro[lfin]); have[lfin] = 0; }
+    }
     for (int lh = 0; lh < 32; lh++) if (have[lh]) goto fail;
     if (!ef_eq(folded, final_poly)) goto fail;
   }

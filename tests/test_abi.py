@@ -128,8 +128,9 @@ def _tampered(pf, fn):
 
 
 def test_verifier_rejects_out_of_range_log_degree_and_round_count():
-    """a log degree word >= 2^31 (a negative int) or 0, and a commit phase shorter
-    than the tallest matrix, are rejected before any shift by them."""
+    """a log degree word >= 2^31 (a negative int) or above 23, and a commit phase
+    shorter than the tallest matrix, are rejected before any shift by them.  Log degree 0 is a
+    legal 1-row trace: claimed for a taller chip it fails the Merkle openings."""
     prog = guests.HELLO
     pf = O.prove(prog, [])
     vk = _vk(prog)
@@ -138,9 +139,11 @@ def test_verifier_rejects_out_of_range_log_degree_and_round_count():
     def set_logdeg(v):
         return lambda m: m["opened"][0].__setitem__("log_degree", v)
 
-    for v in (0x80000000, 0xFFFFFFFF, 0, 24):
+    for v in (0x80000000, 0xFFFFFFFF, 24):
         with pytest.raises(_lib.BfzError, match="log degree out of range"):
             c.verify(sdk.BfProofWithPublicValues(proof=_tampered(pf, set_logdeg(v)), stdin=b""), vk)
+    with pytest.raises(_lib.BfzError, match="path length"):
+        c.verify(sdk.BfProofWithPublicValues(proof=_tampered(pf, set_logdeg(0)), stdin=b""), vk)
 
     def short_commit(m):
         m["commit_roots"].pop()
@@ -285,3 +288,137 @@ def test_rust_ffi_matches_header():
          for m in re.finditer(r"pub fn (bfz_[a-z0-9_]+)\(((?:[^()]|\([^()]*\))*)\)", rs)}
     assert set(c) == set(declared_symbols())
     assert c == r
+
+
+@pytest.mark.parametrize("prog,stdin", [("+", []), (".", []), (">", []), (",", [9]), ("-", [])])
+def test_one_cycle_programs_prove_and_verify(prog, stdin):
+    """A one-cycle program has a 1-row Cpu trace (cpu/trace.rs:33: next_power_of_two, no
+    minimum): its 2-row LDE's reduced opening joins the FRI layer after the last fold
+    (decision D11), and both verifiers accept the proof (log degree 0 is legal)."""
+    pf = O.prove(prog, stdin)
+    assert O.verify(prog, pf)
+    sdk.ProverClient().verify(sdk.BfProofWithPublicValues(proof=pf, stdin=bytes(stdin)), _vk(prog))
+    # the Cpu chip's opened log degree is 0
+    assert sdk.proof_to_bincode(pf)  # and the wire format encodes it
+
+
+def test_event_struct_layouts_match_header(tmp_path):
+    """bfz.h's bfz_*_event structs (compiled with gcc) have exactly the numpy layouts bfz/events.py
+    hands to bfz_record_from_events and the field order of crates/bfz-sys."""
+    import subprocess
+    from bfz import events as E
+    checks = {"bfz_cpu_event": E.CPU, "bfz_alu_event": E.ALU, "bfz_jump_event": E.JUMP,
+              "bfz_mem_instr_event": E.MEM_INSTR, "bfz_io_event": E.IO, "bfz_memory_event": E.MEMORY}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{ROOT}/include/bfz.h"',
+             "int main(void) {"]
+    for st, dt in checks.items():
+        lines.append(f'printf("{st} size %zu\\n", sizeof({st}));')
+        for name in dt.names:
+            field = name
+            for acc in ("mv_access_", "next_mv_access_"):
+                if name.startswith(acc):
+                    field = acc[:-1] + "." + name[len(acc):]
+            lines.append(f'printf("{st} {name} %zu\\n", offsetof({st}, {field}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-o", str(exe), str(src)], check=True)
+    got = {}
+    for ln in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n"):
+        if ln:
+            st, name, v = ln.split()
+            got[(st, name)] = int(v)
+    for st, dt in checks.items():
+        assert got[(st, "size")] == dt.itemsize, st
+        for name in dt.names:
+            assert got[(st, name)] == dt.fields[name][1], (st, name)
+    # crates/bfz-sys declares the same fields in the same order
+    rs = open(os.path.join(ROOT, "crates", "bfz-sys", "src", "lib.rs")).read()
+    hdr = open(os.path.join(ROOT, "include", "bfz.h")).read()
+    for st in list(checks) + ["bfz_memory_access", "bfz_events"]:
+        m = re.search(r"typedef struct \{[^{}]*?\}\s*" + st + ";", hdr, re.S)
+        cfields = re.findall(r"(\w+)(?:\[\d+\])?\s*[,;]", re.sub(r"/\*.*?\*/", "", m.group(0).split("{", 1)[1].rsplit("}", 1)[0]))
+        r = re.search(r"pub struct " + st + r" \{(.*?)\n\}", rs, re.S)
+        rfields = re.findall(r"pub (\w+):", r.group(1))
+        assert cfields == rfields, st
+
+
+def _prep_host_key(prog):
+    import ctypes as ct
+    import numpy as np
+    out = []
+    for c in (5, 1):  # Byte (2^16 rows) sorts before Program
+        p = ct.POINTER(ct.c_uint32)()
+        h, w = ct.c_size_t(), ct.c_size_t()
+        buf, n = _lib.u8buf(b"")
+        _lib.check(_lib.lib().bfz_trace(prog.encode(), buf, n, c, 1, ct.byref(p), ct.byref(h),
+                                        ct.byref(w)))
+        arr = np.ctypeslib.as_array(p, shape=(h.value * w.value,)).copy().reshape(h.value, w.value)
+        _lib.lib().bfz_free(p)
+        out.append((c, sdk.CHIPS[c], arr))
+    commit = [O.to_mont(x) for x in O.setup_root(prog)]
+    return sdk.StarkProvingKey(commit=commit, traces=out,
+                               chip_ordering={"Byte": 0, "Program": 1}, local_only=[False, False])
+
+
+def test_pk_from_host_refuses_traces_that_are_not_the_programs():
+    """bfz_pk_from_host (MachineProver::pk_to_device) checks the host key before any device
+    work: a tampered Byte or Program preprocessed trace, a missing chip or a wrong width is an
+    error (the commit check needs the device and is in tests/test_gpu.py)."""
+    import numpy as np
+    hpk = _prep_host_key(guests.HELLO)
+    bad = [(c, n, t.copy()) for c, n, t in hpk.traces]
+    bad[0][2][5, 1] ^= 1  # Byte multiplicand column
+    with pytest.raises(_lib.BfzError, match="Byte is not the program's"):
+        sdk.CoreProver.pk_to_device(sdk.StarkProvingKey(hpk.commit, bad, hpk.chip_ordering, hpk.local_only))
+    bad = [(c, n, t.copy()) for c, n, t in hpk.traces]
+    bad[1][2][3, 4] = O.to_mont(7)  # an op_a byte of instruction 3
+    with pytest.raises(_lib.BfzError, match="Program is not the program's"):
+        sdk.CoreProver.pk_to_device(sdk.StarkProvingKey(hpk.commit, bad, hpk.chip_ordering, hpk.local_only))
+    with pytest.raises(_lib.BfzError, match="Program and Byte"):
+        sdk.CoreProver.pk_to_device(sdk.StarkProvingKey(hpk.commit, hpk.traces[:1], {}, []))
+    with pytest.raises(_lib.BfzError, match="bad shape"):
+        sdk.CoreProver.pk_to_device(sdk.StarkProvingKey(
+            hpk.commit, [hpk.traces[0], (1, "Program", np.ascontiguousarray(hpk.traces[1][2][:, :5]))],
+            hpk.chip_ordering, hpk.local_only))
+    bad = [(c, n, t.copy()) for c, n, t in hpk.traces]
+    bad[1][2][0, 1] = O.to_mont(9)  # opcode 9 does not exist
+    with pytest.raises(_lib.BfzError, match="opcode"):
+        sdk.CoreProver.pk_to_device(sdk.StarkProvingKey(hpk.commit, bad, hpk.chip_ordering, hpk.local_only))
+
+
+def test_rust_crates_have_no_stubs_and_declare_their_dependencies():
+    """The Rust drop-in (crates/; not compiled here) has no unimplemented!/todo! bodies, every
+    external crate bf-hip-prover uses is a dependency in its Cargo.toml, and it does not depend
+    on bf-prover (which depends on it behind the `hip` feature: no cycle)."""
+    for d, _, files in os.walk(os.path.join(ROOT, "crates")):
+        for f in files:
+            if f.endswith(".rs"):
+                src = open(os.path.join(d, f)).read()
+                assert not re.search(r"\b(unimplemented|todo)!\s*\(", src), f
+    src = open(os.path.join(ROOT, "crates", "bf-hip-prover", "src", "lib.rs")).read()
+    toml = open(os.path.join(ROOT, "crates", "bf-hip-prover", "Cargo.toml")).read()
+    deps = set(re.findall(r"^([a-z0-9-]+)\s*=", toml.split("[dependencies]")[1].split("\n[")[0], re.M))
+    used = set(re.findall(r"(?<![\w:])((?:p3|bf|bfz)_[a-z0-9_]+)::", src)) | set(
+        re.findall(r"^use ((?:p3|bf|bfz)_[a-z0-9_]+)", src, re.M))
+    used |= {"bincode"} if "bincode::" in src else set()
+    used |= {"hashbrown"} if "hashbrown::" in src else set()
+    for crate in used:
+        assert crate.replace("_", "-") in deps, crate
+    assert "bf-prover" not in deps
+    # the workspace patch makes bf-prover select it (components.rs) behind `hip`
+    patch = open(os.path.join(ROOT, "crates", "reference-patch", "0001-hip-core-prover.patch")).read()
+    assert 'type CoreProver = bf_hip_prover::HipProver;' in patch
+    assert 'hip = ["dep:bf-hip-prover"]' in patch and 'hip = ["bf-prover/hip"]' in patch
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/crates"), reason="reference checkout absent")
+def test_reference_patch_applies():
+    """crates/reference-patch applies cleanly to the reference workspace (dry run, nothing
+    written)."""
+    import subprocess
+    r = subprocess.run(["patch", "--dry-run", "-p1", "-d", "/root/reference", "-i",
+                        os.path.join(ROOT, "crates", "reference-patch", "0001-hip-core-prover.patch")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr

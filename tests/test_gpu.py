@@ -163,20 +163,26 @@ def test_prove_from_host_traces_matches(client):
 
 def test_split_commit_open_matches_prove(client):
     """MachineProver::commit + observe_into + open (prover.rs:209-236, 595-601, 242-553) through
-    the split C ABI give the bytes of the one-call prove; open leaves the challenger unchanged
-    (the reference opens on a clone, prover.rs:578) and the main data can be opened again."""
+    the split C ABI give the bytes of the one-call prove; open advances the challenger it is
+    given (prove passes a clone, prover.rs:578) and the main data can be opened again."""
     pk, vk = client.setup(guests.FIBO)
     traces = sdk.generate_traces(guests.FIBO, [17])
     prover = sdk.CoreProver()
     data = prover.commit(pk, traces)
-    ch = prover.new_challenger()
-    prover.observe_into(pk, ch)
-    before = bytes(ch)
+    ch0 = prover.new_challenger()
+    prover.observe_into(pk, ch0)
+    before = bytes(ch0)
+    ch = _lib.Challenger.from_buffer_copy(before)  # prove opens on a clone (prover.rs:578)
     pf = prover.open(pk, data, ch)
-    assert bytes(ch) == before
+    # open advances its &mut challenger through the whole transcript (ADVICE r2), the same
+    # final state every time
+    assert bytes(ch) != before
+    after = bytes(ch)
     assert pf == client.prove(pk, [17]).run().proof
     assert pf == O.prove(guests.FIBO, [17])
-    assert prover.open(pk, data, ch) == pf
+    ch = _lib.Challenger.from_buffer_copy(before)
+    assert prover.open(pk, data, ch) == pf and bytes(ch) == after
+    ch = _lib.Challenger.from_buffer_copy(before)
     # the record path (device-generated traces) commits to the same root
     rec = ctypes.c_void_p()
     buf, n = _lib.u8buf(bytes([17]))
@@ -186,6 +192,7 @@ def test_split_commit_open_matches_prove(client):
     assert data2.main_commit == data.main_commit
     assert prover.open(pk, data2, ch) == pf
     _lib.lib().bfz_record_free(rec)
+    ch = _lib.Challenger.from_buffer_copy(before)
     # a challenger that has not observed the key gives a proof the verifier rejects
     bad = prover.open(pk, data, prover.new_challenger())
     with pytest.raises(_lib.BfzError):
@@ -195,6 +202,7 @@ def test_split_commit_open_matches_prove(client):
     pk2, _ = client.setup(guests.HELLO)
     with pytest.raises(_lib.BfzError, match="another key"):
         prover.open(pk2, data, ch)
+    ch = _lib.Challenger.from_buffer_copy(before)
     mats, chips, ptrs, hs, ws, k = sdk._trace_args(traces)
     out = ctypes.c_void_p()
     root = (ctypes.c_uint32 * 8)()
@@ -259,8 +267,8 @@ def test_prove_traces_rejects_bad_shapes(client):
     bad[3, 0] = P  # a Montgomery word >= p
     with pytest.raises(_lib.BfzError, match="non-canonical"):
         sdk.CoreProver().prove(pk, [(c, name, bad)] + traces[1:])
-    with pytest.raises(_lib.BfzError, match="power of two"):  # height 1
-        sdk.CoreProver().prove(pk, [(c, name, t[:1])] + traces[1:])
+    with pytest.raises(_lib.BfzError, match="power of two"):
+        sdk.CoreProver().prove(pk, [(c, name, t[:6])] + traces[1:])
 
 
 def test_fibo17_end_to_end_sdk(client):
@@ -322,6 +330,11 @@ def test_fibo_x4_2pow22_bytes_match_oracle(client):
     ref = O.prove(guests.FIBO_X4, [255])
     assert a.proof == ref, "headline proof differs from the oracle"
     assert O.verify(guests.FIBO_X4, a.proof)
+    # the Rust drop-in's path: the reference record's events through bfz_record_from_events
+    from bfz import events
+    rec = events.ExecutionRecordArrays.from_executor(guests.FIBO_X4, [255])
+    assert len(rec.cpu) == 3767729
+    assert _record_proof(pk, rec) == ref
     bc = sdk.proof_to_bincode(a.proof)
     client.verify_bincode(bc, vk)
     assert sdk.proof_from_bincode(bc) == a.proof
@@ -382,3 +395,110 @@ def test_trace_beyond_two_adicity_is_an_error(client):
         client.prove(pk, [255]).run()
     pk2, vk2 = client.setup(guests.FIBO)
     client.verify(client.prove(pk2, [17]).run(), vk2)
+
+
+# ---------------------------------------------------------------- the Rust drop-in's flows
+ONE_CYCLE = [("+", []), (".", []), (">", []), (",", [9]), ("-", [])]
+
+
+@pytest.mark.parametrize("prog,stdin", ONE_CYCLE)
+def test_one_cycle_programs_match_oracle(client, prog, stdin):
+    """1-row Cpu traces (cpu/trace.rs:33, no minimum height): the GPU proof is the
+    oracle's, both verifiers accept it; the host-trace path takes the 1-row trace too."""
+    pk, vk = client.setup(prog)
+    pf = client.prove(pk, stdin).run()
+    assert pf.proof == O.prove(prog, stdin)
+    client.verify(pf, vk)
+    assert O.verify(prog, pf.proof)
+    traces = sdk.generate_traces(prog, stdin)
+    assert traces[0][2].shape[0] == 1
+    assert sdk.CoreProver().prove(pk, traces) == pf.proof
+
+
+@pytest.mark.parametrize("name,prog,stdin", guests.REFERENCE_PROGRAMS + [("fibo17", guests.FIBO, [17])])
+def test_bfprover_host_key_flow_matches_oracle(name, prog, stdin):
+    """BfProver<HipProverComponents> as the reference runs it (crates/prover/src/lib.rs:46-90):
+    setup keeps only pk_to_host(pk) and drops the device key; every prove rebuilds it with
+    pk_to_device (bfz_pk_from_host) and proves the executor's record through
+    bfz_record_from_events (HipProver::prove).  Bytes = the oracle's."""
+    bp = sdk.BfProver()
+    pk, vk = bp.setup(prog)
+    assert isinstance(pk.pk, sdk.StarkProvingKey) and pk.pk.commit == vk.commit
+    assert [n for _, n, _ in pk.pk.traces] == ["Byte", "Program"]  # (Reverse(height), name)
+    pf = bp.prove(pk, stdin)
+    assert pf.proof == O.prove(prog, stdin), name
+    bp.verify(pf, vk)
+    assert pf.public_values == client_output(prog, stdin)
+
+
+def client_output(prog, stdin):
+    return sdk.ProverClient().execute(prog, stdin).run()
+
+
+def test_pk_to_device_refuses_a_wrong_commit():
+    """pk_to_device with a commit that is not the traces' (a key from another program, one word
+    changed) is refused: the device key is never silently re-made."""
+    bp = sdk.BfProver()
+    pk, vk = bp.setup(guests.HELLO)
+    other, _ = bp.setup(guests.FIBO)
+    for commit in ([vk.commit[0] ^ 1] + vk.commit[1:], other.pk.commit):
+        bad = sdk.StarkProvingKey(commit=commit, traces=pk.pk.traces,
+                                  chip_ordering=pk.pk.chip_ordering, local_only=pk.pk.local_only)
+        with pytest.raises(_lib.BfzError, match="commitment mismatch"):
+            sdk.CoreProver.pk_to_device(bad)
+    dpk = sdk.CoreProver.pk_to_device(pk.pk)  # the right one is a cache hit of setup's key
+    assert dpk.commit == vk.commit
+
+
+def _record_proof(pk, rec):
+    from bfz import events
+    drec = events.record_from_events(pk, rec)
+    ptr = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t()
+    _lib.check(_lib.lib().bfz_record_prove(ctypes.c_void_p(pk.handle), ctypes.c_void_p(drec.handle),
+                                           ctypes.byref(ptr), ctypes.byref(n), None))
+    return _lib.take_bytes(ptr, n.value)
+
+
+@pytest.mark.parametrize("name,prog,stdin", guests.REFERENCE_PROGRAMS + [("fibo255", guests.FIBO, [255])])
+def test_record_from_events_matches_oracle(client, name, prog, stdin):
+    """bfz_record_from_events: the reference record's event vectors (Executor::run) in HBM,
+    traces generated there; the proof is the oracle's.  The memory events may come in any order
+    (the reference drains a HashMap, executor.rs:74): they are put in address order."""
+    from bfz import events
+    pk, vk = client.setup(prog)
+    rec = events.ExecutionRecordArrays.from_executor(prog, stdin)
+    want = O.prove(prog, stdin)
+    assert _record_proof(pk, rec) == want, name
+    if len(rec.memory) > 1:
+        rec.memory = np.ascontiguousarray(rec.memory[::-1])
+        assert _record_proof(pk, rec) == want, name
+
+
+def test_record_from_events_sub_events_and_bad_events(client):
+    """Sub events in sub_events (chained after add_events, alu/mod.rs:72) give a valid proof of
+    the same execution; out-of-range events are refused before any kernel reads them, and the
+    library keeps working."""
+    from bfz import events
+    prog, stdin = guests.FIBO, [17]
+    pk, vk = client.setup(prog)
+    rec = events.ExecutionRecordArrays.from_executor(prog, stdin)
+    subs = rec.add["opcode"] == events.SUB
+    split = events.ExecutionRecordArrays(**{**rec.__dict__, "add": np.ascontiguousarray(rec.add[~subs]),
+                                            "sub": np.ascontiguousarray(rec.add[subs])})
+    pf = _record_proof(pk, split)
+    client.verify(sdk.BfProofWithPublicValues(proof=pf, stdin=bytes(stdin)), vk)
+    for field, idx, val, msg in (("cpu", 7, ("pc", 10 ** 6), "out of range"),
+                                 ("cpu", 0, ("mv_access_kind", 3), "out of range"),
+                                 ("jump", 0, ("opcode", 2), "out of range"),
+                                 ("memory", 1, ("addr", None), "two memory events")):
+        bad = events.ExecutionRecordArrays(**{k: (v.copy() if isinstance(v, np.ndarray) else v)
+                                              for k, v in rec.__dict__.items()})
+        arr = getattr(bad, field)
+        arr[idx][val[0]] = arr[0][val[0]] if val[1] is None else val[1]
+        with pytest.raises(_lib.BfzError, match=msg):
+            _record_proof(pk, bad)
+    empty = events.ExecutionRecordArrays(**{**rec.__dict__, "cpu": rec.cpu[:0]})
+    with pytest.raises(_lib.BfzError, match="no cpu events"):
+        _record_proof(pk, empty)
+    assert _record_proof(pk, rec) == O.prove(prog, stdin)

@@ -43,6 +43,15 @@ class Challenger(ctypes.Structure):
                 ("n_input", c_uint32), ("output_buffer", c_uint32 * 8), ("n_output", c_uint32)]
 
 
+class Events(ctypes.Structure):
+    """bfz_events: the reference ExecutionRecord's event arrays (pointers to bfz_*_event arrays,
+    see bfz/events.py for their numpy layouts)."""
+    _fields_ = [("cpu", c_void_p), ("n_cpu", c_size_t), ("add", c_void_p), ("n_add", c_size_t),
+                ("sub", c_void_p), ("n_sub", c_size_t), ("jump", c_void_p), ("n_jump", c_size_t),
+                ("io", c_void_p), ("n_io", c_size_t), ("memory_instr", c_void_p),
+                ("n_memory_instr", c_size_t), ("memory", c_void_p), ("n_memory", c_size_t)]
+
+
 # collective callbacks of bfz_record_prove_sharded (bfz_allgather_fn / bfz_allreduce_u32_fn)
 ALLGATHER_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_void_p, c_size_t, c_void_p)
 ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, c_void_p, POINTER(c_uint32), c_size_t)
@@ -67,6 +76,9 @@ SIGNATURES = [
                                  POINTER(POINTER(c_uint32)), POINTER(c_size_t), POINTER(c_size_t)]),
     ("bfz_setup", c_int, [c_char_p, POINTER(c_void_p), POINTER(c_uint32)]),
     ("bfz_pk_free", None, [c_void_p]),
+    ("bfz_pk_from_host", c_int, [POINTER(c_int), POINTER(POINTER(c_uint32)), POINTER(c_size_t),
+                                 POINTER(c_size_t), c_size_t, POINTER(c_uint32), POINTER(c_void_p)]),
+    ("bfz_pk_commit", c_int, [c_void_p, POINTER(c_uint32)]),
     ("bfz_main_commit", c_int, [c_void_p, POINTER(c_int), POINTER(POINTER(c_uint32)),
                                 POINTER(c_size_t), POINTER(c_size_t), c_size_t,
                                 POINTER(c_void_p), POINTER(c_uint32)]),
@@ -89,6 +101,7 @@ SIGNATURES = [
     ("bfz_record_prove", c_int, [c_void_p, c_void_p, POINTER(POINTER(c_uint8)), POINTER(c_size_t),
                                  POINTER(Timings)]),
     ("bfz_record_free", None, [c_void_p]),
+    ("bfz_record_from_events", c_int, [c_void_p, POINTER(Events), POINTER(c_void_p)]),
     ("bfz_record_prove_sharded", c_int, [c_void_p, c_void_p, c_int, c_int, ALLGATHER_FN,
                                          ALLREDUCE_FN, c_void_p, POINTER(POINTER(c_uint8)),
                                          POINTER(c_size_t), POINTER(Timings)]),
@@ -169,5 +182,5 @@ def take_bytes(ptr, n: int) -> bytes:
         lib().bfz_free(ptr)
 
 
-__all__ = ["lib", "check", "init", "u8buf", "take_bytes", "BfzError", "Timings", "LIB_PATH",
+__all__ = ["lib", "check", "init", "u8buf", "take_bytes", "BfzError", "Timings", "Events", "LIB_PATH",
            "SIGNATURES", "byref"]

@@ -1,0 +1,148 @@
+"""The reference's ExecutionRecord events (crates/core/executor/src/record.rs:15-34,
+events/*.rs) as numpy structured arrays laid out exactly like the bfz_*_event structs of
+include/bfz.h, and their hand-over to the device (bfz_record_from_events).
+
+    rec = ExecutionRecordArrays.from_executor(elf, stdin)   # Executor::run's events
+    handle = record_from_events(pk, rec)                     # -> bfz_record (HBM)
+
+`from_executor` parses the field-by-field event stream of bfz_execute_events (the executor a
+Rust caller would have run: `Executor::run`, executor.rs:71-79); a Rust HipProver fills the
+same structs from `record.cpu_events`, `record.add_events`, ... directly.
+"""
+from __future__ import annotations
+
+import ctypes
+import struct
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib, u8buf
+
+
+def _dt(fields, itemsize):
+    names, formats, offsets = zip(*fields)
+    return np.dtype({"names": list(names), "formats": list(formats), "offsets": list(offsets),
+                     "itemsize": itemsize})
+
+
+# bfz.h layouts (explicit padding; tests/test_abi.py checks them against the header)
+ACCESS = [("kind", "u1", 0), ("value", "u1", 1), ("prev_value", "u1", 2), ("timestamp", "<u4", 4),
+          ("prev_timestamp", "<u4", 8)]
+CPU = _dt([("clk", "<u4", 0), ("pc", "<u4", 4), ("next_pc", "<u4", 8), ("mp", "<u4", 12),
+           ("next_mp", "<u4", 16), ("mv", "u1", 20), ("next_mv", "u1", 21)]
+          + [("mv_access_" + n, f, 24 + o) for n, f, o in ACCESS]
+          + [("next_mv_access_" + n, f, 36 + o) for n, f, o in ACCESS], 48)
+ALU = _dt([("pc", "<u4", 0), ("opcode", "u1", 4), ("next_mv", "u1", 5), ("mv", "u1", 6)], 8)
+JUMP = _dt([("pc", "<u4", 0), ("next_pc", "<u4", 4), ("opcode", "u1", 8), ("dst", "<u4", 12),
+            ("mv", "u1", 16)], 20)
+MEM_INSTR = _dt([("clk", "<u4", 0), ("pc", "<u4", 4), ("opcode", "u1", 8), ("mp", "<u4", 12),
+                 ("next_mp", "<u4", 16)], 20)
+IO = _dt([("pc", "<u4", 0), ("opcode", "u1", 4), ("mp", "<u4", 8), ("mv", "u1", 12)], 16)
+MEMORY = _dt([("addr", "<u4", 0), ("initial_timestamp", "<u4", 4), ("final_timestamp", "<u4", 8),
+              ("initial_value", "u1", 12), ("final_value", "u1", 13)], 16)
+
+# bfz_execute_events stream: the same fields packed (no padding), in declaration order
+_P_ACCESS = [("kind", "u1"), ("value", "u1"), ("prev_value", "u1"), ("timestamp", "<u4"),
+             ("prev_timestamp", "<u4")]
+_PACKED = {
+    "cpu": np.dtype([("clk", "<u4"), ("pc", "<u4"), ("next_pc", "<u4"), ("mp", "<u4"),
+                     ("next_mp", "<u4"), ("mv", "u1"), ("next_mv", "u1")]
+                    + [("mv_access_" + n, f) for n, f in _P_ACCESS]
+                    + [("next_mv_access_" + n, f) for n, f in _P_ACCESS]),
+    "alu": np.dtype([("pc", "<u4"), ("opcode", "u1"), ("next_mv", "u1"), ("mv", "u1")]),
+    "jump": np.dtype([("pc", "<u4"), ("next_pc", "<u4"), ("opcode", "u1"), ("dst", "<u4"),
+                      ("mv", "u1")]),
+    "memory_instr": np.dtype([("clk", "<u4"), ("pc", "<u4"), ("opcode", "u1"), ("mp", "<u4"),
+                              ("next_mp", "<u4")]),
+    "io": np.dtype([("pc", "<u4"), ("opcode", "u1"), ("mp", "<u4"), ("mv", "u1")]),
+    "memory": np.dtype([("addr", "<u4"), ("initial_timestamp", "<u4"), ("final_timestamp", "<u4"),
+                        ("initial_value", "u1"), ("final_value", "u1")]),
+}
+_ALIGNED = {"cpu": CPU, "alu": ALU, "jump": JUMP, "memory_instr": MEM_INSTR, "io": IO,
+            "memory": MEMORY}
+# Opcode discriminants (crates/core/executor/src/opcode.rs:13-30)
+ADD, SUB = 2, 3
+
+
+def _aligned(packed: np.ndarray, dt: np.dtype) -> np.ndarray:
+    out = np.zeros(len(packed), dtype=dt)
+    for name in packed.dtype.names:
+        out[name] = packed[name]
+    return out
+
+
+@dataclass
+class ExecutionRecordArrays:
+    """ExecutionRecord's event vectors (record.rs:15-34) in the bfz_events layout."""
+    cpu: np.ndarray
+    add: np.ndarray
+    sub: np.ndarray
+    jump: np.ndarray
+    io: np.ndarray
+    memory_instr: np.ndarray
+    memory: np.ndarray  # cpu_memory_access, any order
+    global_clk: int = 0
+    output: bytes = b""
+
+    @staticmethod
+    def from_executor(elf: str, stdin, executor: int = 0) -> "ExecutionRecordArrays":
+        """Executor::run (executor.rs:71-79) on (elf, stdin): every ALU event is an add_event
+        (the reference executor pushes Add and Sub alike to add_events, executor.rs:219-226)."""
+        buf, n = u8buf(bytes(stdin))
+        p = ctypes.POINTER(ctypes.c_uint8)()
+        ln = ctypes.c_size_t()
+        check(lib().bfz_execute_events(elf.encode(), buf, n, int(executor), ctypes.byref(p),
+                                       ctypes.byref(ln)))
+        blob = _lib.take_bytes(p, ln.value)
+        off = 0
+        arrs = {}
+        for key in ("cpu", "alu", "jump", "memory_instr", "io", "memory"):
+            cnt = struct.unpack_from("<Q", blob, off)[0]
+            off += 8
+            dt = _PACKED[key]
+            packed = np.frombuffer(blob, dtype=dt, count=cnt, offset=off)
+            off += cnt * dt.itemsize
+            arrs[key] = _aligned(packed, _ALIGNED[key])
+        gclk = struct.unpack_from("<Q", blob, off)[0]
+        off += 8 + 8  # global_clk, pc, mp
+        nout = struct.unpack_from("<Q", blob, off)[0]
+        out = bytes(blob[off + 8: off + 8 + nout])
+        return ExecutionRecordArrays(cpu=arrs["cpu"], add=arrs["alu"],
+                                     sub=np.zeros(0, dtype=ALU), jump=arrs["jump"], io=arrs["io"],
+                                     memory_instr=arrs["memory_instr"], memory=arrs["memory"],
+                                     global_clk=gclk, output=out)
+
+    def as_c(self) -> "_lib.Events":
+        ev = _lib.Events()
+        for name in ("cpu", "add", "sub", "jump", "io", "memory_instr", "memory"):
+            a = getattr(self, name)
+            assert a.dtype == {"add": ALU, "sub": ALU}.get(name, _ALIGNED.get(name)), name
+            assert a.flags["C_CONTIGUOUS"], name
+            setattr(ev, name, a.ctypes.data if len(a) else None)
+            setattr(ev, "n_" + name, len(a))
+        return ev
+
+
+class DeviceRecord:
+    """bfz_record: the events resident in HBM (freed on drop)."""
+
+    def __init__(self, handle: int):
+        self.handle = handle
+
+    def __del__(self):
+        if getattr(self, "handle", None):
+            lib().bfz_record_free(ctypes.c_void_p(self.handle))
+            self.handle = None
+
+
+def record_from_events(pk, rec: ExecutionRecordArrays) -> DeviceRecord:
+    """bfz_record_from_events: the record utils::prove hands to MachineProver::prove, on the
+    device (memory events put in address order; events validated)."""
+    _lib.init()
+    c = rec.as_c()
+    out = ctypes.c_void_p()
+    check(lib().bfz_record_from_events(ctypes.c_void_p(pk.handle), ctypes.byref(c),
+                                       ctypes.byref(out)))
+    return DeviceRecord(out.value)

@@ -309,6 +309,123 @@ class CoreProver:
         return take_bytes(ptr, plen.value)
 
 
+@dataclass
+class StarkProvingKey:
+    """StarkProvingKey on the host (crates/stark/src/machine.rs:49-60) as pk_to_host returns it:
+    the preprocessed commit and traces in the key's order (sorted (Reverse(height), name),
+    machine.rs:182-183), chip_ordering and local_only.  traces: [(chip id, name, array)] with
+    each array the row-major Montgomery matrix (RowMajorMatrix<KoalaBear>::values)."""
+    commit: List[int]
+    traces: list
+    chip_ordering: dict
+    local_only: list
+
+
+class DeviceProvingKey:
+    """MachineProver::DeviceProvingKey made by pk_to_device (a bfz_pk handle, freed on drop)."""
+
+    def __init__(self, handle: int, commit):
+        self.handle = handle
+        self.commit = list(commit)
+
+    def __del__(self):
+        if getattr(self, "handle", None):
+            lib().bfz_pk_free(ctypes.c_void_p(self.handle))
+            self.handle = None
+
+
+# local_only per chip (Chip::local_only; the preprocessed chips Program and Byte are not)
+_LOCAL_ONLY = {"Cpu": False, "Program": False, "AddSub": True, "Jump": True, "Memory": False,
+               "Byte": False, "MemoryInstrs": False, "IO": True}
+
+
+def _pk_to_host(pk) -> StarkProvingKey:
+    import numpy as np
+    commit = (ctypes.c_uint32 * 8)()
+    check(lib().bfz_pk_commit(ctypes.c_void_p(pk.handle), commit))
+    named = []
+    for c, name in enumerate(CHIPS):
+        p = ctypes.POINTER(ctypes.c_uint32)()
+        h, w = ctypes.c_size_t(), ctypes.c_size_t()
+        buf, n = u8buf(b"")
+        rc = lib().bfz_trace(pk.elf.encode(), buf, n, c, 1, ctypes.byref(p), ctypes.byref(h),
+                             ctypes.byref(w))
+        if rc == 1:
+            continue
+        check(rc)
+        arr = np.ctypeslib.as_array(p, shape=(h.value * w.value,)).copy().reshape(h.value, w.value)
+        lib().bfz_free(p)
+        named.append((c, name, arr))
+    named.sort(key=lambda t: (-t[2].shape[0], t[1]))  # machine.rs:182-183
+    return StarkProvingKey(commit=list(commit), traces=named,
+                           chip_ordering={name: i for i, (_, name, _) in enumerate(named)},
+                           local_only=[_LOCAL_ONLY[name] for _, name, _ in named])
+
+
+def _pk_to_device(hpk: StarkProvingKey) -> DeviceProvingKey:
+    mats, chips, ptrs, hs, ws, k = _trace_args(hpk.traces)
+    commit = (ctypes.c_uint32 * 8)(*hpk.commit)
+    out = ctypes.c_void_p()
+    check(lib().bfz_pk_from_host(chips, ptrs, hs, ws, k, commit, ctypes.byref(out)))
+    return DeviceProvingKey(out.value, hpk.commit)
+
+
+CoreProver.pk_to_host = staticmethod(_pk_to_host)
+CoreProver.pk_to_host.__doc__ = "MachineProver::pk_to_host (prover.rs:55,205-207)."
+CoreProver.pk_to_device = staticmethod(_pk_to_device)
+CoreProver.pk_to_device.__doc__ = ("MachineProver::pk_to_device (prover.rs:52,201-203) -> "
+                                   "bfz_pk_from_host: refuses traces or a commit that do not match.")
+
+
+@dataclass
+class HostBfProvingKey:
+    """BfProvingKey (crates/prover/src/types.rs:8-15) exactly as BfProver::setup builds it:
+    the HOST key pk_to_host(pk), the elf and the vk (crates/prover/src/lib.rs:46-56)."""
+    pk: StarkProvingKey
+    elf: str
+    vk: BfVerifyingKey
+
+
+class BfProver:
+    """BfProver<HipProverComponents> (crates/prover/src/lib.rs:28-90) -- the reference's own
+    flow around the HIP core prover:
+      setup: MachineProver::setup, keep pk_to_host(pk)                       (lib.rs:46-56)
+      prove: pk_to_device(pk.pk) every time, Executor::run, then the HipProver::prove override:
+             observe_into, bfz_record_from_events (the record's events to HBM, traces and
+             byte-lookup multiplicities generated there), commit, open on a clone (lib.rs:70-90,
+             utils/prove.rs:23-66, prover.rs:560-582)."""
+
+    def __init__(self):
+        self.core = CoreProver()
+
+    def setup(self, elf: str):
+        init()
+        h = ctypes.c_void_p()
+        commit = (ctypes.c_uint32 * 8)()
+        check(lib().bfz_setup(elf.encode(), ctypes.byref(h), commit))
+        vk = BfVerifyingKey(commit=list(commit), elf=elf)
+        dpk = BfProvingKey(handle=h.value, elf=elf, vk=vk)
+        pk = HostBfProvingKey(pk=self.core.pk_to_host(dpk), elf=elf, vk=vk)
+        del dpk  # the device key is dropped, as the reference keeps only the host key
+        return pk, vk
+
+    def prove(self, pk: HostBfProvingKey, stdin) -> BfProofWithPublicValues:
+        from .events import ExecutionRecordArrays, record_from_events
+        dpk = self.core.pk_to_device(pk.pk)                         # lib.rs:76
+        rec = ExecutionRecordArrays.from_executor(pk.elf, stdin)    # Executor::run
+        ch = self.core.new_challenger()                             # config().challenger()
+        self.core.observe_into(dpk, ch)                             # prover.rs:572
+        drec = record_from_events(dpk, rec)
+        data = self.core.commit_record(dpk, drec.handle)
+        opened = Challenger.from_buffer_copy(bytes(ch))             # challenger.clone()
+        proof = self.core.open(dpk, data, opened)                   # prover.rs:578
+        return BfProofWithPublicValues(proof=proof, stdin=bytes(stdin), public_values=rec.output,
+                                       cycles=rec.global_clk)
+
+    def verify(self, proof: BfProofWithPublicValues, vk: BfVerifyingKey) -> None:
+        ProverClient().verify(proof, vk)
+
+
 def set_num_queries(q: int) -> None:
     """FRI_QUERIES override (crates/stark/src/kb31_poseidon2.rs:59-62); 0 = environment/84."""
     check(lib().bfz_set_num_queries(int(q)))

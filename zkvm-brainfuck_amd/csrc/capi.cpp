@@ -2,6 +2,8 @@
 // catches, records the message for bfz_last_error(), and returns a negative status.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstddef>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -296,6 +298,71 @@ void bfz_pk_free(bfz_pk* pk) {
   delete pk;
 }
 
+}  // extern "C"
+namespace {
+// Program text of a Program chip preprocessed trace (program/mod.rs:66-94: row i = pc i, opcode,
+// op_a bytes; rows past the program are zero).  Row 0 is always an instruction (the reference
+// asserts a non-empty program); the first row i > 0 whose pc column is not i starts the padding.
+std::string program_from_prep_trace(const uint32_t* t, size_t h, size_t w) {
+  static const char OPS[8] = {'[', ']', '+', '-', '>', '<', ',', '.'};
+  if (w != 6 || h == 0) throw std::runtime_error("pk_from_host: bad Program preprocessed shape");
+  std::string src;
+  for (size_t i = 0; i < h; i++) {
+    const uint32_t pc = kb::from_mont(t[i * 6]);
+    if (i > 0 && pc != i) break;
+    const uint32_t op = kb::from_mont(t[i * 6 + 1]);
+    if (op > 7) throw std::runtime_error("pk_from_host: bad opcode in the Program trace");
+    src.push_back(OPS[op]);
+  }
+  return src;
+}
+}  // namespace
+extern "C" {
+
+int bfz_pk_from_host(const int* chips, const uint32_t* const* traces, const size_t* heights,
+                     const size_t* widths, size_t n, const uint32_t commit[8], bfz_pk** pk) {
+  return guarded([&] {
+    if (!chips || !traces || !heights || !widths || !commit || !pk)
+      throw std::runtime_error("null argument");
+    if (n != 2) throw std::runtime_error("pk_from_host: expected the Program and Byte preprocessed traces");
+    int ip = -1, ib = -1;
+    for (size_t i = 0; i < n; i++) {
+      if (chips[i] == bfz::CHIP_PROGRAM && ip < 0) ip = (int)i;
+      else if (chips[i] == bfz::CHIP_BYTE && ib < 0) ib = (int)i;
+      else throw std::runtime_error("pk_from_host: preprocessed chips must be Program and Byte");
+    }
+    for (size_t i = 0; i < n; i++) {
+      const size_t need = (size_t)bfz::CHIP_INFO[chips[i]].prep_w;
+      if (widths[i] != need || !traces[i] || heights[i] == 0 || heights[i] > ((size_t)1 << 23))
+        throw std::runtime_error(std::string("pk_from_host: bad shape for ") +
+                                 bfz::CHIP_INFO[chips[i]].name);
+    }
+    const std::string src = program_from_prep_trace(traces[ip], heights[ip], widths[ip]);
+    const bfz::Program prog = bfz::Program::parse(src);  // unmatched brackets throw
+    for (size_t i = 0; i < n; i++) {  // both traces are exactly setup(program)'s
+      std::vector<uint32_t> want;
+      const size_t h = bfz::prep_trace(chips[i], prog, want);
+      if (h != heights[i] || std::memcmp(want.data(), traces[i], want.size() * 4) != 0)
+        throw std::runtime_error(std::string("pk_from_host: preprocessed trace of ") +
+                                 bfz::CHIP_INFO[chips[i]].name + " is not the program's");
+    }
+    auto k = std::make_unique<bfz_pk>();
+    k->pk = cached_setup(src);
+    if (std::memcmp(k->pk->prep.tree.root, commit, 32) != 0)
+      throw std::runtime_error("pk_from_host: preprocessed commitment mismatch");
+    *pk = k.release();
+    return 0;
+  });
+}
+
+int bfz_pk_commit(const bfz_pk* pk, uint32_t commit[8]) {
+  return guarded([&] {
+    if (!pk || !commit) throw std::runtime_error("null argument");
+    std::memcpy(commit, pk->pk->prep.tree.root, 32);
+    return 0;
+  });
+}
+
 int bfz_prove(const bfz_pk* pk, const uint8_t* in, size_t nin, uint8_t** proof, size_t* len) {
   return guarded([&] { return emit(bfz::prove(*pk->pk, in, nin, opts(), nullptr), proof, len); });
 }
@@ -328,8 +395,13 @@ bfz::Challenger from_c(const bfz_challenger* c) {
   for (uint32_t i = 0; i < c->n_output; i++) ch.out[i] = c->output_buffer[i];
   ch.nin = (int)c->n_input;
   ch.nout = (int)c->n_output;
+  // every word the challenger may permute or return must be a canonical Montgomery residue
   for (int i = 0; i < 16; i++)
     if (ch.st[i] >= kb::P) throw std::runtime_error("challenger: non-canonical word");
+  for (int i = 0; i < ch.nin; i++)
+    if (ch.in[i] >= kb::P) throw std::runtime_error("challenger: non-canonical input word");
+  for (int i = 0; i < ch.nout; i++)
+    if (ch.out[i] >= kb::P) throw std::runtime_error("challenger: non-canonical output word");
   return ch;
 }
 void to_c(const bfz::Challenger& ch, bfz_challenger* c) {
@@ -383,13 +455,16 @@ int bfz_record_main_commit(const bfz_pk* pk, const bfz_record* rec, bfz_main_dat
   });
 }
 
-int bfz_open(const bfz_pk* pk, bfz_main_data* data, const bfz_challenger* ch, uint8_t** proof,
+int bfz_open(const bfz_pk* pk, bfz_main_data* data, bfz_challenger* ch, uint8_t** proof,
              size_t* len) {
   return guarded([&] {
     if (!pk || !data || !ch) throw std::runtime_error("null argument");
     if (data->pk && data->pk != pk->pk)
       throw std::runtime_error("open: main data was committed for another key");
-    return emit(bfz::open_main(*pk->pk, data->md, from_c(ch), opts()), proof, len);
+    bfz::Challenger after;
+    emit(bfz::open_main(*pk->pk, data->md, from_c(ch), opts(), &after), proof, len);
+    to_c(after, ch);  // MachineProver::open advances its &mut challenger
+    return 0;
   });
 }
 
@@ -458,6 +533,97 @@ int bfz_record_new(const bfz_pk* pk, const uint8_t* in, size_t nin, bfz_record**
     bfz::upload_events(h, pk->pk->program, r->ev, bfz::stream());
     r->cycles = h.global_clk;
     if (cycles) *cycles = h.global_clk;
+    *rec = r.release();
+    return 0;
+  });
+}
+
+// The C event structs are the device record's layout (machine.h), so the caller's arrays go to
+// HBM as they are.
+}  // extern "C"
+namespace {
+template <class C, class D>
+constexpr bool same_size() { return sizeof(C) == sizeof(D) && alignof(C) == alignof(D); }
+static_assert(same_size<bfz_cpu_event, bfz::CpuEvent>() && same_size<bfz_alu_event, bfz::AluEvent>() &&
+              same_size<bfz_jump_event, bfz::JumpEvent>() &&
+              same_size<bfz_mem_instr_event, bfz::MemInstrEvent>() &&
+              same_size<bfz_io_event, bfz::IoEvent>() && same_size<bfz_memory_event, bfz::MemoryEvent>(),
+              "bfz.h event structs must match machine.h");
+static_assert(offsetof(bfz_cpu_event, mv) == offsetof(bfz::CpuEvent, mv) &&
+              offsetof(bfz_cpu_event, mv_access) == offsetof(bfz::CpuEvent, mv_access) &&
+              offsetof(bfz_cpu_event, next_mv_access) == offsetof(bfz::CpuEvent, next_mv_access) &&
+              offsetof(bfz_memory_access, timestamp) == offsetof(bfz::MemAccess, ts) &&
+              offsetof(bfz_memory_access, prev_timestamp) == offsetof(bfz::MemAccess, prev_ts) &&
+              offsetof(bfz_memory_access, prev_value) == offsetof(bfz::MemAccess, prev_value) &&
+              offsetof(bfz_alu_event, mv) == offsetof(bfz::AluEvent, mv) &&
+              offsetof(bfz_jump_event, dst) == offsetof(bfz::JumpEvent, dst) &&
+              offsetof(bfz_jump_event, mv) == offsetof(bfz::JumpEvent, mv) &&
+              offsetof(bfz_mem_instr_event, next_mp) == offsetof(bfz::MemInstrEvent, next_mp) &&
+              offsetof(bfz_io_event, mv) == offsetof(bfz::IoEvent, mv) &&
+              offsetof(bfz_memory_event, final_value) == offsetof(bfz::MemoryEvent, final_v),
+              "bfz.h event field offsets must match machine.h");
+
+template <class D, class C>
+void put_events(bfz::DBuf<D>& d, const C* src, size_t n, hipStream_t st) {
+  if (n && !src) throw std::runtime_error("record_from_events: null event array");
+  d.reset(std::max<size_t>(n, 1));
+  bfz::upload_bulk(d.p, src, n * sizeof(D), st);
+}
+}  // namespace
+extern "C" {
+
+int bfz_record_from_events(const bfz_pk* pk, const bfz_events* e, bfz_record** rec) {
+  return guarded([&] {
+    if (!pk || !e || !rec) throw std::runtime_error("null argument");
+    if (e->n_cpu == 0) throw std::runtime_error("record_from_events: no cpu events");
+    const size_t lim = (size_t)1 << 26;  // beyond any committable trace (2^23 rows)
+    if (e->n_cpu > lim || e->n_add + e->n_sub > lim || e->n_jump > lim || e->n_io > lim ||
+        e->n_memory_instr > lim || e->n_memory > 2 * lim)
+      throw std::runtime_error("record_from_events: event count out of range");
+    hipStream_t st = bfz::stream();
+    auto r = std::make_unique<bfz_record>();
+    bfz::DeviceEvents& ev = r->ev;
+    put_events(ev.cpu, e->cpu, e->n_cpu, st);
+    // AddSubChip rows: add_events then sub_events (alu/mod.rs:72)
+    const size_t nalu = e->n_add + e->n_sub;
+    if ((e->n_add && !e->add) || (e->n_sub && !e->sub))
+      throw std::runtime_error("record_from_events: null event array");
+    ev.alu.reset(std::max<size_t>(nalu, 1));
+    bfz::upload_bulk(ev.alu.p, e->add, e->n_add * sizeof(bfz::AluEvent), st);
+    bfz::upload_bulk(ev.alu.p + e->n_add, e->sub, e->n_sub * sizeof(bfz::AluEvent), st);
+    put_events(ev.jump, e->jump, e->n_jump, st);
+    put_events(ev.meminstr, e->memory_instr, e->n_memory_instr, st);
+    put_events(ev.io, e->io, e->n_io, st);
+    // cpu_memory_access in the normal form: sorted by address (the reference's order is that of
+    // a HashMap drain, executor.rs:74); one event per address
+    if (e->n_memory && !e->memory) throw std::runtime_error("record_from_events: null event array");
+    std::vector<bfz::MemoryEvent> mem(e->n_memory);
+    if (e->n_memory) std::memcpy(mem.data(), e->memory, mem.size() * sizeof(bfz::MemoryEvent));
+    std::sort(mem.begin(), mem.end(), [](const bfz::MemoryEvent& a, const bfz::MemoryEvent& b) {
+      return a.addr < b.addr;
+    });
+    for (size_t i = 1; i < mem.size(); i++)
+      if (mem[i].addr == mem[i - 1].addr)
+        throw std::runtime_error("record_from_events: two memory events for one address");
+    put_events(ev.memory, mem.data(), mem.size(), st);
+    const bfz::Program& prog = pk->pk->program;
+    ev.prog.reset(std::max<size_t>(prog.instructions.size(), 1));
+    HIP_CHECK(hipMemcpyAsync(ev.prog.p, prog.instructions.data(),
+                             prog.instructions.size() * sizeof(bfz::Instruction),
+                             hipMemcpyHostToDevice, st));
+    bfz::EventCounts n;
+    n.cpu = e->n_cpu;
+    n.alu = nalu;
+    n.jump = e->n_jump;
+    n.meminstr = e->n_memory_instr;
+    n.io = e->n_io;
+    n.memory = mem.size();
+    n.program = prog.instructions.size();
+    bfz::set_event_meta(ev, n, e->n_cpu);
+    if (const size_t bad = bfz::count_invalid_events(ev, st))
+      throw std::runtime_error("record_from_events: " + std::to_string(bad) +
+                               " events out of range (pc outside the program, opcode or access kind)");
+    r->cycles = e->n_cpu;
     *rec = r.release();
     return 0;
   });

@@ -132,10 +132,11 @@ struct MainData {
 void commit_main(MainData& md);  // md.dt holds the traces
 // Challenger state after pk.observe_into (prover.rs:595-601) on a fresh DuplexChallenger.
 Challenger challenger_after_pk(const ProvingKey& pk);
-// ch = the prover's challenger after pk.observe_into; not modified (the reference opens on a
+// ch = the prover's challenger after pk.observe_into.  *after (optional) receives the state at
+// the end of the opening (the trait's open advances its &mut challenger; prove opens on a
 // clone, prover.rs:578).  md may be opened more than once.
 std::vector<uint8_t> open_main(const ProvingKey& pk, MainData& md, const Challenger& ch,
-                               const ProveOptions& opt);
+                               const ProveOptions& opt, Challenger* after = nullptr);
 
 int num_queries_from_env();
 bool observe_openings_from_env();  // BFZ_OBSERVE_OPENINGS = 1 (default) | 0

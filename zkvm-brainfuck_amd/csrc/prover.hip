@@ -320,9 +320,10 @@ void upload_host_traces(const int* chips, const uint32_t* const* mats, const siz
     const int w = CHIP_INFO[c].main_w;
     if ((size_t)w != widths[i])
       throw std::runtime_error(std::string("traces: width mismatch for ") + CHIP_INFO[c].name);
-    // height >= 2: a 1-row trace has a 2-row LDE that the FRI commit phase never folds into
-    if (h < 2 || (h & (h - 1)) || h > ((size_t)1 << 23))
-      throw std::runtime_error(std::string("traces: height not a power of two in [2, 2^23] for ") +
+    // a 1-row trace is legal (the Cpu chip of a one-cycle program, cpu/trace.rs:33): its 2-row
+    // LDE's reduced opening joins the FRI layer after the last fold
+    if (h < 1 || (h & (h - 1)) || h > ((size_t)1 << 23))
+      throw std::runtime_error(std::string("traces: height not a power of two in [1, 2^23] for ") +
                                CHIP_INFO[c].name);
     DBuf<uint32_t> rm(h * w);
     upload_bulk(rm.p, mats[i], h * w * 4, st);
@@ -412,7 +413,7 @@ void commit_main_impl(MainData& md, ProofScope& ps) {
 }
 
 std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch,
-                               const ProveOptions& opt, ProofScope& ps);
+                               const ProveOptions& opt, ProofScope& ps, Challenger* after = nullptr);
 
 // Sharded chips' quotient values: rank j computed LDE positions [j b, (j+1) b) (b = 2n / G),
 // which land in chunk (j b) / n at rows [(j b) mod n, + b) of its 4 columns.  One all-gather of
@@ -459,9 +460,9 @@ void commit_main(MainData& md) {
 }
 
 std::vector<uint8_t> open_main(const ProvingKey& pk, MainData& md, const Challenger& ch,
-                               const ProveOptions& opt) {
+                               const ProveOptions& opt, Challenger* after) {
   ProofScope ps(false, nullptr);
-  return open_impl(pk, md, ch, opt, ps);
+  return open_impl(pk, md, ch, opt, ps, after);
 }
 
 Challenger challenger_after_pk(const ProvingKey& pk) {
@@ -488,7 +489,7 @@ namespace {
 // reference opens on a clone of it, prover.rs:578): observe the main commit, LogUp, quotient,
 // PCS open, FRI, grind, queries, BFZ1 serialization.
 std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch,
-                               const ProveOptions& opt, ProofScope& ps) {
+                               const ProveOptions& opt, ProofScope& ps, Challenger* after) {
   hipStream_t st = stream();
   EvTimer& ev = ps.ev;
   StageTimes* tms = ps.tms;
@@ -1007,6 +1008,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   const int nq = opt.num_queries;
   std::vector<uint32_t> qidx(nq);
   for (int q = 0; q < nq; q++) qidx[q] = ch.sample_bits(Lmax);
+  if (after) *after = ch;  // the transcript is complete: MachineProver::open's &mut challenger
 
   // ---- query openings: gather every opened word in proof order
   // Opening segments in serialization order (same for every query; see GatherSeg).

@@ -32,6 +32,10 @@ void upload_events(const HostEvents& h, const Program& prog, DeviceEvents& ev, h
 // Chip inclusion, heights and counts of ev from the event counts (the device buffers are set
 // by the caller).
 void set_event_meta(DeviceEvents& ev, const EventCounts& n, uint64_t global_clk);
+// Events that came from outside (bfz_record_from_events): the number of events a kernel must
+// not read -- a cpu pc outside the program (k_trace_cpu / k_deps index by it), an opcode or
+// memory-access kind out of range.  Counted on the device after the upload.
+size_t count_invalid_events(const DeviceEvents& ev, hipStream_t st);
 // Pinned host memory for HostEvents (hipHostMalloc / hipHostFree).
 void* pinned_alloc(size_t bytes);
 void pinned_free(void* p);

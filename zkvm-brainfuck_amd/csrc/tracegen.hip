@@ -363,6 +363,46 @@ void upload_events(const HostEvents& h, const Program& prog, DeviceEvents& ev, h
   HIP_CHECK(hipStreamSynchronize(st));
 }
 
+namespace {
+__global__ __launch_bounds__(256) void k_check_events(const CpuEvent* __restrict__ cpu, size_t ncpu,
+                                                      const AluEvent* __restrict__ alu, size_t nalu,
+                                                      const JumpEvent* __restrict__ jump, size_t njump,
+                                                      const MemInstrEvent* __restrict__ mi, size_t nmi,
+                                                      const IoEvent* __restrict__ io, size_t nio,
+                                                      uint32_t nprog, unsigned* __restrict__ bad) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned b = 0;
+  for (size_t i = i0; i < ncpu; i += stride) {
+    const CpuEvent e = cpu[i];
+    b += e.pc >= nprog || e.mv_access.kind > 2 || e.next_mv_access.kind > 2;
+  }
+  for (size_t i = i0; i < nalu; i += stride) b += alu[i].opcode != OP_ADD && alu[i].opcode != OP_SUB;
+  for (size_t i = i0; i < njump; i += stride)
+    b += jump[i].opcode != OP_LOOP_START && jump[i].opcode != OP_LOOP_END;
+  for (size_t i = i0; i < nmi; i += stride) b += mi[i].opcode != OP_MEM_FWD && mi[i].opcode != OP_MEM_BWD;
+  for (size_t i = i0; i < nio; i += stride) b += io[i].opcode != OP_INPUT && io[i].opcode != OP_OUTPUT;
+  if (b) atomicAdd(bad, b);
+}
+}  // namespace
+
+size_t count_invalid_events(const DeviceEvents& ev, hipStream_t st) {
+  DBuf<unsigned> bad(1);
+  HIP_CHECK(hipMemsetAsync(bad.p, 0, sizeof(unsigned), st));
+  size_t most = 0;
+  for (int c : {CHIP_CPU, CHIP_ADDSUB, CHIP_JUMP, CHIP_MEMINSTRS, CHIP_IO}) most = std::max(most, ev.n[c]);
+  const unsigned grid = std::max(1u, std::min<unsigned>(ceil_div(most, 256 * 4), 2048));
+  hipLaunchKernelGGL(k_check_events, dim3(grid), dim3(256), 0, st, (const CpuEvent*)ev.cpu.p,
+                     ev.n[CHIP_CPU], (const AluEvent*)ev.alu.p, ev.n[CHIP_ADDSUB],
+                     (const JumpEvent*)ev.jump.p, ev.n[CHIP_JUMP], (const MemInstrEvent*)ev.meminstr.p,
+                     ev.n[CHIP_MEMINSTRS], (const IoEvent*)ev.io.p, ev.n[CHIP_IO],
+                     (uint32_t)ev.n[CHIP_PROGRAM], bad.p);
+  KCHECK();
+  unsigned h = 0;
+  fetch(&h, bad.p, sizeof h, st);
+  return h;
+}
+
 void* pinned_alloc(size_t bytes) {
   void* p = nullptr;
   if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;

@@ -199,7 +199,9 @@ bool verify_shard(const std::string& src, const uint32_t vk_commit[8], const Sha
     for (uint32_t i = 0; i < nc; i++) {
       const ChipOpened& o = pf.opened[i];
       // unsigned: a huge word must not become a negative shift count below
-      if (o.log_degree < 1 || o.log_degree > 23) throw std::runtime_error("log degree out of range");
+      // log degree 0 is a 1-row trace (the Cpu chip of a one-cycle program: cpu/trace.rs:33
+      // pads to next_power_of_two with no minimum)
+      if (o.log_degree > 23) throw std::runtime_error("log degree out of range");
       co.push_back(ChipOpen{(int)o.log_degree, o.prep_local, o.prep_next, o.main_local, o.main_next,
                             o.perm_local, o.perm_next, o.quotient, o.cumsum});
       const ChipOpen& c = co.back();
@@ -368,6 +370,13 @@ bool verify_shard(const std::string& src, const uint32_t vk_commit[8], const Sha
         const uint32_t x1 = mneg(x0);
         const EF t = ef_mul(ef_sub(betas[s], ef_base(x0)), ef_sub(ev[1], ev[0]));
         folded = ef_add(ev[0], ef_mul_base(t, minv(msub(x1, x0))));
+      }
+      {  // a 1-row trace's height-2 input joins after the last fold, as in the commit phase (D11)
+        auto it = ro.find(log_max - (int)ncommit);
+        if (it != ro.end()) {
+          folded = ef_add(folded, it->second.second);
+          ro.erase(it);
+        }
       }
       if (!ro.empty()) throw std::runtime_error("unconsumed reduced openings");
       if (!ef_eq(folded, final_poly)) throw std::runtime_error("FRI final value mismatch");
