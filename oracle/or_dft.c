@@ -58,20 +58,33 @@ void or_intt(fp* a, int lg) {
   for (size_t i = 0; i < n; i++) a[i] = fp_mul(a[i], ninv);
 }
 
+/* Columns are transformed one at a time (textbook NTT per column), in groups of OR_LDE_GROUP
+ * adjacent columns so the row-major gather and scatter touch whole cache lines. */
+#define OR_LDE_GROUP 16
 void or_coset_lde(const fp* in, size_t n, size_t w, fp shift, int log_blowup, fp* out) {
   int lg = or_log2(n);
   int lgN = lg + log_blowup;
   size_t N = n << log_blowup;
   fp gN = fp_two_adic_gen(lgN);
+  long ngroups = (long)((w + OR_LDE_GROUP - 1) / OR_LDE_GROUP);
 #pragma omp parallel for schedule(dynamic, 1)
-  for (long c = 0; c < (long)w; c++) {
-    fp* a = calloc(N, sizeof(fp));
-    for (size_t i = 0; i < n; i++) a[i] = in[i * w + c];
-    or_intt(a, lg);
-    fp p = 1;
-    for (size_t k = 0; k < n; k++) { a[k] = fp_mul(a[k], p); p = fp_mul(p, shift); }
-    or_ntt(a, lgN, gN);
-    for (size_t r = 0; r < N; r++) out[r * w + c] = a[or_bitrev(r, lgN)];
+  for (long g = 0; g < ngroups; g++) {
+    size_t c0 = (size_t)g * OR_LDE_GROUP;
+    size_t gw = w - c0 < OR_LDE_GROUP ? w - c0 : OR_LDE_GROUP;
+    fp* a = calloc(N * gw, sizeof(fp)); /* column k of the group at a + k N */
+    for (size_t i = 0; i < n; i++)
+      for (size_t k = 0; k < gw; k++) a[k * N + i] = in[i * w + c0 + k];
+    for (size_t k = 0; k < gw; k++) {
+      fp* col = a + k * N;
+      or_intt(col, lg);
+      fp p = 1;
+      for (size_t j = 0; j < n; j++) { col[j] = fp_mul(col[j], p); p = fp_mul(p, shift); }
+      or_ntt(col, lgN, gN);
+    }
+    for (size_t r = 0; r < N; r++) {
+      size_t src = or_bitrev(r, lgN);
+      for (size_t k = 0; k < gw; k++) out[r * w + c0 + k] = a[k * N + src];
+    }
     free(a);
   }
 }

@@ -20,6 +20,23 @@ P = 0x7F000001
 # (log n, columns): the small case runs at 1, 2 and 4 ranks; the second is the "2-rank gloo
 # run at >= 2^18 x 64" of VERDICT r1 (Next 1)
 SHAPES = {"small": (14, 16), "mid": (18, 64)}
+# BASELINE configs 4 and 5 at their multi-rank shape (VERDICT r2 Next 3): columns generated on
+# the device column by column from per-column seeds, so every rank makes only its own columns
+# and world = 1 makes the same matrix
+GEN_SHAPES = {"c4": (20, 256), "c5": (20, 1024)}
+
+
+def _gen_cols(logn, c0, c1):
+    """columns [c0, c1) of the generated trace: int32 CUDA tensor (c1 - c0, 2^logn) of uniform
+    Montgomery words (any word < p is a field element in either form)"""
+    import torch
+    dev = torch.device("cuda", 0)
+    out = torch.empty((c1 - c0, 1 << logn), dtype=torch.int32, device=dev)
+    g = torch.Generator(device=dev)
+    for c in range(c0, c1):
+        g.manual_seed(0xC0175EED + 7919 * c + logn)
+        out[c - c0] = torch.randint(0, P, (1 << logn,), dtype=torch.int32, device=dev, generator=g)
+    return out
 
 
 def _trace(logn, w):
@@ -58,10 +75,15 @@ def _worker(rank, world, port, q, shape):
         from bfz import _lib, shard
         dist.init_process_group("gloo", rank=rank, world_size=world)
         _lib.init(0)
-        logn, w = SHAPES[shape]
-        m = _trace(logn, w)
-        wl = w // world
-        cols = _device_cols(m, rank * wl, (rank + 1) * wl)
+        if shape in GEN_SHAPES:
+            logn, w = GEN_SHAPES[shape]
+            wl = w // world
+            cols = _gen_cols(logn, rank * wl, (rank + 1) * wl)
+        else:
+            logn, w = SHAPES[shape]
+            m = _trace(logn, w)
+            wl = w // world
+            cols = _device_cols(m, rank * wl, (rank + 1) * wl)
         root, fri, fin = shard.commit_fri_sharded(cols, logn, shard.Collectives(dist), rank)
         dist.destroy_process_group()
         q.put((rank, (root.tolist(), fri.tolist(), fin.tolist()), None))
@@ -93,6 +115,13 @@ _SINGLE = {}
 
 
 def single(shape):
+    if shape in GEN_SHAPES and shape not in _SINGLE:
+        sys.path.insert(0, os.path.join(ROOT, "zkvm-brainfuck_amd"))
+        from bfz import _lib, shard
+        _lib.init(0)
+        logn, w = GEN_SHAPES[shape]
+        root, fri, fin = shard.commit_fri_sharded(_gen_cols(logn, 0, w), logn, None)
+        _SINGLE[shape] = None, (root.tolist(), fri.tolist(), fin.tolist())
     if shape not in _SINGLE:
         sys.path.insert(0, os.path.join(ROOT, "zkvm-brainfuck_amd"))
         from bfz import _lib, shard
@@ -123,19 +152,45 @@ def test_sharded_equals_single(world, shape):
 
 
 @pytest.mark.slow
+@pytest.mark.parametrize("world,shape", [(4, "c4"), (8, "c5")])
+def test_configs_4_5_multirank_equal_single(world, shape):
+    """BASELINE config 4 (4 ranks) and config 5 (8 ranks) at their multi-rank shape, 2^20 rows
+    x 256 / 1024 columns: every rank returns exactly the world = 1 roots and final value (the
+    all-to-all moves (N-1)/N of each rank's LDE; gloo ranks sharing the one GPU)."""
+    _, exp = single(shape)
+    res = _run(world, shape)
+    assert len(exp[1]) == GEN_SHAPES[shape][0]
+    for r in range(world):
+        assert res[r] == exp, f"rank {r} differs"
+
+
+@pytest.mark.slow
+@pytest.mark.skipif(os.environ.get("BFZ_HEAVY_TESTS") != "1",
+                    reason="~5 min of oracle time on 16 cores: BFZ_HEAVY_TESTS=1 (profiles/r03/)")
+def test_config5_2pow22x1024_root_matches_oracle():
+    """BASELINE config 5 restated by cell count (2^32 cells = 2^22 x 1024) on
+    one rank: the commitment root equals the oracle's MerkleTreeMmcs root of the coset LDE
+    (16 GB trace and a 32 GB LDE in host memory for the oracle, 2^30 oracle permutations)."""
+    _oracle_root_check(22, 1024)
+
+
+@pytest.mark.slow
 def test_config4_2pow22x256_root_matches_oracle():
     """BASELINE config 4 restated by cell count: a 2^22 x 256 trace through
     bfz_commit_fri_sharded (1 rank) -- the commitment root equals the oracle's MerkleTreeMmcs
     root of the coset LDE, and the FRI input folds to a constant.  The trace is generated and
     laid out on the device (uniform Montgomery words), then handed to the oracle in canonical
     row-major natural order."""
+    _oracle_root_check(22, 256)
+
+
+def _oracle_root_check(logn, w):
     import torch
 
     import oracle_lib as O
     sys.path.insert(0, os.path.join(ROOT, "zkvm-brainfuck_amd"))
     from bfz import _lib, shard
     _lib.init(0)
-    logn, w = 22, 256
     n = 1 << logn
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev)
@@ -155,6 +210,7 @@ def test_config4_2pow22x256_root_matches_oracle():
         blk = (blk * rinv) % P
         m[:, c0:c0 + 32] = blk.index_select(1, rev).t().to(torch.int32).cpu()
     del cols
+    torch.cuda.empty_cache()
     exp = O.merkle_root([O.coset_lde(m.numpy().view(np.uint32), 3)])
     got = [int((int(x) * rinv) % P) for x in root]
     assert got == exp

@@ -96,3 +96,14 @@ def test_sharded_proof_is_bit_exact(world, fri_min):
         assert res[0][i][0] == res[0][i][1], "sharded proof differs from the unsharded one"
         if stdin == [17]:
             assert res[0][i][3] == O.prove(prog, stdin)
+
+
+@pytest.mark.slow
+def test_sharded_headline_two_ranks_is_bit_exact():
+    """The headline workload (FIBO_X4 stdin [255], Cpu 2^22 rows) sharded over 2 ranks: both
+    ranks return the unsharded proof byte for byte (which test_gpu.py checks against the
+    oracle)."""
+    from bfz import guests
+    res = _run(2, [(guests.FIBO_X4, [255])])
+    assert res[0][0][0] == res[1][0][0], "ranks disagree"
+    assert res[0][0][0] == res[0][0][1], "sharded proof differs from the unsharded one"
