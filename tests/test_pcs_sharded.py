@@ -165,12 +165,11 @@ def test_configs_4_5_multirank_equal_single(world, shape):
 
 
 @pytest.mark.slow
-@pytest.mark.skipif(os.environ.get("BFZ_HEAVY_TESTS") != "1",
-                    reason="~5 min of oracle time on 16 cores: BFZ_HEAVY_TESTS=1 (profiles/r03/)")
 def test_config5_2pow22x1024_root_matches_oracle():
     """BASELINE config 5 restated by cell count (2^32 cells = 2^22 x 1024) on
     one rank: the commitment root equals the oracle's MerkleTreeMmcs root of the coset LDE
-    (16 GB trace and a 32 GB LDE in host memory for the oracle, 2^30 oracle permutations)."""
+    (16 GB trace and a 32 GB LDE in host memory for the oracle, 2^30 oracle permutations:
+    ~170 s on the GPU box's 16-core share, profiles/r03/pytest_gpu_configs45.log)."""
     _oracle_root_check(22, 1024)
 
 
