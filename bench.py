@@ -287,6 +287,32 @@ def sharded_latency(dist, pk, rec, rank, world, device, ref_proof, steps=3):
         return {"error": f"{type(e).__name__}: {e}"}
 
 
+def shard_solo(pk, rec, world, steps=3):
+    """Per-rank work of a `world`-GPU sharded proof measured on ONE GPU (VERDICT r2 Next 6):
+    bfz_record_prove_shard_solo runs rank k's share -- the same kernels and sizes as
+    bfz_record_prove_sharded on rank k -- with the exchanges as no-ops, for every k; the slowest
+    rank is the predicted per-proof latency of the N-GPU proof before collective time."""
+    import ctypes
+    from bfz import _lib as _l
+    L = _l.lib()
+    ranks = []
+    for k in range(world):
+        best = None
+        for _ in range(steps):
+            tm = _l.Timings()
+            _l.check(L.bfz_record_prove_shard_solo(ctypes.c_void_p(pk.handle), rec, k, world,
+                                                   ctypes.byref(tm)))
+            if best is None or tm.total_ms < best.total_ms:
+                best = tm
+        ranks.append({"rank": k, "total_ms": round(best.total_ms, 3),
+                      "stages_ms": {n: round(v, 3) for n, v in best.as_dict().items()
+                                    if n.endswith("_ms") and n not in ("total_ms", "lde_ms", "ntt_kernel_ms", "p2_kernel_ms")}})
+    worst = max(r["total_ms"] for r in ranks)
+    return {"world": world, "max_rank_ms": worst, "ranks": ranks,
+            "what": f"each rank's share of a {world}-GPU sharded proof run alone on one GPU with "
+                    "no-op exchanges (bfz_record_prove_shard_solo); excludes collective time"}
+
+
 def sustained(step, seconds, sync):
     """Proofs back to back for about `seconds` after the timed steps (same record, same
     stream): the steady-state rate over many proofs, and a GPU phase long enough for a
@@ -389,6 +415,9 @@ def main():
     ap.add_argument("--sustain-s", type=float, default=8.0,
                     help="replicas mode: seconds of back-to-back proofs after the timed steps "
                          "(0 = skip)")
+    ap.add_argument("--solo-world", type=int, default=0,
+                    help="replicas mode at N=1: also time each rank's share of an N-GPU sharded "
+                         "proof alone (bfz_record_prove_shard_solo), N = this value (0 = skip)")
     ap.add_argument("--log-n", type=int, default=24, help="pcs mode: trace rows = 2^log_n")
     ap.add_argument("--cols", type=int, default=64, help="pcs mode: trace columns")
     args = ap.parse_args()
@@ -505,6 +534,8 @@ def main():
             line["sustained"] = extra["sustained"]
         if world > 1 and not sharded and not args.no_extra and "sharded_proof" in extra:
             line["sharded_proof"] = extra["sharded_proof"]
+        if world == 1 and args.solo_world > 1:
+            line["shard_solo"] = shard_solo(pk, rec, args.solo_world)
         if world == 1 and not args.no_extra:
             line["end_to_end"] = end_to_end(client, pk, prog, stdin)
             line["events_path"] = events_path(pk, prog, stdin, proof)

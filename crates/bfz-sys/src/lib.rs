@@ -182,6 +182,9 @@ extern "C" {
                      out: *mut *mut u32, height: *mut usize, width: *mut usize) -> c_int;
     pub fn bfz_execute_events(elf: *const c_char, stdin_data: *const u8, nin: usize, executor: c_int,
                               out: *mut *mut u8, out_len: *mut usize) -> c_int;
+    pub fn bfz_perm_trace(chip: c_int, main: *const u32, prep: *const u32, height: usize,
+                          alpha: *const u32, beta: *const u32, out: *mut *mut u32,
+                          width: *mut usize, cumsum: *mut u32) -> c_int;
     pub fn bfz_trace_device(elf: *const c_char, stdin_data: *const u8, nin: usize, chip: c_int,
                             out: *mut *mut u32, height: *mut usize, width: *mut usize) -> c_int;
 
@@ -225,6 +228,8 @@ extern "C" {
                                     allreduce_sum: bfz_allreduce_u32_fn, ctx: *mut c_void,
                                     proof: *mut *mut u8, proof_len: *mut usize,
                                     timings: *mut bfz_timings) -> c_int;
+    pub fn bfz_record_prove_shard_solo(pk: *const bfz_pk, rec: *const bfz_record, rank: c_int,
+                                       world: c_int, timings: *mut bfz_timings) -> c_int;
     pub fn bfz_commit_fri_sharded(d_cols: *const u32, log_n: c_int, w_local: usize, rank: c_int,
                                   world: c_int, d_send: *mut u32, d_recv: *mut u32,
                                   alltoall: bfz_alltoall_fn, allgather: bfz_allgather_fn,

@@ -98,6 +98,16 @@ int bfz_trace(const char* elf, const uint8_t* stdin_data, size_t nin, int chip, 
 int bfz_execute_events(const char* elf, const uint8_t* stdin_data, size_t nin, int executor,
                        uint8_t** out, size_t* out_len);
 
+/* generate_permutation_trace (crates/stark/src/permutation.rs:75-148, called at
+ * prover.rs:280-296) of one chip on the device: main (and, for Program/Byte, prep) are
+ * row-major Montgomery traces of `height` rows, alpha/beta the LogUp challenges (EF,
+ * Montgomery).  *out (malloc'd, bfz_free) = the permutation trace flattened to base
+ * (flatten_to_base, prover.rs:318-334), row-major height x *width; cumsum = its last row's
+ * running sum.  Diagnostic entry (the prover keeps the trace in HBM). */
+int bfz_perm_trace(int chip, const uint32_t* main, const uint32_t* prep, size_t height,
+                   const uint32_t alpha[4], const uint32_t beta[4], uint32_t** out, size_t* width,
+                   uint32_t cumsum[4]);
+
 /* Same trace generated on the device from the uploaded events (the prover's own path),
  * returned row-major in natural row order for comparison. */
 int bfz_trace_device(const char* elf, const uint8_t* stdin_data, size_t nin, int chip,
@@ -260,6 +270,14 @@ typedef int (*bfz_allreduce_u32_fn)(void* ctx, uint32_t* data, size_t n);
 int bfz_record_prove_sharded(const bfz_pk* pk, const bfz_record* rec, int rank, int world,
                              bfz_allgather_fn allgather, bfz_allreduce_u32_fn allreduce_sum,
                              void* ctx, uint8_t** proof, size_t* proof_len, bfz_timings* timings);
+
+/* Timing of ONE rank's share of a world-rank sharded proof, run alone on this GPU: the same
+ * kernels and sizes bfz_record_prove_sharded runs on rank `rank`, with every exchange a no-op
+ * (receive buffers keep whatever they hold, so the result is not a proof and is discarded;
+ * the FRI final-constant check is skipped).  Stage times and kernel counters go to *timings.
+ * Predicts the per-rank critical path of an N-GPU proof without N GPUs. */
+int bfz_record_prove_shard_solo(const bfz_pk* pk, const bfz_record* rec, int rank, int world,
+                                bfz_timings* timings);
 
 /* Column-sharded PCS commit + FRI commit phase of a synthetic trace (BASELINE.json configs 4
  * and 5).  Replaces, for one n x (world * w_local) trace, TwoAdicFriPcs::commit

@@ -33,6 +33,9 @@ void or_api_merkle_root(const uint32_t* const* mats, const size_t* heights, cons
 uint32_t or_api_two_adic_gen(int bits);
 void or_api_ef_mul(const uint32_t a[4], const uint32_t b[4], uint32_t out[4]);
 void or_api_ef_inv(const uint32_t a[4], uint32_t out[4]);
+int or_api_perm_trace(int chip, const uint32_t* main, const uint32_t* prep, size_t n,
+                      const uint32_t alpha[4], const uint32_t beta[4], uint32_t* out,
+                      uint32_t cumsum[4]);
 /* sample a challenger transcript: observe `n` values then squeeze `m` samples */
 void or_api_challenger(const uint32_t* obs, size_t n, uint32_t* samples, size_t m);
 

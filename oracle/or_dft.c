@@ -11,6 +11,9 @@
  */
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include "or_field.h"
 #include "or_dft.h"
 
@@ -58,19 +61,26 @@ void or_intt(fp* a, int lg) {
   for (size_t i = 0; i < n; i++) a[i] = fp_mul(a[i], ninv);
 }
 
-/* Columns are transformed one at a time (textbook NTT per column), in groups of OR_LDE_GROUP
- * adjacent columns so the row-major gather and scatter touch whole cache lines. */
-#define OR_LDE_GROUP 16
+/* Columns are transformed one at a time (textbook NTT per column), in groups of up to 16
+ * adjacent columns so the row-major gather and scatter touch whole cache lines; groups are
+ * small enough that every thread gets one (a 31-column trace is 16 groups, not 2). */
 void or_coset_lde(const fp* in, size_t n, size_t w, fp shift, int log_blowup, fp* out) {
   int lg = or_log2(n);
   int lgN = lg + log_blowup;
   size_t N = n << log_blowup;
   fp gN = fp_two_adic_gen(lgN);
-  long ngroups = (long)((w + OR_LDE_GROUP - 1) / OR_LDE_GROUP);
+  int nthreads = 1;
+#ifdef _OPENMP
+  nthreads = omp_get_max_threads();
+#endif
+  size_t G = w / (size_t)nthreads;
+  if (G < 1) G = 1;
+  if (G > 16) G = 16;
+  long ngroups = (long)((w + G - 1) / G);
 #pragma omp parallel for schedule(dynamic, 1)
   for (long g = 0; g < ngroups; g++) {
-    size_t c0 = (size_t)g * OR_LDE_GROUP;
-    size_t gw = w - c0 < OR_LDE_GROUP ? w - c0 : OR_LDE_GROUP;
+    size_t c0 = (size_t)g * G;
+    size_t gw = w - c0 < G ? w - c0 : G;
     fp* a = calloc(N * gw, sizeof(fp)); /* column k of the group at a + k N */
     for (size_t i = 0; i < n; i++)
       for (size_t k = 0; k < gw; k++) a[k * N + i] = in[i * w + c0 + k];

@@ -511,6 +511,28 @@ int or_prove_record(const or_program* prog, or_record* rec, uint8_t** out, size_
   return 0;
 }
 
+/* generate_permutation_trace of one chip on given traces (canonical, row-major): the EF
+ * permutation trace flattened to base (n x 4 pw, flatten_to_base, prover.rs:318-334) and the
+ * cumulative sum.  Returns pw (EF columns). */
+int or_api_perm_trace(int chip, const uint32_t* main, const uint32_t* prep, size_t n,
+                      const uint32_t alpha[4], const uint32_t beta[4], uint32_t* out,
+                      uint32_t cumsum[4]) {
+  chipdata cd;
+  memset(&cd, 0, sizeof cd);
+  cd.chip = chip;
+  cd.n = n;
+  cd.log_n = or_log2(n);
+  cd.main = (fp*)main;
+  ef a, b;
+  memcpy(a.c, alpha, 16);
+  memcpy(b.c, beta, 16);
+  perm_trace(&cd, prep, prep ? (size_t)OR_CHIPS[chip].prep_w : 0, a, b);
+  memcpy(out, cd.perm, sizeof(ef) * n * cd.pw);
+  memcpy(cumsum, cd.cumsum.c, 16);
+  free(cd.perm);
+  return cd.pw;
+}
+
 /* Preprocessed commitment (vk.commit) for a program, canonical form. */
 void or_setup_root(const or_program* p, uint32_t root[8]) {
   pk_t pk;

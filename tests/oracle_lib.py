@@ -42,6 +42,7 @@ def lib():
         L.or_api_two_adic_gen.restype = ctypes.c_uint32
         L.or_api_challenger.argtypes = [P32, ctypes.c_size_t, P32, ctypes.c_size_t]
         L.or_api_setup_root.argtypes = [ctypes.c_char_p, P32]
+        L.or_api_perm_trace.argtypes = [ctypes.c_int, P32, P32, ctypes.c_size_t, P32, P32, P32, P32]
         L.or_set_num_queries.argtypes = [ctypes.c_int]
         L.or_set_pcs_variant.argtypes = [ctypes.c_int]
         _L = L
@@ -153,3 +154,22 @@ def to_mont(x: int) -> int:
 
 def from_mont(x: int) -> int:
     return (x * pow(2, -32, P)) % P
+
+
+def perm_trace(chip: int, main, prep, alpha, beta):
+    """generate_permutation_trace (permutation.rs:75-148) of one chip: (n x 4 pw flattened
+    permutation trace, cumulative sum), canonical values."""
+    import numpy as np
+    P32 = ctypes.POINTER(ctypes.c_uint32)
+    m = np.ascontiguousarray(main, dtype=np.uint32)
+    n = m.shape[0]
+    pr = None if prep is None else np.ascontiguousarray(prep, dtype=np.uint32)
+    out = np.zeros((n, 4 * 9), dtype=np.uint32)  # widest chip: Cpu, 9 EF columns
+    cs = (ctypes.c_uint32 * 4)()
+    a = (ctypes.c_uint32 * 4)(*alpha)
+    b = (ctypes.c_uint32 * 4)(*beta)
+    pw = lib().or_api_perm_trace(chip, m.ctypes.data_as(P32),
+                                 pr.ctypes.data_as(P32) if pr is not None else None, n, a, b,
+                                 out.ctypes.data_as(P32), cs)
+    flat = out.reshape(-1)[: n * 4 * pw].reshape(n, 4 * pw)
+    return flat, list(cs)

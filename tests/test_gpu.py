@@ -502,3 +502,36 @@ def test_record_from_events_sub_events_and_bad_events(client):
     with pytest.raises(_lib.BfzError, match="no cpu events"):
         _record_proof(pk, empty)
     assert _record_proof(pk, rec) == O.prove(prog, stdin)
+
+
+@pytest.mark.parametrize("prog,stdin", [(guests.FIBO, [17]), (guests.HELLO, []), ("+", [])])
+def test_logup_perm_trace_matches_oracle(prog, stdin):
+    """a7 standalone: generate_permutation_trace (permutation.rs:75-148) on the
+    device == the oracle's, every included chip: the flattened EF trace (batched fractions and
+    running sum, flatten_to_base) and the cumulative sum, for seeded random LogUp challenges;
+    plus uniformly random main traces (every row a different denominator)."""
+    rng = np.random.default_rng(33)
+    for trial in range(2):
+        alpha = [int(x) for x in rng.integers(0, P, 4)]
+        beta = [int(x) for x in rng.integers(0, P, 4)]
+        for chip in range(8):
+            main = O.trace(prog, stdin, chip)
+            if main is None:
+                continue
+            if trial:
+                main = rng.integers(0, P, size=main.shape, dtype=np.uint64).astype(np.uint32)
+            prep = O.trace(prog, stdin, chip, prep=True) if chip in (1, 5) else None
+            exp, exp_cs = O.perm_trace(chip, main, prep, alpha, beta)
+            out = ctypes.POINTER(ctypes.c_uint32)()
+            w = ctypes.c_size_t()
+            cs = (ctypes.c_uint32 * 4)()
+            m_dev = mont(main).copy()
+            p_dev = mont(prep).copy() if prep is not None else None
+            _lib.check(_lib.lib().bfz_perm_trace(
+                chip, m_dev.ctypes.data_as(P32), p_dev.ctypes.data_as(P32) if p_dev is not None else None,
+                main.shape[0], (ctypes.c_uint32 * 4)(*mont(alpha)), (ctypes.c_uint32 * 4)(*mont(beta)),
+                ctypes.byref(out), ctypes.byref(w), cs))
+            got = np.ctypeslib.as_array(out, shape=(main.shape[0] * w.value,)).copy()
+            _lib.lib().bfz_free(out)
+            assert np.array_equal(unmont(got).reshape(exp.shape), exp), (prog, chip, trial)
+            assert unmont(list(cs)).tolist() == exp_cs, (prog, chip, trial)

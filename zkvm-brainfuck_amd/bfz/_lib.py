@@ -72,6 +72,9 @@ SIGNATURES = [
                           POINTER(POINTER(c_uint32)), POINTER(c_size_t), POINTER(c_size_t)]),
     ("bfz_execute_events", c_int, [c_char_p, POINTER(c_uint8), c_size_t, c_int,
                                    POINTER(POINTER(c_uint8)), POINTER(c_size_t)]),
+    ("bfz_perm_trace", c_int, [c_int, POINTER(c_uint32), POINTER(c_uint32), c_size_t,
+                               POINTER(c_uint32), POINTER(c_uint32), POINTER(POINTER(c_uint32)),
+                               POINTER(c_size_t), POINTER(c_uint32)]),
     ("bfz_trace_device", c_int, [c_char_p, POINTER(c_uint8), c_size_t, c_int,
                                  POINTER(POINTER(c_uint32)), POINTER(c_size_t), POINTER(c_size_t)]),
     ("bfz_setup", c_int, [c_char_p, POINTER(c_void_p), POINTER(c_uint32)]),
@@ -105,6 +108,7 @@ SIGNATURES = [
     ("bfz_record_prove_sharded", c_int, [c_void_p, c_void_p, c_int, c_int, ALLGATHER_FN,
                                          ALLREDUCE_FN, c_void_p, POINTER(POINTER(c_uint8)),
                                          POINTER(c_size_t), POINTER(Timings)]),
+    ("bfz_record_prove_shard_solo", c_int, [c_void_p, c_void_p, c_int, c_int, POINTER(Timings)]),
     ("bfz_commit_fri_sharded", c_int, [c_void_p, c_int, c_size_t, c_int, c_int, c_void_p, c_void_p,
                                        ALLTOALL_FN, ALLGATHER_FN, c_void_p, POINTER(c_uint32),
                                        c_size_t, POINTER(c_size_t)]),

@@ -12,6 +12,7 @@
 
 #include "../../include/bfz.h"
 #include "fri.h"
+#include "logup.h"
 #include "merkle.h"
 #include "ntt.h"
 #include "pcs_sharded.h"
@@ -250,6 +251,53 @@ int bfz_trace_device(const char* elf, const uint8_t* in, size_t nin, int chip, u
       for (int c = 0; c < w; c++) o[r * w + c] = cm[(size_t)c * h + bfz::bitrev32((uint32_t)r, logh)];
     *out = o;
     *height = h;
+    *width = w;
+    return 0;
+  });
+}
+
+int bfz_perm_trace(int chip, const uint32_t* main, const uint32_t* prep, size_t n,
+                   const uint32_t alpha[4], const uint32_t beta[4], uint32_t** out, size_t* width,
+                   uint32_t cumsum[4]) {
+  return guarded([&] {
+    if (chip < 0 || chip >= bfz::NUM_CHIPS) throw std::runtime_error("bad chip index");
+    if (!main || !alpha || !beta || !out || !width || !cumsum) throw std::runtime_error("null argument");
+    if (n == 0 || (n & (n - 1)) || n > ((size_t)1 << 23)) throw std::runtime_error("height must be a power of two");
+    const int mw = bfz::CHIP_INFO[chip].main_w, pwid = bfz::CHIP_INFO[chip].prep_w;
+    if (pwid && !prep) throw std::runtime_error("this chip has a preprocessed trace");
+    hipStream_t st = bfz::stream();
+    auto colmajor = [&](const uint32_t* rm, int w) {
+      bfz::DBuf<uint32_t> r(n * w), c(n * w);
+      bfz::upload_bulk(r.p, rm, n * w * 4, st);
+      if (bfz::count_noncanonical(r.p, n * w, st)) throw std::runtime_error("non-canonical field word");
+      bfz::transpose_bitrev(r.p, n, w, c.p, st);
+      return c;
+    };
+    bfz::DBuf<uint32_t> mc = colmajor(main, mw);
+    bfz::DBuf<uint32_t> pc;
+    if (pwid) pc = colmajor(prep, pwid);
+    bfz::PermChallenges ch;
+    std::memcpy(ch.alpha.c, alpha, 16);
+    kb::EF beta_e;
+    std::memcpy(beta_e.c, beta, 16);
+    for (int k = 0; k < 4; k++)
+      if (ch.alpha.c[k] >= kb::P || beta_e.c[k] >= kb::P) throw std::runtime_error("non-canonical challenge");
+    ch.beta_pows[0] = kb::ef_one();
+    for (int j = 1; j < 8; j++) ch.beta_pows[j] = kb::ef_mul(ch.beta_pows[j - 1], beta_e);
+    const int w = 4 * bfz::perm_width(chip);
+    bfz::DBuf<uint32_t> pe(n * w);
+    bfz::DBuf<kb::EF> cs(1);
+    bfz::perm_trace(chip, mc.p, pwid ? pc.p : nullptr, n, ch, pe.p, cs.p, st);
+    std::vector<uint32_t> cm(n * w);
+    HIP_CHECK(hipMemcpyAsync(cm.data(), pe.p, cm.size() * 4, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(cumsum, cs.p, 16, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    uint32_t* o = (uint32_t*)std::malloc(cm.size() * 4 + 4);
+    if (!o) throw std::runtime_error("out of host memory");
+    const int logh = bfz::log2i(n);
+    for (size_t r = 0; r < n; r++)  // column-major bit-reversed -> row-major natural
+      for (int c = 0; c < w; c++) o[r * w + c] = cm[(size_t)c * n + bfz::bitrev32((uint32_t)r, logh)];
+    *out = o;
     *width = w;
     return 0;
   });
@@ -692,6 +740,28 @@ int bfz_record_prove_sharded(const bfz_pk* pk, const bfz_record* rec, int rank, 
     auto v = bfz::prove_events(*pk->pk, rec->ev, o, &st);
     fill_timings(st, t);
     return emit(std::move(v), proof, len);
+  });
+}
+
+int bfz_record_prove_shard_solo(const bfz_pk* pk, const bfz_record* rec, int rank, int world,
+                                bfz_timings* t) {
+  return guarded([&] {
+    if (!pk || !rec || !t) throw std::runtime_error("null argument");
+    if (world < 2 || rank < 0 || rank >= world || (world & (world - 1)))
+      throw std::runtime_error("shard solo: world must be a power of two >= 2, 0 <= rank < world");
+    bfz::ShardCtx c;
+    c.rank = rank;
+    c.world = world;
+    c.solo = true;
+    c.allgather = [](const void*, size_t, void*) {};  // receive buffers keep what they hold
+    c.allreduce_sum_u32 = [](uint32_t*, size_t) {};
+    ShardScope scope(&c);
+    bfz::ProveOptions o = opts();
+    o.timing = true;
+    bfz::StageTimes st;
+    (void)bfz::prove_events(*pk->pk, rec->ev, o, &st);  // not a proof: discarded
+    fill_timings(st, t);
+    return 0;
   });
 }
 

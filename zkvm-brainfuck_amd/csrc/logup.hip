@@ -62,14 +62,10 @@ __device__ __forceinline__ void batch_frac(const uint32_t (&pr)[PWD], const uint
   }
 }
 
-// Optional occupancy floor for A/B builds (the Cpu instance holds ~246 VGPRs: 2 waves/SIMD),
-// e.g. -DBFZ_PERM_KATTR='__attribute__((amdgpu_waves_per_eu(3)))'.
-#ifndef BFZ_PERM_KATTR
-#define BFZ_PERM_KATTR
-#endif
-
+// The Cpu instance holds ~246 VGPRs (2 waves/SIMD); forcing 3 waves spilled and was slower
+// (profiles/r02/ab_perm_occupancy.txt).
 template <int CHIP>
-__global__ __launch_bounds__(256) BFZ_PERM_KATTR void k_perm_rows(const uint32_t* __restrict__ mainc,
+__global__ __launch_bounds__(256) void k_perm_rows(const uint32_t* __restrict__ mainc,
                                                    const uint32_t* __restrict__ prepc, size_t n,
                                                    PermChallenges ch, uint32_t* __restrict__ perm,
                                                    EF* __restrict__ rowsum) {

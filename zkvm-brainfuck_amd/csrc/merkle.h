@@ -35,6 +35,9 @@ struct ShardCtx {
   std::function<void(const void* send, size_t bytes, void* recv)> allgather;
   // element-wise sum over ranks, in place
   std::function<void(uint32_t* data, size_t n)> allreduce_sum_u32;
+  // timing-only run of one rank's share (bfz_record_prove_shard_solo): the exchanges are
+  // no-ops, so the data after them is not the proof's and its consistency checks are skipped
+  bool solo = false;
 };
 constexpr size_t SHARD_MIN_LEAVES = 1024;
 ShardCtx*& shard_ctx();

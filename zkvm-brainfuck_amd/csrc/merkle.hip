@@ -5,7 +5,6 @@
 // One thread per row/node; leaf rows are read column by column so every load of a wave is
 // a contiguous 256-byte segment.
 #include <algorithm>
-#include <atomic>
 
 #include "merkle.h"
 #include "poseidon2.h"
@@ -144,45 +143,30 @@ __device__ __forceinline__ uint32_t merkle_node_lane(uint32_t v, const ColList& 
 // Subtree layers in lane mode (16 lanes per node: the permutation latency, not throughput,
 // is the cost here).  Block b owns TOP_NODES consecutive nodes of the first layer and
 // computes their subtree up to its root: up to TOP_LAYERS layers, every layer but the first
-// read from LDS, every digest written to HBM (query paths need every layer).  With
-// BFZ_TOP_ONE_LAUNCH=1 the tree's remaining layers ride on the same launch: each
-// block takes a ticket once its subtree is in HBM and the last block to finish (no block
-// waits on another) reads the n1-th layer back and builds the rest up to the root, so a tree
-// top of up to LANE_LAYER_MAX nodes is one launch instead of three.  Off by default: in a
-// same-box A/B it was no faster (FRI stage 2.69 ms without, 2.74 ms with one fence pair per
-// block, 3.5 ms with a fence in every thread) -- the release/acquire fences (L2 write-back
-// and invalidate across XCDs) cost what the launch boundaries did.
-#ifndef BFZ_TOP_ONE_LAUNCH
-#define BFZ_TOP_ONE_LAUNCH 0
-#endif
+// read from LDS, every digest written to HBM (query paths need every layer).  (A variant that
+// let the last block to finish build the rest of the tree in the same launch was no faster:
+// the cross-XCD release/acquire cost what the launch boundary did, profiles/r02/ab_merkle_top.txt.)
 constexpr int TOP_NODES = 64;   // fills a 1024-thread block in one lane-mode pass
 constexpr int TOP_LAYERS = 7;   // 64 nodes -> 1
 // Medium layers (TOP_NODES < nodes <= LANE_LAYER_MAX) go to lane mode: a single-lane launch
 // of this size is one permutation latency long (~12 us) while 16 lanes per node finish sooner.
-#ifndef BFZ_LANE_LOG
-#define BFZ_LANE_LOG 14
-#endif
-constexpr size_t LANE_LAYER_MAX = (size_t)1 << BFZ_LANE_LOG;
-constexpr int TOP_LAST = (int)(LANE_LAYER_MAX >> TOP_LAYERS);  // most first-layer nodes the last block builds
-constexpr int MAXTOP = BFZ_LANE_LOG + 1;                       // 2^BFZ_LANE_LOG nodes -> 1
+constexpr size_t LANE_LAYER_MAX = (size_t)1 << 14;
+constexpr int MAXTOP = TOP_LAYERS;
 struct TopLayers {
   uint32_t* out[MAXTOP];
   int c0[MAXTOP], c1[MAXTOP];
-  int n;                        // layers in this launch
-  int n1;                       // of which every block builds the first n1 (its subtree)
-  unsigned* ticket;             // zero between launches; null when n1 == n
+  int n;  // layers in this launch
 };
 
 __global__ __launch_bounds__(1024) void k_compress_top(const uint32_t* __restrict__ prev,
                                                        size_t nlen, ColList inj, TopLayers tl,
                                                        RootChallenge rc) {
-  __shared__ uint32_t buf[2][(BFZ_TOP_ONE_LAUNCH ? TOP_LAST : TOP_NODES) * 8];
-  __shared__ int last;
+  __shared__ uint32_t buf[2][TOP_NODES * 8];
   const size_t per = nlen < (size_t)TOP_NODES ? nlen : (size_t)TOP_NODES;
   const size_t g0 = (size_t)blockIdx.x * per;  // first-layer node of this block
   const int lane = threadIdx.x & 15;
   const LaneConsts kc = lane_consts(lane);
-  for (int l = 0; l < tl.n1; l++) {
+  for (int l = 0; l < tl.n; l++) {
     const size_t m = per >> l, g = g0 >> l;
     const uint32_t* src = l == 0 ? prev + 16 * g : buf[(l - 1) & 1];
     uint32_t* dst = buf[l & 1];
@@ -196,31 +180,6 @@ __global__ __launch_bounds__(1024) void k_compress_top(const uint32_t* __restric
     }
     __syncthreads();
   }
-  if (BFZ_TOP_ONE_LAUNCH && tl.n > tl.n1) {
-    // release this block's digests device-wide, then take a ticket; the last block acquires
-    // every other block's layer n1-1 and finishes the tree
-    if (threadIdx.x == 0) {  // one fence pair per block, after the barrier
-      __threadfence();
-      last = atomicAdd(tl.ticket, 1u) == gridDim.x - 1;
-      if (last) __threadfence();
-    }
-    __syncthreads();
-    if (!last) return;
-    for (int l = tl.n1; l < tl.n; l++) {
-      const size_t m = nlen >> l;
-      const uint32_t* src = l == tl.n1 ? tl.out[l - 1] : buf[(l - 1) & 1];
-      uint32_t* dst = buf[l & 1];
-      for (size_t j = threadIdx.x >> 4; j < m; j += blockDim.x >> 4) {
-        const uint32_t v = merkle_node_lane(src[16 * j + lane], inj, tl.c0[l], tl.c1[l], j, lane, kc);
-        if (lane < 8) {
-          tl.out[l][8 * j + lane] = v;
-          dst[8 * j + lane] = v;
-        }
-      }
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) *tl.ticket = 0u;  // every block has taken its ticket
-  }
   // FRI transcript step on the finished root (the root's block only): observe the root,
   // duplex, beta = the last 4 outputs popped in reverse (as k_fri_challenge)
   if (rc.state && threadIdx.x < 64) {
@@ -232,21 +191,6 @@ __global__ __launch_bounds__(1024) void k_compress_top(const uint32_t* __restric
       if (lane >= 4 && lane < 8) rc.beta->c[7 - lane] = v;
     }
   }
-}
-
-// Ticket counters for k_compress_top, zeroed once; launches rotate through them so trees
-// built on different streams never share one.
-static unsigned* top_ticket() {
-  constexpr int NT = 256;
-  static unsigned* t = [] {
-    unsigned* p = nullptr;
-    HIP_CHECK(hipMalloc(&p, NT * sizeof(unsigned)));
-    HIP_CHECK(hipMemset(p, 0, NT * sizeof(unsigned)));
-    HIP_CHECK(hipDeviceSynchronize());
-    return p;
-  }();
-  static std::atomic<unsigned> next{0};
-  return t + (next.fetch_add(1, std::memory_order_relaxed) % NT);
 }
 
 // Medium layers in lane mode (see LANE_LAYER_MAX).
@@ -358,17 +302,11 @@ static void build_layers(MerkleTree& t, int L0, size_t len, const std::vector<co
     launch_layer(t, L, 0, nlen, grp, st);
     len = nlen;
   }
-  while (L <= nl) {  // subtree launches: one per tree top with BFZ_TOP_ONE_LAUNCH
+  while (L <= nl) {  // subtree launches
     const size_t first = len >> 1;
     const int sub = first > (size_t)TOP_NODES ? TOP_LAYERS : log2i(first) + 1;
-    const bool rest = BFZ_TOP_ONE_LAUNCH && first > (size_t)TOP_NODES;
-    const int maxl = rest ? log2i(first) + 1 : sub;
-    if (maxl > MAXTOP || (rest && (first >> TOP_LAYERS) > (size_t)TOP_LAST))
-      throw std::runtime_error("merkle: tree top larger than k_compress_top handles");
     TopLayers tl{};
-    tl.n = std::min(maxl, nl - L + 1);
-    tl.n1 = std::min(sub, tl.n);
-    tl.ticket = tl.n > tl.n1 ? top_ticket() : nullptr;
+    tl.n = std::min(sub, nl - L + 1);
     std::vector<const MatRef*> all;
     size_t nlen = first;
     for (int l = 0; l < tl.n; l++, nlen >>= 1) {

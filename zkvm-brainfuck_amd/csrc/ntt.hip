@@ -98,22 +98,14 @@ constexpr SmallRoots make_small_roots() {
 }
 constexpr SmallRoots SMALL = make_small_roots();
 
-#ifndef BFZ_TILE_LOG
-#define BFZ_TILE_LOG 14
-#endif
-constexpr int R16_TILE_LOG = BFZ_TILE_LOG;  // 2^14 elements per tile: 1024 threads x 16
-// Second-pass tiles take 2^c adjacent columns (2^c * 4 B coalesced runs); c <= MID_CMAX.
-#ifndef BFZ_TILE_DIRECT
-#define BFZ_TILE_DIRECT 1
-#endif
-#ifndef BFZ_MID_CMAX
-#define BFZ_MID_CMAX 5
-#endif
-constexpr int MID_CMAX = BFZ_MID_CMAX;
-#ifndef BFZ_MID_TW_LOAD
-#define BFZ_MID_TW_LOAD 1
-#endif
-constexpr bool MID_TW_LOAD = BFZ_MID_TW_LOAD;
+// 2^14 elements per tile: 1024 threads x 16 (2^13 tiles measured +7%)
+constexpr int R16_TILE_LOG = 14;
+// Second-pass tiles take 2^c adjacent columns (2^c * 4 B coalesced runs); c <= MID_CMAX
+// (16- or 64-column runs measured +8% / +2%).
+constexpr int MID_CMAX = 5;
+// k_lde_mid reads every twiddle of a stage from the table instead of multiplying one loaded
+// base by the small roots (a load replaces a Montgomery product).
+constexpr bool MID_TW_LOAD = true;
 
 __device__ __forceinline__ int lds_pad(int idx, int c) { return c < 5 ? idx + (idx >> 4) : idx; }
 
@@ -127,7 +119,7 @@ __device__ __forceinline__ int lds_pad(int idx, int c) { return c < 5 ? idx + (i
 // TW_LOAD: read every twiddle of the stage from the table (tile kernels: s0 = lo_g = 0, the
 // table slice below 2^14 is L2-resident) instead of multiplying one loaded base by the small
 // roots -- a load replaces a Montgomery product.
-// R = 5 (tile kernels, BFZ_TILE_R): 32 elements per thread, windows of 5 stages.
+// R is the window size in stages (2^R elements per thread); every launch uses R = 4.
 template <bool DIF, bool CONST_TW, bool TW_LOAD = false, int R = 4>
 __device__ __forceinline__ void r16_window(uint32_t (&x)[1 << R], int g0, int kk_lo, int kk_hi, int s0,
                                            uint32_t m_low, uint32_t lo_g, const uint32_t* __restrict__ tw) {
@@ -260,21 +252,8 @@ __device__ __forceinline__ constexpr int tile_off(int i) { return (i << G0) + ((
 // DIN (DIT only): the first window (g0 = 0) holds the 16 consecutive words tid*16 + i, read
 // straight from HBM as four 16-byte loads (no LDS staging, one barrier fewer); the launch picks
 // it when the source rows are 16-byte aligned.
-#ifndef BFZ_TILE_DIRECT_IN
-#define BFZ_TILE_DIRECT_IN 1
-#endif
-// R (BFZ_TILE_R): 2^R elements per thread and R stages per register window; R = 5 takes a
-// 2^14 tile in three windows (5 + 5 + 4 stages) and two LDS exchanges instead of four windows
-// (4 + 4 + 4 + 2) and three exchanges, at 512 threads and 32 elements per thread.
-#ifndef BFZ_TILE_R
-#define BFZ_TILE_R 4
-#endif
-#ifndef BFZ_TILE_R_DIT
-#define BFZ_TILE_R_DIT BFZ_TILE_R
-#endif
-#ifndef BFZ_TILE_R_DIF
-#define BFZ_TILE_R_DIF BFZ_TILE_R
-#endif
+// R: 2^R elements per thread and R stages per register window (R = 5, three windows of a 2^14
+// tile at 512 threads, measured DIT neutral / DIF +2%: R = 4 everywhere).
 template <bool DIF, int B, bool DIN = false, int R = 4>
 __global__ __launch_bounds__(1 << (B - R)) void k_ntt_tile(const uint32_t* __restrict__ src,
                                                            uint32_t* __restrict__ dst,
@@ -299,7 +278,7 @@ __global__ __launch_bounds__(1 << (B - R)) void k_ntt_tile(const uint32_t* __res
 #ifndef BFZ_NTT_REPS
 #define BFZ_NTT_REPS 1
 #endif
-  constexpr bool DIRECT = BFZ_TILE_DIRECT && BFZ_NTT_REPS == 1;
+  constexpr bool DIRECT = BFZ_NTT_REPS == 1;
   static_assert(!DIN || (!DIF && BFZ_NTT_REPS == 1), "direct first window: DIT passes only");
   uint32_t x[E];
   if constexpr (DIN) {
@@ -563,11 +542,11 @@ static void r16_attrs() {
                         (const void*)&k_lde_mid<23>};
   for (const void* f : mids)
     HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<true, R16_TILE_LOG, false, BFZ_TILE_R_DIF>),
+  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<true, R16_TILE_LOG, false>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<false, R16_TILE_LOG, false, BFZ_TILE_R_DIT>),
+  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<false, R16_TILE_LOG, false>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<false, R16_TILE_LOG, true, BFZ_TILE_R_DIT>),
+  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<false, R16_TILE_LOG, true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   done = true;
 }
@@ -575,11 +554,10 @@ static void r16_attrs() {
 template <bool DIF, int B>
 static void tile_launch(dim3 grid, const uint32_t* in, size_t is, uint32_t* dst, size_t ds,
                         const uint32_t* tw, hipStream_t st) {
-  // the full-size tile takes BFZ_TILE_R; smaller tiles (short columns) stay radix-16
-  constexpr int R = B == R16_TILE_LOG ? (DIF ? BFZ_TILE_R_DIF : BFZ_TILE_R_DIT) : 4;
+  constexpr int R = 4;
   const size_t lds = ((size_t)1 << B) + ((size_t)1 << (B - R));
   const dim3 block(1 << (B - R));
-  if constexpr (!DIF && BFZ_TILE_DIRECT_IN && BFZ_NTT_REPS == 1) {
+  if constexpr (!DIF && BFZ_NTT_REPS == 1) {
     if (((uintptr_t)in & 15) == 0 && (is & 3) == 0) {
       hipLaunchKernelGGL((k_ntt_tile<false, B, true, R>), grid, block, lds * 4, st, in, dst, is,
                          ds, tw);

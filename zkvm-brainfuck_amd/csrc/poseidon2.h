@@ -106,15 +106,6 @@ KB_HD void mds_light64(uint64_t s[16]) {
 //    |t_i| < 7p/8; the result is sum + d_i x_i in Montgomery form.  The next round's constant
 //    rides on t_0's reduction (the terminal external round's on every element after the last
 //    internal round).
-#ifndef BFZ_P2_PRE_RC
-#define BFZ_P2_PRE_RC 1
-#endif
-#ifndef BFZ_P2_LAZY_DIAG
-#define BFZ_P2_LAZY_DIAG 1
-#endif
-#ifndef BFZ_P2_SUM_CHAINS
-#define BFZ_P2_SUM_CHAINS 2
-#endif
 constexpr int32_t centred(uint32_t x) { return x > P / 2 ? (int32_t)(x - P) : (int32_t)x; }
 struct P2Signed {
   int32_t rc_init[4][16];  // centred rc R^2 (R^2-form constants)
@@ -137,7 +128,7 @@ constexpr P2Signed make_p2_signed() {
 }
 constexpr P2Signed P2S = make_p2_signed();
 
-// Round constants moved in front of the MDS-light (BFZ_P2_PRE_RC): the MDS layer M is linear
+// Round constants moved in front of the MDS-light: the MDS layer M is linear
 // and invertible, so M y + rc = M (y + K) with K = M^-1 rc (mod p).  K rides on the 64-bit
 // addend of the S-box's last product (x^3 = m a + K, one v_mad_i64_i32 either way; |K| < p/2)
 // or of the initial s * C32, and the separate 64-bit "+ rc" before each reduction is gone.
@@ -284,22 +275,10 @@ KB_HD int64_t cube_s(int32_t a) {
 KB_HD int64_t fold_s(int64_t u) {
   return (int64_t)(int32_t)(u >> 32) * (int64_t)C32 + (int64_t)(uint32_t)u;
 }
-// a[i]: first-round S-box inputs (constant included); rc: constants of rounds 1..3.
-// Leaves the 4th MDS output (64-bit R^2-form) in y.
-KB_HD void external_rounds_s(const int32_t a[16], int64_t y[16], const int32_t (&rc)[4][16]) {
-  uint64_t* u = reinterpret_cast<uint64_t*>(y);
-#pragma unroll
-  for (int i = 0; i < 16; i++) y[i] = fold_s(cube_s(a[i]));
-  mds_light64(u);
-#pragma unroll
-  for (int r = 1; r < 4; r++) {
-#pragma unroll
-    for (int i = 0; i < 16; i++) y[i] = fold_s(cube_s(mred_s(y[i] + rc[r][i])));
-    mds_light64(u);
-  }
-}
-// The same with the constants already in front of the MDS layers (P2Pre): round r's S-box
-// output gets K[r] (the M^-1 image of the constant the reduction after its MDS would add).
+// External rounds with the constants already in front of the MDS layers (P2Pre): a[i] are the
+// first round's S-box inputs (constant included); round r's S-box output gets K[r] (the M^-1
+// image of the constant the reduction after its MDS would add).  Leaves the 4th MDS output
+// (64-bit R^2-form) in y.
 KB_HD void external_rounds_pre(const int32_t a[16], int64_t y[16], const int32_t (&K)[4][16]) {
   uint64_t* u = reinterpret_cast<uint64_t*>(y);
 #pragma unroll
@@ -316,7 +295,6 @@ KB_HD void external_rounds_pre(const int32_t a[16], int64_t y[16], const int32_t
 KB_HD void poseidon2_permute(uint32_t s[16]) {
   int64_t y[16];
   int32_t t[16];
-#if BFZ_P2_PRE_RC
   // initial MDS-light on x R^2 + M^-1 rc_0 (s C32 < 2^56, rows sum to 35: < 2^61.2)
 #pragma unroll
   for (int i = 0; i < 16; i++) y[i] = (int64_t)((uint64_t)s[i] * C32) + P2PRE.init0[i];
@@ -326,18 +304,6 @@ KB_HD void poseidon2_permute(uint32_t s[16]) {
   external_rounds_pre(t, y, P2PRE.init);
 #pragma unroll
   for (int i = 0; i < 16; i++) t[i] = mred_s(y[i]);  // rc_int[0] already in y[0]
-#else
-  // initial MDS-light on x R^2 (s C32 < 2^56, rows sum to 35: < 2^61.2)
-#pragma unroll
-  for (int i = 0; i < 16; i++) y[i] = (int64_t)((uint64_t)s[i] * C32);
-  mds_light64(reinterpret_cast<uint64_t*>(y));
-#pragma unroll
-  for (int i = 0; i < 16; i++) t[i] = mred_s(y[i] + P2S.rc_init[0][i]);
-  external_rounds_s(t, y, P2S.rc_init);
-#pragma unroll
-  for (int i = 0; i < 16; i++) t[i] = mred_s(i == 0 ? y[i] + P2S.rc_int[0] : y[i]);
-#endif
-#if BFZ_P2_LAZY_DIAG
   // Elements 1, 2, 4, 5 (d = 1, 2, 3, 4) stay unreduced 64-bit R-form values through rounds
   // 0..11: u <- d u + T_R with T_R = reduce(q) the R-form round sum (|T_R| < p/2 + 2^28), a
   // 64-bit shift-add instead of multiply + reduction.  Growth: |u_5| < 4^12 2^30.2 + 4^12 p/6
@@ -382,49 +348,7 @@ KB_HD void poseidon2_permute(uint32_t s[16]) {
       t[5] = mred_s((int64_t)P2M.dd[5] * mred_s(u5) + (q + P2S.rc_term[0][5]));
     }
   }
-#else
-#pragma unroll
-  for (int r = 0; r < 13; r++) {
-    const int32_t c = mred_s(cube_s(t[0]));
-#if BFZ_P2_SUM_CHAINS == 2
-    // two multiply-add chains of 8 that start from a product, not from a sign-extended
-    // element (ashr + mov + 64-bit add per chain otherwise)
-    int64_t part[2];
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-      part[k] = (int64_t)P2M.one[8 * k] * (k ? t[8] : c);
-#pragma unroll
-      for (int i = 8 * k + 1; i < 8 * k + 8; i++) part[k] = (int64_t)P2M.one[i] * t[i] + part[k];
-    }
-    const int32_t sp = mred_s(part[0] + part[1]);
-#else
-    int64_t part[4];  // four independent multiply-add chains
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      part[k] = k ? (int64_t)t[4 * k] : (int64_t)c;
-#pragma unroll
-      for (int i = 4 * k + 1; i < 4 * k + 4; i++) part[k] = (int64_t)P2M.one[i] * t[i] + part[k];
-    }
-    const int32_t sp = mred_s((part[0] + part[1]) + (part[2] + part[3]));
-#endif
-    if (r < 12) {
-      const int64_t q = opaque64((int64_t)P2M.k * sp);  // one product, not one per element
-      t[0] = mred_s((int64_t)P2M.d[0] * c + (q + P2S.rc_int[r + 1]));
-#pragma unroll
-      for (int i = 1; i < 16; i++) t[i] = mred_s((int64_t)P2M.d[i] * t[i] + q);
-    } else {
-      const int64_t q = opaque64((int64_t)P2M.k * sp);  // one product, not one per element
-      t[0] = mred_s((int64_t)P2M.d[0] * c + (q + P2S.rc_term[0][0]));
-#pragma unroll
-      for (int i = 1; i < 16; i++) t[i] = mred_s((int64_t)P2M.d[i] * t[i] + (q + P2S.rc_term[0][i]));
-    }
-  }
-#endif
-#if BFZ_P2_PRE_RC
   external_rounds_pre(t, y, P2PRE.term);
-#else
-  external_rounds_s(t, y, P2S.rc_term);
-#endif
 #pragma unroll
   for (int i = 0; i < 16; i++) {
     const uint32_t r = (uint32_t)mred_s(y[i]);

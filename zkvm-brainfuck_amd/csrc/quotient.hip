@@ -85,11 +85,10 @@ __global__ __launch_bounds__(256) void k_sel_inv(int logN, uint32_t shift, uint3
   out[t] = minv(mmul(msub(x, ONE), msub(x, wn_inv)));
 }
 
-#ifndef BFZ_Q_MINB  // blocks per CU the register budget is sized for (A/B builds)
-#define BFZ_Q_MINB 3
-#endif
+// Register budget sized for 3 blocks per CU (4 spilled and was slower,
+// profiles/r02/ab_quotient_occupancy.txt).
 template <int CHIP>
-__global__ __launch_bounds__(256, BFZ_Q_MINB) void k_quotient(QuotRows in, int logN, QuotParams qp,
+__global__ __launch_bounds__(256, 3) void k_quotient(QuotRows in, int logN, QuotParams qp,
                                                   const uint32_t* __restrict__ twf,
                                                   const uint32_t* __restrict__ sel_inv,
                                                   QuotOut qo) {
