@@ -7,7 +7,7 @@ export BFZ_AB_VARIANT=1  # the builds come from other source revisions
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 cp zkvm-brainfuck_amd/libbfz.so /tmp/libbfz_orig.so
-for rep in 1 2; do
+for rep in $(seq 1 ${AB_REPS:-2}); do
   for so in "$@"; do
     v=$(basename $so .so)
     cp "$so" zkvm-brainfuck_amd/libbfz.so

@@ -75,6 +75,34 @@ void fri_fold_dev(const kb::EF* in, kb::EF* out, size_t h, const kb::EF* beta, c
 // Outputs [i0, i0 + count) of the same fold; in, out and add hold only that range.
 void fri_fold_range(const kb::EF* in, kb::EF* out, size_t h, size_t i0, size_t count,
                     const kb::EF* beta, const kb::EF* add, hipStream_t st);
+// The fold of layer `in` (4 h values) fused with the next round's leaf hashes: out[k] =
+// fold(in[2k], in[2k+1]) (+ add[k]) for k < 2 h, and leaf i = P(out[2i] || out[2i+1])[0..8] into
+// digests[8 i ..] (k_fri_fold_dev + k_hash_rows8 in one pass).  Thread mode only: the
+// prover uses it where the leaves are hashed one permutation per thread (h > FRI_FUSE_MIN / 2).
+// (A lane-mode form, 16 lanes per leaf with every fold computed by four lanes, took 14.7 us per
+// round against 4.7 + 4.8 us for the separate fold and lane-mode hash.)
+constexpr size_t FRI_FUSE_MIN = (size_t)1 << 15;  // merkle.hip: lane-mode leaves up to 2^14
+void fri_fold_leaves(const kb::EF* in, kb::EF* out, size_t h, const kb::EF* beta,
+                     const kb::EF* add, uint32_t* digests, hipStream_t st);
+// The last commit-phase rounds (at most FRI_TAIL_MAXH leaves) in one single-workgroup launch:
+// per round the leaf hashes, every tree layer, the transcript step (observe the root, duplex,
+// beta) and the fold, with the layer and the digests kept in LDS between the steps.  Every
+// digest and fold output is also written to its buffer (the query openings read them).
+// (same-box A/B, profiles/r03/ab_open_and_tops.txt: FRI stage 2.675 -> 2.624 ms with the fused
+// folds and a 128-leaf tail; 64 and 256 leaves were no better)
+constexpr int FRI_TAIL_MAXH = 128;
+constexpr int FRI_TAIL_MAXR = 10;
+struct FriTailRounds {
+  int nr = 0;                             // rounds: h = 2^logh0, 2^(logh0-1), ...
+  int logh0 = 0;
+  const kb::EF* in = nullptr;             // the first round's layer (2 h values)
+  kb::EF* layer[FRI_TAIL_MAXR] = {};      // round r's fold output (h_r values)
+  uint32_t* tree[FRI_TAIL_MAXR] = {};     // round r's tree: layers of 8 h_r, 4 h_r, ..., 8 words
+  const kb::EF* add[FRI_TAIL_MAXR] = {};  // reduced openings added to round r's fold, or null
+  uint32_t* state = nullptr;              // device challenger state (16 words), in/out
+  kb::EF* beta = nullptr;                 // the rounds' betas
+};
+void fri_tail_rounds(const FriTailRounds& a, hipStream_t st);
 // Query openings: word k of segment s for query index I is
 //   base[((I >> shift) ^ xr) * unit + k * stride],  k < count
 // (matrix rows: unit 1, stride = height; Merkle siblings: unit 8; FRI siblings: unit 4).

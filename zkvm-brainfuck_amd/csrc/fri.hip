@@ -99,7 +99,7 @@ __device__ __forceinline__ void open_tile(const uint32_t* __restrict__ mat, size
     const size_t t = c0 + (size_t)r * OPEN_T;
     if (TAB) {
 #pragma unroll
-      for (int k = 0; k < NP; k++) W[k][r] = r < nr ? (k ? invd_b : invd_a)[t] : ef_zero();
+      for (int k = 0; k < NP; k++) W[k][r] = r < nr ? ld_global(k ? invd_b : invd_a, t) : ef_zero();
       continue;
     }
     const uint32_t x = r < nr ? coset_point((uint32_t)t, logH, twf) : 0u;
@@ -110,21 +110,24 @@ __device__ __forceinline__ void open_tile(const uint32_t* __restrict__ mat, size
       // w_n^-1 into scale_b), so the zeta table serves both points
       const size_t tk = k && !invd_b ? prev2_pos(t, logH) : t;
       const EF* tab = k && invd_b ? invd_b : invd_a;
-      W[k][r] = r < nr ? ef_neg(ef_mul_base(tab[tk], x)) : ef_zero();
+      W[k][r] = r < nr ? ef_neg(ef_mul_base(ld_global(tab, tk), x)) : ef_zero();
     }
   }
   auto load = [&](int c, uint32_t (&v)[OPEN_R]) {
     const uint32_t* col = mat + (size_t)c * height + c0;
 #pragma unroll
-    for (int r = 0; r < OPEN_R; r++) v[r] = r < nr ? col[(size_t)r * OPEN_T] : 0u;
+    for (int r = 0; r < OPEN_R; r++) v[r] = r < nr ? ld_global(col, (size_t)r * OPEN_T) : 0u;
   };
   // four column buffers in a ring: three columns stay in flight while one is consumed
   uint32_t vr[4][OPEN_R];
 #pragma unroll
   for (int j = 0; j < 4; j++)
     if (j < w) load(j, vr[j]);
-  __shared__ uint32_t red[NP * 4 * 4 * OPEN_T];  // [(k * 4 + col) * 4 + coef][thread]
   constexpr int NSUM = NP * 16, PER = OPEN_T / NSUM;  // sums per group, threads per sum
+  // row stride OPEN_T + PER: the PER-strided reads of the 32 / PER sums a half-wave adds up
+  // land in distinct banks (stride OPEN_T put 32 / PER of them in each bank; kernel -1.6%)
+  constexpr int RS = OPEN_T + PER;
+  __shared__ uint32_t red[NSUM * RS];  // [(k * 4 + col) * 4 + coef][thread]
   for (int c = 0; c < w; c += 4) {
 #pragma unroll
     for (int j = 0; j < 4; j++) {
@@ -137,7 +140,7 @@ __device__ __forceinline__ void open_tile(const uint32_t* __restrict__ mat, size
           for (int r = 0; r < OPEN_R; r++) lz.add(W[k][r], vr[j][r]);
           const EF acc = lz.get();
 #pragma unroll
-          for (int e = 0; e < 4; e++) red[((k * 4 + j) * 4 + e) * OPEN_T + threadIdx.x] = acc.c[e];
+          for (int e = 0; e < 4; e++) red[((k * 4 + j) * 4 + e) * RS + threadIdx.x] = acc.c[e];
         }
         if (c + j + 4 < w) load(c + j + 4, vr[j]);
       }
@@ -145,7 +148,7 @@ __device__ __forceinline__ void open_tile(const uint32_t* __restrict__ mat, size
     __syncthreads();
     {  // sum q = (k * 4 + j) * 4 + e is added up by the PER threads q * PER .. q * PER + PER - 1
       const int q = threadIdx.x / PER, part = threadIdx.x % PER;
-      const uint32_t* src = red + q * OPEN_T;
+      const uint32_t* src = red + q * RS;
       uint64_t a64 = 0;
 #pragma unroll 8
       for (int i = part; i < OPEN_T; i += PER) a64 += src[i];  // < 32 p < 2^36
@@ -255,14 +258,14 @@ __global__ __launch_bounds__(256) void k_reduce(const RedCol* __restrict__ cols,
       for (; c + RED_STEP <= end; c += RED_STEP) {  // RED_STEP column loads in flight per step
         uint32_t v[RED_STEP];
 #pragma unroll
-        for (int k = 0; k < RED_STEP; k++) v[k] = cols[c + k].col[t];
+        for (int k = 0; k < RED_STEP; k++) v[k] = ld_global(cols[c + k].col, t);
 #pragma unroll
         for (int k = 0; k < RED_STEP; k++) acc.add(cols[c + k].ca, v[k]);
       }
       if (RED_STEP > 8 && c + 8 <= end) {
         uint32_t v[8];
 #pragma unroll
-        for (int k = 0; k < 8; k++) v[k] = cols[c + k].col[t];
+        for (int k = 0; k < 8; k++) v[k] = ld_global(cols[c + k].col, t);
 #pragma unroll
         for (int k = 0; k < 8; k++) acc.add(cols[c + k].ca, v[k]);
         c += 8;
@@ -270,12 +273,12 @@ __global__ __launch_bounds__(256) void k_reduce(const RedCol* __restrict__ cols,
       if (c + 4 <= end) {
         uint32_t v[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) v[k] = cols[c + k].col[t];
+        for (int k = 0; k < 4; k++) v[k] = ld_global(cols[c + k].col, t);
 #pragma unroll
         for (int k = 0; k < 4; k++) acc.add(cols[c + k].ca, v[k]);
         c += 4;
       }
-      for (; c < end; c++) acc.add(cols[c].ca, cols[c].col[t]);
+      for (; c < end; c++) acc.add(cols[c].ca, ld_global(cols[c].col, t));
       const EF s = acc.get();
       sa = ef_add(sa, s);
       if (rm.has_b) sb = ef_add(sb, ef_mul(s, rm.kb));
@@ -321,6 +324,44 @@ __global__ __launch_bounds__(256) void k_fri_fold_dev(const EF* __restrict__ in,
   out[i] = r;
 }
 
+// Fold output k of a layer folded to n = 2^logn values (k_fri_fold_dev's formula).
+__device__ __forceinline__ EF fold_one(const EF* __restrict__ in, size_t k, size_t n, int logn,
+                                       const EF& half_beta, uint32_t halfv,
+                                       const uint32_t* __restrict__ twi, const EF* __restrict__ add) {
+  const EF p = ef_mul_base(half_beta, ld_global(twi, n + dbitrev((uint32_t)k, logn)));
+  EF r = ef_add(ef_mul(ef_add_base(p, halfv), ld_global(in, 2 * k)),
+                ef_mul(ef_sub(ef_base(halfv), p), ld_global(in, 2 * k + 1)));
+  if (add) r = ef_add(r, ld_global(add, k));
+  return r;
+}
+
+// Thread mode: thread i folds outputs 2i, 2i+1 and hashes them as leaf i.
+__global__ __launch_bounds__(256) void k_fold_leaves(
+    const EF* __restrict__ in, EF* __restrict__ out, size_t h, int logn,
+    const EF* __restrict__ beta, const uint32_t* __restrict__ twi, const EF* __restrict__ add,
+    uint32_t* __restrict__ digests) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= h) return;
+  const uint32_t halfv = to_mont_c((P + 1) / 2);
+  const EF half_beta = ef_mul_base(*beta, halfv);
+  const EF a = fold_one(in, 2 * i, 2 * h, logn, half_beta, halfv, twi, add);
+  const EF b = fold_one(in, 2 * i + 1, 2 * h, logn, half_beta, halfv, twi, add);
+  out[2 * i] = a;
+  out[2 * i + 1] = b;
+  uint32_t st[16];
+#pragma unroll
+  for (int e = 0; e < 4; e++) {
+    st[e] = a.c[e];
+    st[4 + e] = b.c[e];
+    st[8 + e] = 0;
+    st[12 + e] = 0;
+  }
+  poseidon2_permute(st);
+  uint4* o = reinterpret_cast<uint4*>(digests + 8 * i);
+  o[0] = make_uint4(st[0], st[1], st[2], st[3]);
+  o[1] = make_uint4(st[4], st[5], st[6], st[7]);
+}
+
 // One 16-lane row: lane l holds state word l (lane-mode permutation).
 __global__ __launch_bounds__(64) void k_fri_challenge(uint32_t* __restrict__ state,
                                                       const uint32_t* __restrict__ root,
@@ -333,6 +374,79 @@ __global__ __launch_bounds__(64) void k_fri_challenge(uint32_t* __restrict__ sta
     state[lane] = v;
     if (lane >= 4 && lane < 8) beta->c[7 - lane] = v;
   }
+}
+
+// The commit-phase tail (FriTailRounds, fri.h): one 1024-thread block, 16 lanes per
+// permutation (lane-mode Poseidon2), 64 permutations per pass.
+__global__ __launch_bounds__(1024) void k_fri_tail(FriTailRounds a, const uint32_t* __restrict__ twi) {
+  __shared__ EF cur[2 * FRI_TAIL_MAXH];          // the round's input layer
+  __shared__ uint32_t dig[2][FRI_TAIL_MAXH * 8];  // digests of the layer being built / below it
+  __shared__ EF sbeta;
+  const int lane = threadIdx.x & 15, row = threadIdx.x >> 4;
+  constexpr int ROWS = 1024 / 16;
+  const LaneConsts kc = lane_consts(lane);
+  uint32_t stv = threadIdx.x < 16 ? ld_global(a.state, threadIdx.x) : 0u;  // lane l: state[l]
+  for (int i = threadIdx.x; i < (2 << a.logh0); i += blockDim.x) cur[i] = ld_global(a.in, i);
+  __syncthreads();
+  const uint32_t halfv = to_mont_c((P + 1) / 2);
+  for (int r = 0; r < a.nr; r++) {
+    const int logh = a.logh0 - r, h = 1 << logh;
+    uint32_t* out = a.tree[r];
+    // leaves: row i = cur[2i] || cur[2i+1] (8 words), one permutation.  Waves with no row below
+    // h skip the pass (a permutation costs its latency only while few waves share a SIMD); in
+    // the others whole 16-lane rows permute (DPP) and rows < h store.
+    for (int b = 0; b < h; b += ROWS) {
+      if (b + (row & ~3) >= h) break;
+      const int i = b + row;
+      const uint32_t x = i < h && lane < 8 ? cur[2 * i + (lane >> 2)].c[lane & 3] : 0u;
+      const uint32_t v = poseidon2_permute_lane(x, lane, kc);
+      if (i < h && lane < 8) {
+        out[8 * i + lane] = v;
+        dig[0][8 * i + lane] = v;
+      }
+    }
+    __syncthreads();
+    out += 8 * h;
+    int pp = 0;
+    for (int m = h >> 1; m >= 1; m >>= 1) {  // node j = P(child 2j || child 2j+1)[0..8]
+      for (int b = 0; b < m; b += ROWS) {
+        if (b + (row & ~3) >= m) break;
+        const int j = b + row;
+        const uint32_t v = poseidon2_permute_lane(j < m ? dig[pp][16 * j + lane] : 0u, lane, kc);
+        if (j < m && lane < 8) {
+          out[8 * j + lane] = v;
+          dig[pp ^ 1][8 * j + lane] = v;
+        }
+      }
+      __syncthreads();
+      pp ^= 1;
+      out += 8 * m;
+    }
+    if (threadIdx.x < 64) {  // observe the root (input buffer empty), duplex, pop 4 outputs
+      const uint32_t v = poseidon2_permute_lane(lane < 8 ? dig[pp][lane] : stv, lane, kc);
+      if (threadIdx.x < 16) {
+        stv = v;
+        if (lane >= 4 && lane < 8) {
+          sbeta.c[7 - lane] = v;
+          a.beta[r].c[7 - lane] = v;
+        }
+      }
+    }
+    __syncthreads();
+    EF f = ef_zero();  // fold (k_fri_fold_dev)
+    const int i = threadIdx.x;
+    if (i < h) {
+      const EF half_beta = ef_mul_base(sbeta, halfv);
+      const EF p = ef_mul_base(half_beta, ld_global(twi, (size_t)h + dbitrev((uint32_t)i, logh)));
+      f = ef_add(ef_mul(ef_add_base(p, halfv), cur[2 * i]), ef_mul(ef_sub(ef_base(halfv), p), cur[2 * i + 1]));
+      if (a.add[r]) f = ef_add(f, ld_global(a.add[r], i));
+      a.layer[r][i] = f;
+    }
+    __syncthreads();
+    if (i < h) cur[i] = f;
+    __syncthreads();
+  }
+  if (threadIdx.x < 16) a.state[threadIdx.x] = stv;
 }
 
 // ------------------------------------------------------------------ grind
@@ -373,7 +487,7 @@ __global__ __launch_bounds__(256) void k_gather_segs(const GatherSeg* __restrict
   uint32_t* o = out + (size_t)q * words_per_q + seg_off[s];
   // canonical form here, so the host copies the words straight into the proof
   for (uint32_t k = 0; k < g.count; k++)
-    o[k] = owner == rank ? from_mont(g.base[pos + k * g.stride]) : 0u;
+    o[k] = owner == rank ? from_mont(ld_global(g.base, pos + k * g.stride)) : 0u;
 }
 
 // ================================================================== host wrappers
@@ -476,6 +590,27 @@ void fri_fold_range(const EF* in, EF* out, size_t h, size_t i0, size_t count, co
   twiddles().ensure(logh + 1);
   hipLaunchKernelGGL(k_fri_fold_dev, dim3(ceil_div(count, 256)), dim3(256), 0, st, in, out, h,
                      logh, i0, count, beta, (const uint32_t*)twiddles().inv.p, add);
+  KCHECK();
+}
+
+void fri_fold_leaves(const EF* in, EF* out, size_t h, const EF* beta, const EF* add,
+                     uint32_t* digests, hipStream_t st) {
+  const int logn = log2i(2 * h);
+  twiddles().ensure(logn + 1);
+  const uint32_t* twi = (const uint32_t*)twiddles().inv.p;
+  KernelProbe& probe = p2_probe();
+  hipEvent_t ev0 = probe.on ? probe.begin(st) : nullptr;
+  hipLaunchKernelGGL(k_fold_leaves, dim3(ceil_div(h, 256)), dim3(256), 0, st, in, out, h, logn,
+                     beta, twi, add, digests);
+  if (probe.on) probe.end(ev0, st, (double)h);
+  KCHECK();
+}
+
+void fri_tail_rounds(const FriTailRounds& a, hipStream_t st) {
+  if (a.nr < 1 || a.nr > FRI_TAIL_MAXR || a.logh0 < a.nr || (1 << a.logh0) > FRI_TAIL_MAXH)
+    throw std::runtime_error("fri_tail_rounds: bad round count");
+  twiddles().ensure(a.logh0 + 1);
+  hipLaunchKernelGGL(k_fri_tail, dim3(1), dim3(1024), 0, st, a, (const uint32_t*)twiddles().inv.p);
   KCHECK();
 }
 

@@ -246,4 +246,17 @@ struct LazyEF {
 };
 
 
+// ---------------------------------------------------------------- global loads
+// Pointers read out of a device-side descriptor lose their address space: reading through them
+// compiles to flat loads, which count against lgkmcnt as well, so every scalar-load or LDS wait
+// also waits for the column loads in flight.  These read through the global address space.
+typedef uint32_t kb_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t ld_global(const uint32_t* p, size_t i) {
+  return ((const __attribute__((address_space(1))) uint32_t*)p)[i];
+}
+__device__ __forceinline__ EF ld_global(const EF* p, size_t i) {
+  const kb_u32x4 u = ((const __attribute__((address_space(1))) kb_u32x4*)p)[i];
+  return EF{{u.x, u.y, u.z, u.w}};
+}
+
 }  // namespace kb

@@ -62,7 +62,10 @@ struct RootChallenge {
 // Tree over h >= 2 rows of 8 elements (FRI commit-phase leaves: pairs of EF values, one
 // permutation each).  With fetch_root = false the root stays on the device
 // (tree.layers.back()) and tree.root is not filled.
+// leaves(r0, count, digests) replaces the leaf hashing when given (fri.hip fuses the previous
+// round's fold into it).
 void merkle_from_rows8(MerkleTree& tree, const uint32_t* rows, size_t h, hipStream_t st,
-                       bool fetch_root = true, RootChallenge rc = {}, bool allow_shard = true);
+                       bool fetch_root = true, RootChallenge rc = {}, bool allow_shard = true,
+                       const std::function<void(size_t, size_t, uint32_t*)>& leaves = {});
 
 }  // namespace bfz

@@ -146,6 +146,9 @@ __device__ __forceinline__ uint32_t merkle_node_lane(uint32_t v, const ColList& 
 // read from LDS, every digest written to HBM (query paths need every layer).  (A variant that
 // let the last block to finish build the rest of the tree in the same launch was no faster:
 // the cross-XCD release/acquire cost what the launch boundary did, profiles/r02/ab_merkle_top.txt.)
+// (32- and 16-node subtrees, i.e. 512- and 256-thread blocks with one wave per SIMD from the
+// first layer on, left k_compress_top's time unchanged within 3%: a layer costs one lane-mode
+// permutation latency whatever the occupancy, profiles/r03/ab_open_and_tops.txt)
 constexpr int TOP_NODES = 64;   // fills a 1024-thread block in one lane-mode pass
 constexpr int TOP_LAYERS = 7;   // 64 nodes -> 1
 // Medium layers (TOP_NODES < nodes <= LANE_LAYER_MAX) go to lane mode: a single-lane launch
@@ -168,11 +171,13 @@ __global__ __launch_bounds__(1024) void k_compress_top(const uint32_t* __restric
   const LaneConsts kc = lane_consts(lane);
   for (int l = 0; l < tl.n; l++) {
     const size_t m = per >> l, g = g0 >> l;
-    const uint32_t* src = l == 0 ? prev + 16 * g : buf[(l - 1) & 1];
+    const uint32_t* src = buf[(l - 1) & 1];
     uint32_t* dst = buf[l & 1];
-    // whole 16-lane rows are active together (DPP needs all of them)
+    // whole 16-lane rows are active together (DPP needs all of them); the first layer is read
+    // from HBM, the rest from LDS (one pointer for both would compile to flat loads)
     for (size_t j = threadIdx.x >> 4; j < m; j += blockDim.x >> 4) {
-      const uint32_t v = merkle_node_lane(src[16 * j + lane], inj, tl.c0[l], tl.c1[l], g + j, lane, kc);
+      const uint32_t x = l == 0 ? ld_global(prev, 16 * (g + j) + lane) : src[16 * j + lane];
+      const uint32_t v = merkle_node_lane(x, inj, tl.c0[l], tl.c1[l], g + j, lane, kc);
       if (lane < 8) {
         tl.out[l][8 * (g + j) + lane] = v;
         dst[8 * j + lane] = v;
@@ -184,7 +189,7 @@ __global__ __launch_bounds__(1024) void k_compress_top(const uint32_t* __restric
   // duplex, beta = the last 4 outputs popped in reverse (as k_fri_challenge)
   if (rc.state && threadIdx.x < 64) {
     const uint32_t* root = buf[(tl.n - 1) & 1];
-    uint32_t v = lane < 8 ? root[lane] : rc.state[lane];
+    uint32_t v = lane < 8 ? root[lane] : ld_global(rc.state, lane);
     v = poseidon2_permute_lane(v, lane, kc);
     if (threadIdx.x < 16) {
       rc.state[lane] = v;
@@ -320,7 +325,7 @@ static void build_layers(MerkleTree& t, int L0, size_t len, const std::vector<co
     }
     const unsigned blocks = first > (size_t)TOP_NODES ? (unsigned)(first / TOP_NODES) : 1u;
     const bool root_launch = L + tl.n > nl;
-    hipLaunchKernelGGL(k_compress_top, dim3(blocks), dim3(1024), 0, st,
+    hipLaunchKernelGGL(k_compress_top, dim3(blocks), dim3(16 * TOP_NODES), 0, st,
                        (const uint32_t*)t.layers[L - 1].p, first, make_cols(all), tl,
                        root_launch ? rc : RootChallenge{});
     KCHECK();
@@ -422,14 +427,16 @@ static void hash_rows8_range(const uint32_t* rows, size_t r0, size_t count, uint
 }
 
 void merkle_from_rows8(MerkleTree& t, const uint32_t* rows, size_t h, hipStream_t st,
-                       bool fetch_root, RootChallenge rc, bool allow_shard) {
+                       bool fetch_root, RootChallenge rc, bool allow_shard,
+                       const std::function<void(size_t, size_t, uint32_t*)>& fused) {
   t.mats = {MatRef{rows, h, 8}};
   t.layers.clear();
   t.layers.resize(log2i(h) + 1);
   t.layers[0].reset(8 * h);
   t.sharded_below = 0;
   auto leaves = [&](size_t r0, size_t count) {
-    hash_rows8_range(rows, r0, count, t.layers[0].p, st);
+    if (fused) fused(r0, count, t.layers[0].p);
+    else hash_rows8_range(rows, r0, count, t.layers[0].p, st);
   };
   if (h < 2) throw std::runtime_error("merkle: rows8 tree needs two leaves");
   if (allow_shard && shard_tree(h)) {

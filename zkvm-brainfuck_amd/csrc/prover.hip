@@ -946,9 +946,62 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     shard->allgather(v.p, plan.blk(len) * sizeof(EF), all.p);
     v = std::move(all);
   };
+  DBuf<uint32_t> tail_trees;  // the tail rounds' trees and layers (views below borrow them)
+  DBuf<EF> tail_layers;
+  // A replicated round's fold is left pending and runs fused with the next round's leaf hashes
+  // (fri_fold_leaves): layers.back() is then allocated but not yet written.
+  struct PendingFold {
+    const EF* in = nullptr;
+    const EF* beta = nullptr;
+    const EF* add = nullptr;
+    size_t n = 0;  // fold outputs
+  } pend;
+  auto flush_fold = [&]() {
+    if (!pend.in) return;
+    fri_fold_range(pend.in, layers.back().v.p, pend.n, 0, pend.n, pend.beta, pend.add, st);
+    pend = PendingFold{};
+  };
   for (int rd = 0; len > ((size_t)1 << LOG_BLOWUP); rd++) {
     const size_t h = len / 2;
     FriLayer& cur = layers.back();
+    if (!cur.local && h <= (size_t)FRI_TAIL_MAXH) {  // every remaining round in one launch
+      flush_fold();
+      FriTailRounds a;
+      a.logh0 = log2i(h);
+      a.nr = log2i(len) - LOG_BLOWUP;
+      a.in = cur.v.p;
+      a.state = dstate.p;
+      a.beta = betas.p + rd;
+      size_t nw = 0, nv = 0;
+      for (int r = 0; r < a.nr; r++) {
+        nw += 8 * ((h >> r) * 2 - 1);
+        nv += h >> r;
+      }
+      tail_trees.reset(nw);
+      tail_layers.reset(nv);
+      nw = nv = 0;
+      for (int r = 0; r < a.nr; r++) {
+        const size_t hr = h >> r;
+        const EF* rows = r ? tail_layers.p + nv - 2 * hr : cur.v.p;
+        trees.emplace_back();
+        MerkleTree& t = trees.back();
+        t.mats = {MatRef{(const uint32_t*)rows, hr, 8}};
+        t.layers.resize(log2i(hr) + 1);
+        a.tree[r] = tail_trees.p + nw;
+        for (size_t L = 0; L < t.layers.size(); L++) {
+          t.layers[L] = DBuf<uint32_t>::borrow(tail_trees.p + nw, 8 * (hr >> L));
+          nw += 8 * (hr >> L);
+        }
+        a.layer[r] = tail_layers.p + nv;
+        const int lgh = log2i(hr);
+        a.add[r] = ro.count(lgh) ? ro.at(lgh).p : nullptr;
+        layers.push_back({DBuf<EF>::borrow(tail_layers.p + nv, hr), 0, false});
+        nv += hr;
+      }
+      fri_tail_rounds(a, st);
+      len = h >> (a.nr - 1);
+      break;
+    }
     if (cur.local && !fri_sharded(h)) {
       gather(cur.v, len);
       cur.e0 = 0;
@@ -958,16 +1011,27 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     const size_t i0 = loc ? plan.row0(h) : 0, cnt = loc ? plan.blk(h) : h;
     trees.emplace_back();
     MerkleTree& t = trees.back();
+    std::function<void(size_t, size_t, uint32_t*)> fused;
+    if (pend.in) {  // this round's layer is the pending fold's output: fold + hash in one pass
+      const PendingFold pf = pend;
+      EF* out = cur.v.p;
+      fused = [pf, out, h, &st](size_t, size_t, uint32_t* dig) {
+        fri_fold_leaves(pf.in, out, h, pf.beta, pf.add, dig, st);
+      };
+      pend = PendingFold{};
+    }
     merkle_from_rows8(t, (const uint32_t*)(cur.v.p - 2 * i0), h, st, /*fetch_root=*/false,
-                      RootChallenge{dstate.p, betas.p + rd}, /*allow_shard=*/loc);
+                      RootChallenge{dstate.p, betas.p + rd}, /*allow_shard=*/loc, fused);
     DBuf<EF> next(cnt);
     const int lgh = log2i(h);
     if (!loc && ro.count(lgh) && plan.sharded(h)) gather(ro.at(lgh), h);  // replicated tail
     const EF* add = ro.count(lgh) ? ro.at(lgh).p : nullptr;  // same range as next
-    fri_fold_range(cur.v.p, next.p, h, i0, cnt, betas.p + rd, add, st);
+    if (!loc && h / 2 >= FRI_FUSE_MIN) pend = PendingFold{cur.v.p, betas.p + rd, add, h};
+    else fri_fold_range(cur.v.p, next.p, h, i0, cnt, betas.p + rd, add, st);
     layers.push_back({std::move(next), i0, loc});
     len = h;
   }
+  flush_fold();
   // one device-to-host copy for the commit-phase roots, the transcript state and the final
   // layer (small copies each cost a copy-kernel launch)
   const int nt = (int)trees.size();
