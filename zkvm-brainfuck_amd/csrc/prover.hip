@@ -745,7 +745,15 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     ptabs.emplace(key, std::move(t));
     return p;
   };
-  std::vector<OpenDesc> open1, open2;
+  // Unsharded: the openings run in three transcript-ordered groups (preprocessed + main rounds,
+  // the permutation round, the quotient round), each copied to the host as soon as it is done,
+  // so the host observes a group (~250 host permutations in all) while the GPU computes the
+  // next one instead of after all of them.
+  const bool grouped = !plan.on();
+  auto group_of = [&](int r) { return !grouped ? 0 : r <= 1 ? 0 : r - 1; };
+  constexpr int NGROUP = 3;
+  std::vector<OpenDesc> open1g[NGROUP], open2g[NGROUP];
+  size_t gend[NGROUP] = {0, 0, 0};  // end of each group's range in the opened-value buffer
   for (int r = 0; r < 4; r++)
     for (size_t i = 0; i < rounds[r]->mats.size(); i++) {
       const CMat& m = rounds[r]->mats[i];
@@ -784,11 +792,37 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
       if (two && !o.invd_b) o.scale_b = ef_mul_base(o.scale_b, minv(two_adic_gen(m.log_n)));
       o.out_a = out_a;
       o.out_b = two ? out_b : out_a;
-      (two ? open2 : open1).push_back(o);
+      (two ? open2g : open1g)[group_of(r)].push_back(o);
     }
-  open_batch(open2, 2, st);  // every barycentric opening: two partial + two final launches
-  open_batch(open1, 1, st);
+  for (int r = 0; r < 4; r++)
+    if (!mp[r].empty()) {
+      const MatPts& last = mp[r].back();
+      gend[group_of(r)] = std::max(gend[group_of(r)], last.off[last.npts - 1] +
+                                                          rounds[r]->mats.back().lde.width);
+    }
   std::vector<EF> opened(nvals);
+  static hipEvent_t gev[NGROUP] = {};
+  static EF* gbox = nullptr;  // pinned: the groups' opened values
+  static size_t gcap = 0;
+  if (grouped) {
+    if (!gev[0])
+      for (hipEvent_t& e : gev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (nvals > gcap) {  // no copy into it is pending: every proof waits for its groups
+      if (gbox) HIP_CHECK(hipHostFree(gbox));
+      gcap = std::max(nvals, (size_t)1024);
+      HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&gbox), gcap * sizeof(EF), hipHostMallocDefault));
+    }
+  }
+  for (int g = 0; g < (grouped ? NGROUP : 1); g++) {
+    open_batch(open2g[g], 2, st);  // barycentric openings: two partial + two final launches
+    open_batch(open1g[g], 1, st);
+    if (!grouped) break;
+    const size_t b0 = g ? gend[g - 1] : 0, b1 = std::max(gend[g], b0);
+    if (b1 > b0)
+      HIP_CHECK(hipMemcpyAsync(gbox + b0, opened_d.p + b0, (b1 - b0) * sizeof(EF),
+                               hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipEventRecord(gev[g], st));
+  }
   if (plan.on()) {  // one all-gather; sharded matrices' slices summed, replicated ones kept
     DBuf<EF> all(nvals * plan.G);
     HIP_CHECK(hipStreamSynchronize(st));
@@ -810,16 +844,35 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
             opened[o] = v;
           }
       }
-  } else {
-    fetch(opened.data(), opened_d.p, nvals * sizeof(EF), st);
-    htrace().mark("opened fetched");
   }
-  if (opt.observe_openings)  // decision D1: opened values enter the transcript
+  auto wait_group = [&](int g) {  // the group's values in `opened`
+    for (;;) {
+      const hipError_t e = hipEventQuery(gev[g]);
+      if (e == hipSuccess) break;
+      if (e != hipErrorNotReady) HIP_CHECK(e);
+    }
+    const size_t b0 = g ? gend[g - 1] : 0, b1 = std::max(gend[g], b0);
+    std::copy(gbox + b0, gbox + b1, opened.begin() + b0);
+  };
+  if (grouped) {
+    int have = -1;  // groups copied into `opened` so far
+    for (int r = 0; r < 4; r++) {
+      while (have < group_of(r)) wait_group(++have);
+      if (opt.observe_openings)  // decision D1: opened values enter the transcript
+        for (size_t i = 0; i < rounds[r]->mats.size(); i++)
+          for (int j = 0; j < mp[r][i].npts; j++)
+            for (int c = 0; c < rounds[r]->mats[i].lde.width; c++)
+              ch.observe_ef(opened[mp[r][i].off[j] + c]);
+    }
+    while (have < NGROUP - 1) wait_group(++have);
+    htrace().mark("opened observed");
+  } else if (opt.observe_openings) {
     for (int r = 0; r < 4; r++)
       for (size_t i = 0; i < rounds[r]->mats.size(); i++)
         for (int j = 0; j < mp[r][i].npts; j++)
           for (int c = 0; c < rounds[r]->mats[i].lde.width; c++)
             ch.observe_ef(opened[mp[r][i].off[j] + c]);
+  }
   const EF fri_alpha = ch.sample_ef();
   htrace().mark("fri alpha");
 
@@ -836,11 +889,17 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   std::vector<RedCol> red_cols;
   std::vector<RedMat> red_mats;
   std::vector<RedJob> red_jobs;
+  std::map<int, EF> alpha_pow_w;  // alpha^w by matrix width
+  auto alpha_pow = [&](int w) {
+    auto it = alpha_pow_w.find(w);
+    if (it == alpha_pow_w.end()) it = alpha_pow_w.emplace(w, ef_pow(fri_alpha, (uint64_t)w)).first;
+    return it->second;
+  };
   for (int lh = Lmax; lh >= 1; lh--) {
     std::vector<RedCol> cols;
     std::vector<RedMat> rmats;
     EF ya = ef_zero(), yb = ef_zero();
-    size_t num_red = 0;
+    EF a = ef_one();  // alpha^(number of reduced columns so far at this height)
     bool has_b = false;
     for (int r = 0; r < 4; r++)
       for (size_t i = 0; i < rounds[r]->mats.size(); i++) {
@@ -859,8 +918,6 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
         // point j's coefficients are alpha^(num_red + k): those of the second point are the
         // first point's times alpha^w (they follow it directly in the reduction order)
         for (int j = 0; j < mp[r][i].npts; j++) {
-          EF a = ef_pow(fri_alpha, num_red);
-          num_red += w;
           for (int c = 0; c < w; c++) {
             const EF y = opened[mp[r][i].off[j] + c];
             if (j == 0) {
@@ -875,7 +932,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
         }
         if (mp[r][i].npts == 2) {
           rm.has_b = 1;
-          rm.kb = ef_pow(fri_alpha, (uint64_t)w);
+          rm.kb = alpha_pow(w);
           // single GPU: the second point's denominators come from the zeta table times w_n^-1
           // (reduce_range), folded in here and into yb below
           if (!plan.on()) rm.kb = ef_mul_base(rm.kb, minv(two_adic_gen(m.log_n)));
