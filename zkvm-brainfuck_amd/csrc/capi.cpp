@@ -9,6 +9,8 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <unordered_map>
+#include <vector>
 
 #include "../../include/bfz.h"
 #include "fri.h"
@@ -37,6 +39,15 @@ struct bfz_record {
 namespace {
 std::mutex g_mu;
 thread_local std::string g_err;
+// proofs handed out by emit, by data pointer (bfz_free releases them)
+std::mutex& emitted_mu() {
+  static std::mutex m;
+  return m;
+}
+std::unordered_map<void*, std::vector<uint8_t>*>& emitted() {
+  static auto* m = new std::unordered_map<void*, std::vector<uint8_t>*>();
+  return *m;
+}
 int g_num_queries = -1;
 int g_observe_openings = -1;  // -1: BFZ_OBSERVE_OPENINGS / default
 
@@ -102,7 +113,19 @@ int bfz_device_name(char* buf, size_t cap) {
   });
 }
 
-void bfz_free(void* p) { std::free(p); }
+void bfz_free(void* p) {
+  if (!p) return;
+  {
+    std::lock_guard<std::mutex> lk(emitted_mu());
+    auto it = emitted().find(p);
+    if (it != emitted().end()) {
+      delete it->second;
+      emitted().erase(it);
+      return;
+    }
+  }
+  std::free(p);
+}
 
 int bfz_execute(const char* elf, const uint8_t* in, size_t nin, uint8_t* out, size_t cap,
                 size_t* out_len, uint64_t* cycles) {
@@ -146,12 +169,23 @@ int bfz_trace(const char* elf, const uint8_t* in, size_t nin, int chip, int prep
   });
 }
 
+// A proof (about 1 MB) is handed to the caller without a copy: the vector moves to the heap
+// and bfz_free finds it by its data pointer.
 static int emit(std::vector<uint8_t>&& v, uint8_t** proof, size_t* len) {
-  uint8_t* p = (uint8_t*)std::malloc(v.size() ? v.size() : 1);
-  if (!p) throw std::runtime_error("out of host memory");
-  std::memcpy(p, v.data(), v.size());
-  *proof = p;
-  *len = v.size();
+  if (v.empty()) {
+    uint8_t* p = (uint8_t*)std::malloc(1);
+    if (!p) throw std::runtime_error("out of host memory");
+    *proof = p;
+    *len = 0;
+    return 0;
+  }
+  auto* h = new std::vector<uint8_t>(std::move(v));
+  {
+    std::lock_guard<std::mutex> lk(emitted_mu());
+    emitted()[h->data()] = h;
+  }
+  *proof = h->data();
+  *len = h->size();
   return 0;
 }
 
@@ -287,7 +321,9 @@ int bfz_perm_trace(int chip, const uint32_t* main, const uint32_t* prep, size_t 
     const int w = 4 * bfz::perm_width(chip);
     bfz::DBuf<uint32_t> pe(n * w);
     bfz::DBuf<kb::EF> cs(1);
-    bfz::perm_trace(chip, mc.p, pwid ? pc.p : nullptr, n, ch, pe.p, cs.p, st);
+    bfz::DBuf<bfz::PermChallenges> chd(1);
+    bfz::upload_async(chd.p, &ch, sizeof(ch), st);
+    bfz::perm_trace(chip, mc.p, pwid ? pc.p : nullptr, n, chd.p, pe.p, cs.p, st);
     std::vector<uint32_t> cm(n * w);
     HIP_CHECK(hipMemcpyAsync(cm.data(), pe.p, cm.size() * 4, hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipMemcpyAsync(cumsum, cs.p, 16, hipMemcpyDeviceToHost, st));
@@ -712,7 +748,9 @@ int bfz_record_prove(const bfz_pk* pk, const bfz_record* rec, uint8_t** proof, s
     bfz::StageTimes st;
     auto v = bfz::prove_events(*pk->pk, rec->ev, o, &st);
     fill_timings(st, t);
-    return emit(std::move(v), proof, len);
+    const int r = emit(std::move(v), proof, len);
+    bfz::host_mark("emitted");
+    return r;
   });
 }
 

@@ -11,6 +11,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <map>
+#include <unordered_map>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -81,8 +82,10 @@ class DevicePool {
   ~DevicePool() {}
 
  private:
-  std::map<size_t, std::vector<void*>> free_;
-  std::map<void*, size_t> size_of_;
+  // hash maps: a proof allocates and releases a few hundred buffers, and the releases at the
+  // end of a proof sit between the last kernel of one proof and the first of the next
+  std::unordered_map<size_t, std::vector<void*>> free_;
+  std::unordered_map<void*, size_t> size_of_;
 };
 
 DevicePool& pool();

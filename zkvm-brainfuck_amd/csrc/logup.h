@@ -13,8 +13,22 @@ struct PermChallenges {
 
 // mainc/prepc: column-major bit-reversed trace evaluations (n rows).  perm: 4*perm_width(chip)
 // base columns (n rows, bit-reversed).  cumsum_dev: device EF receiving the cumulative sum.
+// ch: DEVICE memory (the prover samples the challenges on the device, challenge_perm).
 void perm_trace(int chip, const uint32_t* mainc, const uint32_t* prepc, size_t n,
-                const PermChallenges& ch, uint32_t* perm, kb::EF* cumsum_dev, hipStream_t st);
+                const PermChallenges* ch, uint32_t* perm, kb::EF* cumsum_dev, hipStream_t st);
+// Device transcript step after the main commit: the DuplexChallenger state `ch` (host layout,
+// device memory) observes the 8-word root and samples the LogUp alpha and beta (prover.rs:
+// 269-272); out receives alpha and beta^0..7.  The host replays the same step when it fetches
+// the root later, so its transcript stays in step.
+struct DevChallenger {
+  uint32_t st[16];
+  uint32_t in[8];
+  int32_t nin;
+  uint32_t out[8];
+  int32_t nout;
+};
+void challenge_perm(const DevChallenger* ch, const uint32_t* root, PermChallenges* out,
+                    hipStream_t st);
 
 void ef_inclusive_scan(kb::EF* data, size_t n, hipStream_t st);
 

@@ -12,6 +12,8 @@
 
 #include <type_traits>
 
+#include "poseidon2.h"
+
 namespace bfz {
 
 using namespace kb;
@@ -67,8 +69,10 @@ __device__ __forceinline__ void batch_frac(const uint32_t (&pr)[PWD], const uint
 template <int CHIP>
 __global__ __launch_bounds__(256) void k_perm_rows(const uint32_t* __restrict__ mainc,
                                                    const uint32_t* __restrict__ prepc, size_t n,
-                                                   PermChallenges ch, uint32_t* __restrict__ perm,
+                                                   const PermChallenges* __restrict__ chp,
+                                                   uint32_t* __restrict__ perm,
                                                    EF* __restrict__ rowsum) {
+  const PermChallenges ch = *chp;  // uniform: scalar loads
   constexpr int MW = MAIN_W[CHIP];
   constexpr int PWD = PREP_W[CHIP] > 0 ? PREP_W[CHIP] : 1;
   constexpr int NB = (LookupsOf<CHIP>::v.n + 1) / 2;
@@ -194,14 +198,14 @@ void ef_inclusive_scan(EF* data, size_t n, hipStream_t st) {
 
 template <int CHIP>
 static void launch_rows(const uint32_t* mainc, const uint32_t* prepc, size_t n,
-                        const PermChallenges& ch, uint32_t* perm, EF* rowsum, hipStream_t st) {
+                        const PermChallenges* ch, uint32_t* perm, EF* rowsum, hipStream_t st) {
   hipLaunchKernelGGL(k_perm_rows<CHIP>, dim3(ceil_div(n, 256)), dim3(256), 0, st, mainc, prepc, n,
                      ch, perm, rowsum);
   KCHECK();
 }
 
 void perm_trace(int chip, const uint32_t* mainc, const uint32_t* prepc, size_t n,
-                const PermChallenges& ch, uint32_t* perm, EF* cumsum_dev, hipStream_t st) {
+                const PermChallenges* ch, uint32_t* perm, EF* cumsum_dev, hipStream_t st) {
   const int logn = log2i(n);
   DBuf<EF> rows(n), nat(n);
   switch (chip) {
@@ -243,6 +247,52 @@ __global__ __launch_bounds__(256) void k_write_phi(const EF* __restrict__ local,
 #pragma unroll
   for (int e = 0; e < 4; e++) perm[(size_t)(col0 + e) * n + t] = v.c[e];
   if (t == n - 1) *cumsum = v;
+}
+
+// One 16-lane row runs the DuplexChallenger of prover.hip (Challenger) on the device: lane l
+// holds state word l, lanes 0..7 the input and output buffers; nin / nout are uniform.
+__global__ __launch_bounds__(64) void k_challenge_perm(const DevChallenger* __restrict__ c,
+                                                       const uint32_t* __restrict__ root,
+                                                       PermChallenges* __restrict__ out) {
+  const int lane = threadIdx.x & 15;
+  const LaneConsts kc = lane_consts(lane);
+  uint32_t stv = c->st[lane], inv = lane < 8 ? c->in[lane] : 0u, outv = lane < 8 ? c->out[lane] : 0u;
+  int nin = c->nin, nout = c->nout;
+  auto duplex = [&]() {
+    if (lane < nin) stv = inv;
+    stv = poseidon2_permute_lane(stv, lane, kc);
+    outv = stv;
+    nout = 8;
+    nin = 0;
+  };
+  auto observe = [&](uint32_t v) {
+    nout = 0;
+    if (lane == nin) inv = v;
+    if (++nin == 8) duplex();
+  };
+  auto sample = [&]() {
+    if (nin > 0 || nout == 0) duplex();
+    --nout;
+    return (uint32_t)__shfl(outv, nout, 16);
+  };
+  for (int i = 0; i < 8; i++) observe(root[i]);
+  EF alpha, beta;
+  for (int e = 0; e < 4; e++) alpha.c[e] = sample();
+  for (int e = 0; e < 4; e++) beta.c[e] = sample();
+  if (threadIdx.x == 0) {
+    out->alpha = alpha;
+    EF p = ef_one();
+    for (int j = 0; j < 8; j++) {
+      out->beta_pows[j] = p;
+      p = ef_mul(p, beta);
+    }
+  }
+}
+
+void challenge_perm(const DevChallenger* ch, const uint32_t* root, PermChallenges* out,
+                    hipStream_t st) {
+  hipLaunchKernelGGL(k_challenge_perm, dim3(1), dim3(64), 0, st, ch, root, out);
+  KCHECK();
 }
 
 }  // namespace bfz

@@ -42,8 +42,10 @@ struct ShardCtx {
 constexpr size_t SHARD_MIN_LEAVES = 1024;
 ShardCtx*& shard_ctx();
 
-// Builds the tree (heights must be powers of two) and copies the root to the host.
-void merkle_build(const std::vector<MatRef>& mats, MerkleTree& tree, hipStream_t st);
+// Builds the tree (heights must be powers of two) and copies the root to the host (with
+// fetch_root = false the root stays on the device, tree.layers.back(), tree.root not filled).
+void merkle_build(const std::vector<MatRef>& mats, MerkleTree& tree, hipStream_t st,
+                  bool fetch_root = true);
 
 // Batched Poseidon2 permutations of n 16-element states in place (device pointer).
 void poseidon2_batch(uint32_t* states, size_t n, hipStream_t st);

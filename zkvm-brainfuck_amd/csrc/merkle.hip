@@ -379,7 +379,7 @@ static void build_sharded(MerkleTree& t, size_t h0, const std::vector<const MatR
   build_layers(t, nl - lg + 1, G, sorted, next, st, fetch_root, rc);
 }
 
-void merkle_build(const std::vector<MatRef>& mats, MerkleTree& t, hipStream_t st) {
+void merkle_build(const std::vector<MatRef>& mats, MerkleTree& t, hipStream_t st, bool fetch_root) {
   if (mats.empty()) throw std::runtime_error("merkle: no matrices");
   t.mats = mats;
   std::vector<const MatRef*> sorted;
@@ -404,11 +404,11 @@ void merkle_build(const std::vector<MatRef>& mats, MerkleTree& t, hipStream_t st
     if (probe.on) probe.end(ev0, st, (double)count * ((cl.n + 7) / 8));
   };
   if (shard_tree(h0)) {
-    build_sharded(t, h0, sorted, next, leaves, st, true);
+    build_sharded(t, h0, sorted, next, leaves, st, fetch_root);
     return;
   }
   leaves(0, h0);
-  build_layers(t, 1, h0, sorted, next, st);
+  build_layers(t, 1, h0, sorted, next, st, fetch_root);
 }
 
 static void hash_rows8_range(const uint32_t* rows, size_t r0, size_t count, uint32_t* digests,

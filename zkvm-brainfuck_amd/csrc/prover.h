@@ -61,7 +61,7 @@ struct CMat {               // a committed matrix: LDE on 3*H_2n (bit-reversed, 
 struct Round {
   std::vector<CMat> mats;
   MerkleTree tree;
-  void commit(hipStream_t st);
+  void commit(hipStream_t st, bool fetch_root = true);
 };
 
 struct ProvingKey {
@@ -122,12 +122,16 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
 // The split MachineProver surface (crates/stark/src/prover.rs:209-236 commit, :242-553 open).
 // MainData is ShardMainData (types.rs:13-18) kept in HBM: the traces' evaluations, the
 // committed LDEs and their Merkle tree, alive from commit until the owner frees it.
+// BFZ_HOST_TRACE=1: prints the host time (us since the proof started) with a label
+void host_mark(const char* what);
+
 struct MainData {
   DeviceTraces dt;
   std::vector<int> order;   // dt index of the k-th committed matrix
   std::vector<int> chip;    // chip of the k-th committed matrix, sorted (Reverse(height), name)
   std::vector<size_t> hn;   // its height
   Round mainr;              // the main commit (LDEs + tree)
+  bool root_on_host = true; // mainr.tree.root filled (false: on the device only, prove_device)
 };
 void commit_main(MainData& md);  // md.dt holds the traces
 // Challenger state after pk.observe_into (prover.rs:595-601) on a fresh DuplexChallenger.

@@ -112,13 +112,17 @@ struct HostTrace {
     if (!on) return;
     const auto now = std::chrono::steady_clock::now();
     if (reset) t0 = now;
-    std::fprintf(stderr, "host %9.1f %s\n", std::chrono::duration<double, std::micro>(now - t0).count(), what);
+    std::fprintf(stderr, "host %9.1f %s (abs %.1f)\n", std::chrono::duration<double, std::micro>(now - t0).count(), what,
+                 std::chrono::duration<double, std::micro>(now.time_since_epoch()).count());
   }
 };
 HostTrace& htrace() {
   static HostTrace h;
   return h;
 }
+}  // namespace
+void host_mark(const char* what) { htrace().mark(what); }
+namespace {
 struct EvTimer {
   bool on = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
@@ -155,36 +159,40 @@ void to_canon_digest(const uint32_t* d, uint32_t* o) {
   for (int i = 0; i < 8; i++) o[i] = from_mont(d[i]);
 }
 
-struct Writer {  // appends into a buffer sized up front (reserve): a memcpy per word
+struct Writer {  // appends through a cursor into a buffer sized up front (one fill, no per-word resize)
   std::vector<uint8_t> b;
-  void u32(uint32_t v) {
-    const size_t n = b.size();
-    b.resize(n + 4);
-    std::memcpy(b.data() + n, &v, 4);
+  size_t n = 0;
+  void reserve(size_t cap) { b.resize(cap); }
+  uint8_t* room(size_t k) {
+    if (n + k > b.size()) b.resize(std::max(2 * b.size(), n + k));
+    uint8_t* p = b.data() + n;
+    n += k;
+    return p;
   }
+  void u32(uint32_t v) { std::memcpy(room(4), &v, 4); }
   void fp(uint32_t mont) { u32(from_mont(mont)); }
-  void raw(const uint32_t* w, size_t n) {  // words already canonical
-    const size_t o = b.size();
-    b.resize(o + 4 * n);
-    std::memcpy(b.data() + o, w, 4 * n);
-  }
+  void raw(const uint32_t* w, size_t k) { std::memcpy(room(4 * k), w, 4 * k); }  // canonical words
   void ef(const EF& e) {
-    for (int i = 0; i < 4; i++) fp(e.c[i]);
+    uint32_t v[4];
+    for (int i = 0; i < 4; i++) v[i] = from_mont(e.c[i]);
+    std::memcpy(room(16), v, 16);
   }
   void digest(const uint32_t* d) {
-    for (int i = 0; i < 8; i++) fp(d[i]);
+    uint32_t v[8];
+    for (int i = 0; i < 8; i++) v[i] = from_mont(d[i]);
+    std::memcpy(room(32), v, 32);
   }
-  void bytes(const void* p, size_t n) {
-    const uint8_t* q = (const uint8_t*)p;
-    b.insert(b.end(), q, q + n);
+  void bytes(const void* p, size_t k) { std::memcpy(room(k), p, k); }
+  std::vector<uint8_t> take() {
+    b.resize(n);
+    return std::move(b);
   }
-};
-}  // namespace
+};}  // namespace
 
-void Round::commit(hipStream_t st) {
+void Round::commit(hipStream_t st, bool fetch_root) {
   std::vector<MatRef> refs;
   for (CMat& m : mats) refs.push_back(m.ref());
-  merkle_build(refs, tree, st);
+  merkle_build(refs, tree, st, fetch_root);
 }
 
 namespace {
@@ -385,7 +393,7 @@ struct ProofScope {
 
 // MachineProver::commit (prover.rs:209-236): sort by (Reverse(height), name), coset LDE of
 // every main trace, one MerkleTreeMmcs commit.  md.dt must hold the traces.
-void commit_main_impl(MainData& md, ProofScope& ps) {
+void commit_main_impl(MainData& md, ProofScope& ps, bool fetch_root = true) {
   hipStream_t st = stream();
   DeviceTraces& dt = md.dt;
   const int nc = (int)dt.chips.size();
@@ -408,7 +416,8 @@ void commit_main_impl(MainData& md, ProofScope& ps) {
   for (int k = 0; k < nc; k++)
     lde_into(md.mainr.mats[k], dt.evals[md.order[k]].p, md.hn[k], CHIP_INFO[md.chip[k]].main_w, ONE,
              st, &ps.ev, ps.tms, &plan, &chip_next_cols(md.chip[k]).main);
-  md.mainr.commit(st);
+  md.mainr.commit(st, fetch_root);
+  md.root_on_host = fetch_root;
   if (ps.ev.on) ps.ev.end(e0, st, &ps.tms->main_commit);
 }
 
@@ -477,8 +486,9 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
   ProofScope ps(opt.timing, times);
   MainData md;
   md.dt = std::move(dt);
-  commit_main_impl(md, ps);
+  commit_main_impl(md, ps, /*fetch_root=*/false);  // the LogUp challenges are sampled on the device
   auto proof = open_impl(pk, md, challenger_after_pk(pk), opt, ps);
+  htrace().mark("open returned");
   ps.finish();
   dt = std::move(md.dt);
   return proof;
@@ -504,37 +514,67 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   const ShardCtx* shard = shard_ctx();
 
   // ---- open (prover.rs:242-553), on a clone of the challenger (prover.rs:578)
-  htrace().mark("main root fetched");
-  ch.observe_digest(mainr.tree.root);
-  const EF perm_alpha = ch.sample_ef();
-  const EF perm_beta = ch.sample_ef();
+  htrace().mark("open start");
   PermChallenges pc;
-  pc.alpha = perm_alpha;
-  pc.beta_pows[0] = ef_one();
-  for (int j = 1; j < 8; j++) pc.beta_pows[j] = ef_mul(pc.beta_pows[j - 1], perm_beta);
+  EF perm_alpha;
+  auto host_perm_challenges = [&]() {  // prover.rs:265-272
+    ch.observe_digest(mainr.tree.root);
+    perm_alpha = ch.sample_ef();
+    const EF perm_beta = ch.sample_ef();
+    pc.alpha = perm_alpha;
+    pc.beta_pows[0] = ef_one();
+    for (int j = 1; j < 8; j++) pc.beta_pows[j] = ef_mul(pc.beta_pows[j - 1], perm_beta);
+  };
+  DBuf<PermChallenges> pc_d(1);
+  if (md.root_on_host) {
+    host_perm_challenges();
+    upload_async(pc_d.p, &pc, sizeof(pc), st);
+  } else {  // the root is still on the device: the same transcript step runs there, and the host
+            // replays it when the root comes back with the cumulative sums (no round trip here)
+    DevChallenger dc;
+    std::memcpy(dc.st, ch.st, sizeof(dc.st));
+    std::memcpy(dc.in, ch.in, sizeof(dc.in));
+    std::memcpy(dc.out, ch.out, sizeof(dc.out));
+    dc.nin = ch.nin;
+    dc.nout = ch.nout;
+    DBuf<DevChallenger> dc_d(1);
+    upload_async(dc_d.p, &dc, sizeof(dc), st);
+    challenge_perm(dc_d.p, mainr.tree.layers.back().p, pc_d.p, st);
+  }
+  htrace().mark("perm challenges");
 
   hipEvent_t e1 = ev.on ? ev.begin(st) : nullptr;
   Round permr;
   permr.mats.resize(nc);
-  DBuf<EF> cums_d(nc);
+  DBuf<EF> cums_d(nc + 2);  // + the main root (8 words) when it is fetched with the sums
+  if (!md.root_on_host)
+    HIP_CHECK(hipMemcpyAsync(cums_d.p + nc, mainr.tree.layers.back().p, 32, hipMemcpyDeviceToDevice, st));
   for (int k = 0; k < nc; k++) {
     const int c = chip[k];
     const int pw = perm_width(c);
     DBuf<uint32_t> pe(4 * (size_t)pw * hn[k]);
     const int pi = pk.idx_of_chip[c];
     const uint32_t* prep = pi >= 0 ? pk.prep_evals[pi].p : nullptr;
-    if (k == 0) htrace().mark("perm_rows launch");
-    perm_trace(c, dt.evals[order[k]].p, prep, hn[k], pc, pe.p, cums_d.p + k, st);
+    if (k == 0) htrace().mark("perm_rows buffers");
+    perm_trace(c, dt.evals[order[k]].p, prep, hn[k], pc_d.p, pe.p, cums_d.p + k, st);
+    if (k == 0) htrace().mark("perm_rows launched");
     lde_into(permr.mats[k], pe.p, hn[k], 4 * pw, ONE, st, &ev, tms, &plan, &chip_next_cols(c).perm);
   }
   permr.commit(st);
-  std::vector<EF> cums(nc);
-  fetch(cums.data(), cums_d.p, nc * sizeof(EF), st);
+  std::vector<EF> cums(nc + 2);
+  fetch(cums.data(), cums_d.p, (md.root_on_host ? nc : nc + 2) * sizeof(EF), st);
   htrace().mark("cums fetched");
+  if (!md.root_on_host) {
+    std::memcpy(mainr.tree.root, &cums[nc], 32);
+    md.root_on_host = true;
+    host_perm_challenges();
+  }
+  cums.resize(nc);
   if (ev.on) ev.end(e1, st, &tms->perm);
   ch.observe_digest(permr.tree.root);
   for (int k = 0; k < nc; k++) ch.observe_ef(cums[k]);
   const EF alpha = ch.sample_ef();
+  htrace().mark("quotient challenge");
 
   // ---- quotient (prover.rs:344-412)
   hipEvent_t e2 = ev.on ? ev.begin(st) : nullptr;
@@ -1162,11 +1202,12 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   }
   size_t nwords = 0;
   uint32_t* words = gather_queries(segs, qidx, nwords, shard, st);
+  htrace().mark("queries gathered");
   if (ev.on) ev.end(e4, st, &tms->fri);
 
   // ---- serialize (BFZ1 normal form)
   Writer w;
-  w.b.reserve(4 * nwords + ((size_t)64 << 10));
+  w.reserve(4 * nwords + ((size_t)64 << 10));
   w.u32(0x315a4642u);
   w.u32((uint32_t)nc);
   for (int k = 0; k < nc; k++) {
@@ -1240,7 +1281,8 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   }
   w.ef(fin[0]);
   w.u32(witness);
-  return std::move(w.b);
+  htrace().mark("serialized");
+  return w.take();
 }
 }  // namespace
 
@@ -1257,8 +1299,10 @@ std::vector<uint8_t> prove_events(const ProvingKey& pk, const DeviceEvents& ev,
   htrace().mark("proof start", true);
   DeviceTraces dt;
   generate_traces_device(ev, dt, st);
+  htrace().mark("traces launched");
   if (timing) HIP_CHECK(hipEventRecord(b, st));
   auto proof = prove_device(pk, dt, opt, times);
+  htrace().mark("proof returned");
   if (timing) {
     float ms = 0;
     HIP_CHECK(hipEventElapsedTime(&ms, a, b));
