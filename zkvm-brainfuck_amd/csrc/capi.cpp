@@ -119,6 +119,7 @@ void bfz_free(void* p) {
     std::lock_guard<std::mutex> lk(emitted_mu());
     auto it = emitted().find(p);
     if (it != emitted().end()) {
+      bfz::release_proof_buffer(std::move(*it->second));
       delete it->second;
       emitted().erase(it);
       return;

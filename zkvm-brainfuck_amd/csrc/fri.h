@@ -116,7 +116,8 @@ struct GatherSeg {
   int32_t own_shift;
   int32_t pad;
 };
-// out[q * words_per_query + ...] = the segments' words for qidx[q], segments in order.  In a
+// out[q * words_per_query + ...] = the segments' words for qidx[q], segments in order; a segment
+// with base == nullptr is `count` literal words of value xr.  In a
 // sharded proof (shard != nullptr, world > 1) every rank writes the words it owns and one sum
 // all-reduce over the device buffer completes them.
 // Returns the nwords gathered words (canonical form) in a pinned host buffer that stays valid

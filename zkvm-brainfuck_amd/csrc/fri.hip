@@ -481,10 +481,14 @@ __global__ __launch_bounds__(256) void k_gather_segs(const GatherSeg* __restrict
   if (t >= (size_t)nseg * nq) return;
   const int q = (int)(t / nseg), s = (int)(t % nseg);
   const GatherSeg g = segs[s];
+  uint32_t* o = out + (size_t)q * words_per_q + seg_off[s];
+  if (!g.base) {  // literal words (the serialized length fields): rank 0 writes them
+    for (uint32_t k = 0; k < g.count; k++) o[k] = rank == 0 ? g.xr : 0u;
+    return;
+  }
   const uint32_t e = (qidx[q] >> g.shift) ^ g.xr;
   const int owner = g.own_shift >= 0 ? (int)(e >> g.own_shift) : 0;
   const uint64_t pos = (uint64_t)e * g.unit;
-  uint32_t* o = out + (size_t)q * words_per_q + seg_off[s];
   // canonical form here, so the host copies the words straight into the proof
   for (uint32_t k = 0; k < g.count; k++)
     o[k] = owner == rank ? from_mont(ld_global(g.base, pos + k * g.stride)) : 0u;

@@ -124,6 +124,9 @@ std::vector<uint8_t> prove_device(const ProvingKey& pk, DeviceTraces& dt, const 
 // committed LDEs and their Merkle tree, alive from commit until the owner frees it.
 // BFZ_HOST_TRACE=1: prints the host time (us since the proof started) with a label
 void host_mark(const char* what);
+// A buffer for the next proof's bytes (a returned one when available) / hand one back.
+std::vector<uint8_t> acquire_proof_buffer();
+void release_proof_buffer(std::vector<uint8_t>&& v);
 
 struct MainData {
   DeviceTraces dt;

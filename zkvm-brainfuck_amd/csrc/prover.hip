@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 
 #include "fri.h"
 #include "host_p2.h"
@@ -122,6 +123,22 @@ HostTrace& htrace() {
 }
 }  // namespace
 void host_mark(const char* what) { htrace().mark(what); }
+
+// Proof buffers come back through bfz_free and are reused: a fresh 1 MB vector costs a page fault
+// per 4 KB page on first touch (hundreds of microseconds on a busy host).
+static std::mutex g_pb_mu;
+static std::vector<std::vector<uint8_t>> g_pb;
+std::vector<uint8_t> acquire_proof_buffer() {
+  std::lock_guard<std::mutex> lk(g_pb_mu);
+  if (g_pb.empty()) return {};
+  std::vector<uint8_t> v = std::move(g_pb.back());
+  g_pb.pop_back();
+  return v;
+}
+void release_proof_buffer(std::vector<uint8_t>&& v) {
+  std::lock_guard<std::mutex> lk(g_pb_mu);
+  if (g_pb.size() < 4) g_pb.push_back(std::move(v));
+}
 namespace {
 struct EvTimer {
   bool on = false;
@@ -162,7 +179,10 @@ void to_canon_digest(const uint32_t* d, uint32_t* o) {
 struct Writer {  // appends through a cursor into a buffer sized up front (one fill, no per-word resize)
   std::vector<uint8_t> b;
   size_t n = 0;
-  void reserve(size_t cap) { b.resize(cap); }
+  void reserve(size_t cap) {
+    b = acquire_proof_buffer();  // a returned proof's pages: no page faults on the ~1 MB
+    b.resize(cap);
+  }
   uint8_t* room(size_t k) {
     if (n + k > b.size()) b.resize(std::max(2 * b.size(), n + k));
     uint8_t* p = b.data() + n;
@@ -1179,23 +1199,33 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   };
   std::vector<GatherSeg> segs;
   const int ncommit = (int)trees.size();
+  // The segments follow the serialized query layout, its length words included as literal
+  // segments (base == nullptr: count words of value xr), so the gathered words are the query
+  // section of the proof as is.
+  auto lit = [&](uint32_t v) { segs.push_back({nullptr, 0, 0, v, 0, 1, -1, 0}); };
+  lit(4);
   for (int r = 0; r < 4; r++) {
     const Round& R = *rounds[r];
     const int lrm = (int)R.tree.layers.size() - 1;
+    lit((uint32_t)R.mats.size());
     for (const CMat& m : R.mats) {  // row (index >> (Lmax - lh)) of every column
       const int lh = log2i(m.lde.height);
+      lit((uint32_t)m.lde.width);
       segs.push_back({m.rows(), (uint64_t)m.stride(), (uint32_t)(Lmax - lh), 0, 1,
                       (uint32_t)m.lde.width, m.sharded ? lh - plan.lg : -1, 0});
     }
+    lit((uint32_t)lrm);
     for (int L = 0; L < lrm; L++)  // sibling digest at layer L
       segs.push_back({R.tree.layers[L].p, 1, (uint32_t)(Lmax - lrm + L), 1, 8, 8,
                       owner_shift(R.tree, L), 0});
   }
+  lit((uint32_t)ncommit);
   for (int i = 0; i < ncommit; i++) {
     const FriLayer& fl = layers[i];  // sibling EF
     segs.push_back({(const uint32_t*)(fl.v.p - fl.e0), 1, (uint32_t)i, 1, 4, 4,
                     fl.local ? Lmax - i - plan.lg : -1, 0});
     const int lm = (int)trees[i].layers.size() - 1;
+    lit((uint32_t)lm);
     for (int L = 0; L < lm; L++)
       segs.push_back({trees[i].layers[L].p, 1, (uint32_t)(i + 1 + L), 1, 8, 8,
                       owner_shift(trees[i], L), 0});
@@ -1253,32 +1283,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   w.u32((uint32_t)ncommit);
   for (int i = 0; i < ncommit; i++) w.digest(trees[i].root);
   w.u32((uint32_t)nq);
-  size_t pos = 0;  // the gathered words arrive canonical (k_gather_segs)
-  auto take = [&](size_t n) {
-    w.raw(words + pos, n);
-    pos += n;
-  };
-  for (int q = 0; q < nq; q++) {
-    w.u32(4);
-    for (int r = 0; r < 4; r++) {
-      const Round& R = *rounds[r];
-      const int lrm = (int)R.tree.layers.size() - 1;
-      w.u32((uint32_t)R.mats.size());
-      for (const CMat& m : R.mats) {
-        w.u32((uint32_t)m.lde.width);
-        take(m.lde.width);
-      }
-      w.u32((uint32_t)lrm);
-      take((size_t)lrm * 8);
-    }
-    w.u32((uint32_t)ncommit);
-    for (int i = 0; i < ncommit; i++) {
-      take(4);
-      const int lm = (int)trees[i].layers.size() - 1;
-      w.u32((uint32_t)lm);
-      take((size_t)lm * 8);
-    }
-  }
+  w.raw(words, nwords);  // every query in serialized form (canonical words + length words)
   w.ef(fin[0]);
   w.u32(witness);
   htrace().mark("serialized");
