@@ -126,6 +126,32 @@ def poseidon2_roofline(tm):
             "frac": round(tops / VALU_PEAK_TOPS, 4)}
 
 
+def openings_roofline(tm):
+    """HBM roofline of the opening kernels, timed per launch with HIP events on the prover
+    stream: k_open_partial_batch (barycentric sums over each matrix's low coset: 4 B per word +
+    16 B of weight table per row and point) and k_reduce (FRI reduced openings over the whole
+    LDE: 4 B per word + 16 B per row for each denominator table read and for ro written)."""
+    out = {}
+    for key, ms, nbytes, launches, kernel in (
+            ("partial", tm.open_kernel_ms, tm.open_kernel_bytes, tm.open_kernel_launches,
+             "k_open_partial_batch<NP>"),
+            ("reduce", tm.reduce_kernel_ms, tm.reduce_kernel_bytes, tm.reduce_kernel_launches,
+             "k_reduce")):
+        if ms <= 0:
+            continue
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        out[key] = {"kernel": kernel, "bytes_per_proof": int(nbytes), "kernel_ms": round(ms, 3),
+                    "launches": launches, "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    if not out:
+        return None
+    ms = sum(v["kernel_ms"] for v in out.values())
+    nb = sum(v["bytes_per_proof"] for v in out.values())
+    gbs = nb / (ms * 1e-3) / 1e9
+    out.update({"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(gbs / HBM_PEAK_GBS, 4)})
+    return out
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -528,6 +554,7 @@ def main():
             "roofline": ntt_roofline(tm),
             "ntt_valu": ntt_valu(tm),
             "poseidon2": poseidon2_roofline(tm),
+            "openings": openings_roofline(tm),
             "proof_bytes": len(proof),
         }
         if "sustained" in extra:

@@ -49,6 +49,12 @@ pub struct bfz_timings {
     pub p2_perms: f64,
     pub p2_launches: c_int,
     pub lde_elem_stages: f64,
+    pub open_kernel_ms: f64,
+    pub open_kernel_bytes: f64,
+    pub open_kernel_launches: c_int,
+    pub reduce_kernel_ms: f64,
+    pub reduce_kernel_bytes: f64,
+    pub reduce_kernel_launches: c_int,
 }
 
 #[repr(C)]

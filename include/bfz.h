@@ -69,6 +69,13 @@ typedef struct {
   double p2_kernel_ms, p2_perms; /* Poseidon2 leaf/compress kernels: time and permutations */
   int p2_launches;
   double lde_elem_stages; /* radix-2 element-stages of the coset LDEs: 3*n*log2(n)*w per call */
+  /* Openings (k_open_partial_batch: 4*n*w + 16*n*points B per matrix, the low coset) and reduced
+   * openings (k_reduce: 4*H*w + 16*H*(2 or 3) B per LDE height): per-launch events, algorithmic
+   * bytes. */
+  double open_kernel_ms, open_kernel_bytes;
+  int open_kernel_launches;
+  double reduce_kernel_ms, reduce_kernel_bytes;
+  int reduce_kernel_launches;
 } bfz_timings;
 
 int bfz_init(int device);

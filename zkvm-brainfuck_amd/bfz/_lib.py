@@ -26,6 +26,9 @@ class Timings(ctypes.Structure):
         ("lde_calls", c_int), ("ntt_kernel_ms", c_double), ("ntt_kernel_bytes", c_double),
         ("ntt_kernel_launches", c_int), ("p2_kernel_ms", c_double), ("p2_perms", c_double),
         ("p2_launches", c_int), ("lde_elem_stages", c_double),
+        ("open_kernel_ms", c_double), ("open_kernel_bytes", c_double), ("open_kernel_launches", c_int),
+        ("reduce_kernel_ms", c_double), ("reduce_kernel_bytes", c_double),
+        ("reduce_kernel_launches", c_int),
     ]
 
     def as_dict(self) -> dict:

@@ -734,6 +734,12 @@ void fill_timings(const bfz::StageTimes& st, bfz_timings* t) {
   t->p2_perms = st.p2_perms;
   t->p2_launches = st.p2_launches;
   t->lde_elem_stages = st.lde_elem_stages;
+  t->open_kernel_ms = st.open_kernel_ms;
+  t->open_kernel_bytes = st.open_kernel_bytes;
+  t->open_kernel_launches = st.open_kernel_launches;
+  t->reduce_kernel_ms = st.reduce_kernel_ms;
+  t->reduce_kernel_bytes = st.reduce_kernel_bytes;
+  t->reduce_kernel_launches = st.reduce_kernel_launches;
 }
 struct ShardScope {  // installs the shard context for one proof
   explicit ShardScope(bfz::ShardCtx* c) { bfz::shard_ctx() = c; }

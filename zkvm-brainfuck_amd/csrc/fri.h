@@ -63,7 +63,7 @@ void open_batch(std::vector<OpenDesc>& ds, int np, hipStream_t st);
 // folded w_n^-1 into every RedMat::kb and into yb.
 void reduce_range(const RedCol* cols, const RedMat* mats, int nmats, size_t height, size_t t0,
                   size_t count, const kb::EF* invd_a, const kb::EF* invd_b, const kb::EF& ya,
-                  const kb::EF& yb, bool has_b, kb::EF* ro, hipStream_t st);
+                  const kb::EF& yb, bool has_b, kb::EF* ro, hipStream_t st, int ncols = 0);
 uint32_t grind(const GrindState& gs, int bits, hipStream_t st);
 // One FRI commit-phase transcript step on the device (DuplexChallenger with an empty input
 // buffer): observe the 8-word root, duplex, sample an EF (pops out[7], out[6], out[5], out[4]).

@@ -550,20 +550,25 @@ void open_batch(std::vector<OpenDesc>& ds, int np, hipStream_t st) {
   }
   DBuf<OpenDesc> dd(ds.size());
   upload_async(dd.p, ds.data(), ds.size() * sizeof(OpenDesc), st);
+  double obytes = 0;  // the low coset's words + the weight tables read (16 B per row and point)
+  for (const OpenDesc& o : ds) obytes += (double)(o.height / 2) * (4.0 * o.w + 16.0 * np);
+  KernelProbe& probe = open_probe();
   DBuf<EF> partial(std::max<uint64_t>(part, 1));
   const uint32_t* twf = (const uint32_t*)twiddles().fwd.p;
   const int nd = (int)ds.size();
-  if (np == 2) {
+  hipEvent_t ev0 = probe.on ? probe.begin(st) : nullptr;
+  if (np == 2)
     hipLaunchKernelGGL(k_open_partial_batch<2>, dim3(chunks), dim3(OPEN_T), 0, st, dd.p, nd, twf,
                        partial.p);
-    KCHECK();
-    hipLaunchKernelGGL(k_open_final_batch<2>, dim3(cols), dim3(256), 0, st, dd.p, nd, partial.p);
-  } else {
+  else
     hipLaunchKernelGGL(k_open_partial_batch<1>, dim3(chunks), dim3(OPEN_T), 0, st, dd.p, nd, twf,
                        partial.p);
-    KCHECK();
+  KCHECK();
+  if (probe.on) probe.end(ev0, st, obytes);
+  if (np == 2)
+    hipLaunchKernelGGL(k_open_final_batch<2>, dim3(cols), dim3(256), 0, st, dd.p, nd, partial.p);
+  else
     hipLaunchKernelGGL(k_open_final_batch<1>, dim3(cols), dim3(256), 0, st, dd.p, nd, partial.p);
-  }
   KCHECK();
 }
 
@@ -572,11 +577,15 @@ void open_batch(std::vector<OpenDesc>& ds, int np, hipStream_t st) {
 #endif
 void reduce_range(const RedCol* cols, const RedMat* mats, int nmats, size_t height, size_t t0,
                   size_t count, const EF* invd_a, const EF* invd_b, const EF& ya, const EF& yb,
-                  bool has_b, EF* ro, hipStream_t st) {
+                  bool has_b, EF* ro, hipStream_t st, int ncols) {
   const unsigned grid = std::min<unsigned>(ceil_div(count, 256), BFZ_RED_GRID);
+  KernelProbe& probe = reduce_probe();
+  hipEvent_t ev0 = probe.on ? probe.begin(st) : nullptr;
   hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(256), 0, st, cols, mats, nmats, t0, t0 + count,
                      invd_a, invd_b, ya, yb, has_b ? 1 : 0, log2i(height), ro);
   KCHECK();
+  // the columns' words, the denominator tables read (one or two points) and ro written
+  if (probe.on) probe.end(ev0, st, (double)count * (4.0 * ncols + 16.0 * (has_b ? 3 : 2)));
 }
 
 void fri_challenge(uint32_t* state, const uint32_t* root, EF* beta, hipStream_t st) {

@@ -204,5 +204,7 @@ KernelProbe& ntt_probe();  // NTT kernels: k_ntt_r16 (8 B/element), k_lde_mid (1
 // Throughput Poseidon2 kernels (k_hash_leaves, k_compress, k_hash_rows8); "bytes" counts
 // permutations.
 KernelProbe& p2_probe();
+KernelProbe& open_probe();    // k_open_partial_batch: algorithmic bytes (fri.hip open_batch)
+KernelProbe& reduce_probe();  // k_reduce: algorithmic bytes (fri.hip reduce_range)
 
 }  // namespace bfz

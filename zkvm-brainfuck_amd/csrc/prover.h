@@ -84,6 +84,10 @@ struct StageTimes {          // milliseconds, measured with HIP events on the pr
   double p2_perms = 0;       // permutations they computed
   int p2_launches = 0;
   double lde_elem_stages = 0;  // iDFT n + DFT n on each coset half: 3 * n * log2(n) * w per call
+  double open_kernel_ms = 0, open_kernel_bytes = 0;  // k_open_partial_batch (algorithmic bytes)
+  int open_kernel_launches = 0;
+  double reduce_kernel_ms = 0, reduce_kernel_bytes = 0;  // k_reduce
+  int reduce_kernel_launches = 0;
 };
 
 std::unique_ptr<ProvingKey> setup(const std::string& program_src);

@@ -384,6 +384,10 @@ struct ProofScope {
     ntt_probe().on = ev.on;
     p2_probe().reset();
     p2_probe().on = ev.on;
+    open_probe().reset();
+    open_probe().on = ev.on;
+    reduce_probe().reset();
+    reduce_probe().on = ev.on;
     if (ev.on) e_total = ev.begin(stream());
   }
   void finish() {  // collects every event of the call into *tms
@@ -402,12 +406,26 @@ struct ProofScope {
     tms->p2_kernel_ms = p2.ms;
     tms->p2_perms = p2.bytes;
     tms->p2_launches = p2.launches;
+    KernelProbe& op = open_probe();
+    op.collect();
+    op.on = false;
+    tms->open_kernel_ms = op.ms;
+    tms->open_kernel_bytes = op.bytes;
+    tms->open_kernel_launches = op.launches;
+    KernelProbe& rp = reduce_probe();
+    rp.collect();
+    rp.on = false;
+    tms->reduce_kernel_ms = rp.ms;
+    tms->reduce_kernel_bytes = rp.bytes;
+    tms->reduce_kernel_launches = rp.launches;
   }
   ~ProofScope() {  // the pinned upload arena is rewound when the call is done
     (void)hipStreamSynchronize(stream());
     staging_reset();
     ntt_probe().on = false;
     p2_probe().on = false;
+    open_probe().on = false;
+    reduce_probe().on = false;
   }
 };
 
@@ -1010,14 +1028,16 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   htrace().mark("reduce descriptors");
   upload_async(red_cols_d.p, red_cols.data(), red_cols.size() * sizeof(RedCol), st);
   upload_async(red_mats_d.p, red_mats.data(), red_mats.size() * sizeof(RedMat), st);
-  for (const RedJob& j : red_jobs) {
+  for (size_t ji = 0; ji < red_jobs.size(); ji++) {
+    const RedJob& j = red_jobs[ji];
+    const size_t ncols = (ji + 1 < red_jobs.size() ? red_jobs[ji + 1].col0 : red_cols.size()) - j.col0;
     const size_t H = (size_t)1 << j.lh;
     const bool sh = plan.sharded(H);
     const size_t t0 = sh ? plan.row0(H) : 0, cnt = sh ? plan.blk(H) : H;
     DBuf<EF> r(cnt);
     const Invd& d = invd.at(j.lh);
     reduce_range(red_cols_d.p + j.col0, red_mats_d.p + j.mat0, j.nmats, H, t0, cnt, d.pa(),
-                 j.has_b ? d.pb() : nullptr, j.ya, j.yb, j.has_b, r.p - t0, st);
+                 j.has_b ? d.pb() : nullptr, j.ya, j.yb, j.has_b, r.p - t0, st, (int)ncols);
     ro.emplace(j.lh, std::move(r));
   }
   if (ev.on) ev.end(e3, st, &tms->open);

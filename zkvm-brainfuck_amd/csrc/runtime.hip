@@ -34,6 +34,16 @@ KernelProbe& p2_probe() {
   return *k;
 }
 
+KernelProbe& open_probe() {
+  static KernelProbe* k = new KernelProbe();
+  return *k;
+}
+
+KernelProbe& reduce_probe() {
+  static KernelProbe* k = new KernelProbe();
+  return *k;
+}
+
 // Pinned staging for the small host -> device uploads inside a proof.  A copy from pageable
 // memory is staged synchronously by the runtime and leaves the GPU idle until the host catches
 // up; from pinned memory it is a plain stream-ordered DMA.  The arena is rewound when a proof
