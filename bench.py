@@ -34,7 +34,7 @@ VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 # Full-rate-equivalent VALU lane-ops of one Poseidon2 permutation in k_permute_batch
 # (gfx950 ISA instruction mix, profiles/r02/poseidon2_isa_mix.txt).
 P2_UNITS_PER_PERM = 5133
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02", "pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03", "pmc_summary.json")
 
 
 # VALU units (full-rate lane-ops) per radix-2 element-stage of a 2^22 coset LDE, from the gfx950
@@ -80,7 +80,7 @@ def ntt_roofline(tm):
             "traffic": round(traffic) if traffic else None,
             "algorithmic_per_launch": round(alg_per_launch),
             "traffic_over_algorithmic": round(traffic / alg_per_launch, 3) if traffic else None,
-            "traffic_source": "profiles/r02/pmc_summary.json (FETCH_SIZE x2 + WRITE_SIZE per "
+            "traffic_source": "profiles/r03/pmc_summary.json (FETCH_SIZE x2 + WRITE_SIZE per "
                               "launch, scaled to this proof's launches)",
             "basis": "SURVEY 8(d): 12*n*w B per coset LDE (read n, write 2n) / NTT kernel time",
             "kernel": "coset LDE = k_ntt_tile<false,14> (iDFT stages 0-13) + k_lde_mid<L> (iDFT "
@@ -129,8 +129,9 @@ def poseidon2_roofline(tm):
 def openings_roofline(tm):
     """HBM roofline of the opening kernels, timed per launch with HIP events on the prover
     stream: k_open_partial_batch (barycentric sums over each matrix's low coset: 4 B per word +
-    16 B of weight table per row and point) and k_reduce (FRI reduced openings over the whole
-    LDE: 4 B per word + 16 B per row for each denominator table read and for ro written)."""
+    16 B per row and point for one weight table per LDE height) and k_reduce (FRI reduced
+    openings over the whole LDE: 4 B per word + 16 B per row for each denominator table read
+    and for ro written)."""
     out = {}
     for key, ms, nbytes, launches, kernel in (
             ("partial", tm.open_kernel_ms, tm.open_kernel_bytes, tm.open_kernel_launches,

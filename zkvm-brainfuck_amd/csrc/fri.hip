@@ -13,6 +13,8 @@
 
 #include "poseidon2.h"
 
+#include <algorithm>
+
 namespace bfz {
 
 using namespace kb;
@@ -550,8 +552,17 @@ void open_batch(std::vector<OpenDesc>& ds, int np, hipStream_t st) {
   }
   DBuf<OpenDesc> dd(ds.size());
   upload_async(dd.p, ds.data(), ds.size() * sizeof(OpenDesc), st);
-  double obytes = 0;  // the low coset's words + the weight tables read (16 B per row and point)
-  for (const OpenDesc& o : ds) obytes += (double)(o.height / 2) * (4.0 * o.w + 16.0 * np);
+  // algorithmic bytes: every matrix's low-coset words + one weight table (16 B per row and
+  // point) per LDE height (matrices of one height share it)
+  double obytes = 0;
+  std::vector<uint64_t> heights;
+  for (const OpenDesc& o : ds) {
+    obytes += (double)(o.height / 2) * 4.0 * o.w;
+    if (std::find(heights.begin(), heights.end(), o.height) == heights.end()) {
+      heights.push_back(o.height);
+      obytes += (double)(o.height / 2) * 16.0 * np;
+    }
+  }
   KernelProbe& probe = open_probe();
   DBuf<EF> partial(std::max<uint64_t>(part, 1));
   const uint32_t* twf = (const uint32_t*)twiddles().fwd.p;
