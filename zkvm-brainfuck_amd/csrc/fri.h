@@ -2,6 +2,7 @@
 #pragma once
 #include <vector>
 
+#include "challenger.h"
 #include "gpu.h"
 #include "merkle.h"
 
@@ -16,12 +17,6 @@ struct RedMat {            // the columns [first, first + count) of one matrix
   int has_b;               // opened at the second point too: coefficient there = kb * ca
   int pad;
   kb::EF kb;               // alpha^width
-};
-
-struct GrindState {        // DuplexChallenger state at grind time
-  uint32_t st[16];
-  uint32_t in[8];
-  int nin;
 };
 
 // out[t] = 1 / (x_t - z), x_t = 3 * w_H^bitrev(t), t < 2^logH
@@ -64,7 +59,15 @@ void open_batch(std::vector<OpenDesc>& ds, int np, hipStream_t st);
 void reduce_range(const RedCol* cols, const RedMat* mats, int nmats, size_t height, size_t t0,
                   size_t count, const kb::EF* invd_a, const kb::EF* invd_b, const kb::EF& ya,
                   const kb::EF& yb, bool has_b, kb::EF* ro, hipStream_t st, int ncols = 0);
-uint32_t grind(const GrindState& gs, int bits, hipStream_t st);
+// The transcript after the commit phase, on the device (prover.rs:470 open -> TwoAdicFriPcs
+// [p3-recalled]: observe the final constant, grind, sample the query indices) with no host round
+// trip.  c: the challenger, in device memory -- taken as is when fri_state is null (no FRI round),
+// otherwise rebuilt from the commit phase's sponge state (the last round's duplex, 4 outputs
+// left).  It ends as the host challenger would after the last query index.  res[0] = the smallest
+// witness w with sample_bits(bits) == 0 after observe(w), res[1] = 1 when the replayed check
+// holds; qidx[q] = sample_bits(log_max), q < nq.
+void fri_transcript_tail(DevChallenger* c, const uint32_t* fri_state, const kb::EF* fin, int bits,
+                         int nq, int log_max, uint32_t* qidx, uint32_t* res, hipStream_t st);
 // One FRI commit-phase transcript step on the device (DuplexChallenger with an empty input
 // buffer): observe the 8-word root, duplex, sample an EF (pops out[7], out[6], out[5], out[4]).
 // state: 16 words (Montgomery), updated in place; beta: EF written for the fold.
@@ -116,13 +119,13 @@ struct GatherSeg {
   int32_t own_shift;
   int32_t pad;
 };
-// out[q * words_per_query + ...] = the segments' words for qidx[q], segments in order; a segment
-// with base == nullptr is `count` literal words of value xr.  In a
-// sharded proof (shard != nullptr, world > 1) every rank writes the words it owns and one sum
-// all-reduce over the device buffer completes them.
-// Returns the nwords gathered words (canonical form) in a pinned host buffer that stays valid
-// until the next call.
-uint32_t* gather_queries(const std::vector<GatherSeg>& segs, const std::vector<uint32_t>& qidx,
-                         size_t& nwords, const ShardCtx* shard, hipStream_t st);
+// Words per query of a segment list.
+size_t query_words(const std::vector<GatherSeg>& segs);
+// out[q * query_words(segs) + ...] = the segments' words for qidx[q] (device), q < nq, segments
+// in order, canonical form; a segment with base == nullptr is `count` literal words of value xr.
+// In a sharded proof (shard != nullptr, world > 1) every rank writes the words it owns and one
+// sum all-reduce over the device buffer completes them.
+void gather_queries(const std::vector<GatherSeg>& segs, const uint32_t* qidx, int nq, uint32_t* out,
+                    const ShardCtx* shard, hipStream_t st);
 
 }  // namespace bfz

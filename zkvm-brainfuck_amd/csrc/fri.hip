@@ -451,26 +451,86 @@ __global__ __launch_bounds__(1024) void k_fri_tail(FriTailRounds a, const uint32
   if (threadIdx.x < 16) a.state[threadIdx.x] = stv;
 }
 
-// ------------------------------------------------------------------ grind
-// Challenger state: sponge state st[16], pending inputs in[0..nin).  observe(w) then
-// sample_bits(bits) == 0  <=>  perm(st with in[0..nin), w written at 0..nin)[7] low bits 0.
-__global__ __launch_bounds__(256) void k_grind(GrindState gs, uint32_t start, uint32_t bits,
+// ------------------------------------------------------------------ transcript tail
+// The challenger after the commit phase, then observe(final constant).  Also arms the grind's
+// result word (no candidate yet).
+__global__ __launch_bounds__(64) void k_fri_finish(DevChallenger* __restrict__ c,
+                                                   const uint32_t* __restrict__ fri_state,
+                                                   const EF* __restrict__ fin,
+                                                   uint32_t* __restrict__ res) {
+  LaneSponge sp;
+  if (fri_state) {  // after the last round's duplex and its beta (4 pops): out = st[0..8), 4 left
+    sp.lane = threadIdx.x & 15;
+    sp.kc = lane_consts(sp.lane);
+    sp.stv = fri_state[sp.lane];
+    sp.inv = 0;
+    sp.outv = sp.lane < 8 ? sp.stv : 0u;
+    sp.nin = 0;
+    sp.nout = 4;
+  } else {
+    sp.load(c);
+  }
+  const EF f = *fin;
+  for (int e = 0; e < 4; e++) sp.observe(f.c[e]);
+  sp.store(c);
+  if (threadIdx.x == 0) {
+    res[0] = 0xffffffffu;
+    res[1] = 0;
+  }
+}
+
+// Proof-of-work grind: observe(w) then sample_bits(bits) == 0  <=>  perm(st with in[0..nin),
+// w at nin)[7] has its low bits clear.  The grid scans the candidates chunk by chunk (chunk =
+// the grid's thread count) in order; a thread leaves once the best witness lies in a chunk it
+// has finished, so every thread has covered every chunk up to the smallest witness's and the
+// atomicMin result is that witness (the normal form).  Every thread reaches the exit: a witness
+// turns up with probability 1 - e^-2 per 2^(bits+1)-candidate chunk, and the scan ends at P.
+__global__ __launch_bounds__(256) void k_grind(const DevChallenger* __restrict__ c, uint32_t bits,
                                                uint32_t* __restrict__ best) {
-  const uint32_t w = start + blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= P) return;
-  uint32_t s[16];
+  uint32_t s0[16];
+  const int nin = c->nin;
 #pragma unroll
-  for (int i = 0; i < 16; i++) s[i] = gs.st[i];
-#pragma unroll
-  for (int i = 0; i < 8; i++)
-    if (i < gs.nin) s[i] = gs.in[i];
-  const uint32_t wm = to_mont(w);
+  for (int i = 0; i < 16; i++) s0[i] = c->st[i];
 #pragma unroll
   for (int i = 0; i < 8; i++)
-    if (i == gs.nin) s[i] = wm;
-  poseidon2_permute(s);
-  const uint32_t v = from_mont(s[7]);
-  if ((v & ((1u << bits) - 1)) == 0) atomicMin(best, w);
+    if (i < nin) s0[i] = c->in[i];
+  const uint32_t stride = gridDim.x * blockDim.x;
+  const uint32_t mask = (1u << bits) - 1;
+  for (uint32_t base = 0; base < P; base += stride) {
+    const uint32_t w = base + blockIdx.x * blockDim.x + threadIdx.x;
+    if (w < P) {
+      uint32_t s[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++) s[i] = s0[i];
+      const uint32_t wm = to_mont(w);
+#pragma unroll
+      for (int i = 0; i < 8; i++)
+        if (i == nin) s[i] = wm;
+      poseidon2_permute(s);
+      if ((from_mont(s[7]) & mask) == 0) atomicMin(best, w);
+    }
+    const uint32_t b = __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((uint64_t)b < (uint64_t)base + stride) break;
+  }
+}
+
+// observe(witness), the witness check, then the query indices; the challenger is stored back.
+__global__ __launch_bounds__(64) void k_sample_queries(DevChallenger* __restrict__ c, int bits,
+                                                       int nq, int log_max,
+                                                       uint32_t* __restrict__ qidx,
+                                                       uint32_t* __restrict__ res) {
+  LaneSponge sp;
+  sp.load(c);
+  const uint32_t w = res[0];
+  sp.observe(to_mont(w));
+  const uint32_t v = from_mont(sp.sample()) & ((1u << bits) - 1);
+  const uint32_t qmask = (uint32_t)(((uint64_t)1 << log_max) - 1);
+  for (int q = 0; q < nq; q++) {
+    const uint32_t x = from_mont(sp.sample()) & qmask;
+    if (threadIdx.x == 0) qidx[q] = x;
+  }
+  sp.store(c);
+  if (threadIdx.x == 0) res[1] = (w < P && v == 0) ? 1u : 0u;
 }
 
 // ------------------------------------------------------------------ query gather
@@ -638,27 +698,31 @@ void fri_tail_rounds(const FriTailRounds& a, hipStream_t st) {
   KCHECK();
 }
 
-uint32_t grind(const GrindState& gs, int bits, hipStream_t st) {
-  DBuf<uint32_t> best(1);
-  // 2^(bits+2) candidates per launch: a witness exists in the first chunk with probability
-  // 1 - e^-4, and chunks are scanned in order so the first hit is the smallest witness.
-  const uint32_t chunk = 1u << std::min(22, std::max(16, bits + 2));
-  for (uint64_t start = 0; start < P; start += chunk) {
-    HIP_CHECK(hipMemsetAsync(best.p, 0xff, 4, st));  // no candidate yet
-    hipLaunchKernelGGL(k_grind, dim3(chunk / 256), dim3(256), 0, st, gs, (uint32_t)start,
-                       (uint32_t)bits, best.p);
-    KCHECK();
-    uint32_t h = 0;
-    fetch(&h, best.p, 4, st);
-    if (h != 0xffffffffu) return h;
-  }
-  throw std::runtime_error("grind: no witness");
+void fri_transcript_tail(DevChallenger* c, const uint32_t* fri_state, const EF* fin, int bits,
+                         int nq, int log_max, uint32_t* qidx, uint32_t* res, hipStream_t st) {
+  if (bits < 0 || bits > 30 || log_max < 0 || log_max > 31 || nq < 0)
+    throw std::runtime_error("fri_transcript_tail: bad parameters");
+  hipLaunchKernelGGL(k_fri_finish, dim3(1), dim3(64), 0, st, c, fri_state, fin, res);
+  KCHECK();
+  // 2^(bits+1) candidates per chunk (2^17 at 16 bits: the first chunk holds a witness with
+  // probability 1 - e^-2; a further chunk costs ~10 us and no round trip, where 2^18 per chunk
+  // took 31 us)
+  const uint32_t chunk = 1u << std::min(22, std::max(16, bits + 1));
+  hipLaunchKernelGGL(k_grind, dim3(chunk / 256), dim3(256), 0, st, (const DevChallenger*)c,
+                     (uint32_t)bits, res);
+  KCHECK();
+  hipLaunchKernelGGL(k_sample_queries, dim3(1), dim3(64), 0, st, c, bits, nq, log_max, qidx, res);
+  KCHECK();
 }
 
-// The gathered words land in a pinned host buffer (grown on demand, reused by every proof):
-// the device-to-host copy is a plain DMA instead of a runtime staging through pageable memory.
-uint32_t* gather_queries(const std::vector<GatherSeg>& segs, const std::vector<uint32_t>& qidx,
-                         size_t& nwords, const ShardCtx* shard, hipStream_t st) {
+size_t query_words(const std::vector<GatherSeg>& segs) {
+  size_t w = 0;
+  for (const GatherSeg& g : segs) w += g.count;
+  return w;
+}
+
+void gather_queries(const std::vector<GatherSeg>& segs, const uint32_t* qidx, int nq, uint32_t* out,
+                    const ShardCtx* shard, hipStream_t st) {
   const int rank = shard ? shard->rank : 0;
   std::vector<uint32_t> off(segs.size());
   uint32_t wpq = 0;
@@ -666,32 +730,21 @@ uint32_t* gather_queries(const std::vector<GatherSeg>& segs, const std::vector<u
     off[s] = wpq;
     wpq += segs[s].count;
   }
-  nwords = (size_t)wpq * qidx.size();
-  if (!nwords) return nullptr;
-  static uint32_t* host = nullptr;
-  static size_t cap = 0;
-  if (nwords > cap) {  // no copy into it is pending: every proof ends with a synchronize
-    if (host) HIP_CHECK(hipHostFree(host));
-    cap = nwords + nwords / 4;
-    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host), cap * 4, hipHostMallocDefault));
-  }
+  const size_t nwords = (size_t)wpq * nq;
+  if (!nwords) return;
   DBuf<GatherSeg> dseg(segs.size());
-  DBuf<uint32_t> doff(off.size()), dq(qidx.size()), dout(nwords);
+  DBuf<uint32_t> doff(off.size());
   upload_async(dseg.p, segs.data(), segs.size() * sizeof(GatherSeg), st);
   upload_async(doff.p, off.data(), off.size() * 4, st);
-  upload_async(dq.p, qidx.data(), qidx.size() * 4, st);
-  const size_t nthreads = segs.size() * qidx.size();
+  const size_t nthreads = segs.size() * (size_t)nq;
   hipLaunchKernelGGL(k_gather_segs, dim3(ceil_div(nthreads, 256)), dim3(256), 0, st,
                      (const GatherSeg*)dseg.p, (int)segs.size(), (const uint32_t*)doff.p, wpq,
-                     (const uint32_t*)dq.p, (int)qidx.size(), rank, dout.p);
+                     qidx, nq, rank, out);
   KCHECK();
   if (shard && shard->world > 1) {  // owner-masked words: one sum all-reduce, device to device
     HIP_CHECK(hipStreamSynchronize(st));
-    shard->allreduce_sum_u32(dout.p, nwords);
+    shard->allreduce_sum_u32(out, nwords);
   }
-  HIP_CHECK(hipMemcpyAsync(host, dout.p, nwords * 4, hipMemcpyDeviceToHost, st));
-  spin_sync(st);  // host is pinned already
-  return host;
 }
 
 }  // namespace bfz

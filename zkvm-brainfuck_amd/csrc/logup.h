@@ -1,5 +1,6 @@
 // Device LogUp permutation trace (see logup.hip).
 #pragma once
+#include "challenger.h"
 #include "air.h"
 #include "gpu.h"
 #include "machine.h"
@@ -16,19 +17,11 @@ struct PermChallenges {
 // ch: DEVICE memory (the prover samples the challenges on the device, challenge_perm).
 void perm_trace(int chip, const uint32_t* mainc, const uint32_t* prepc, size_t n,
                 const PermChallenges* ch, uint32_t* perm, kb::EF* cumsum_dev, hipStream_t st);
-// Device transcript step after the main commit: the DuplexChallenger state `ch` (host layout,
-// device memory) observes the 8-word root and samples the LogUp alpha and beta (prover.rs:
-// 269-272); out receives alpha and beta^0..7.  The host replays the same step when it fetches
-// the root later, so its transcript stays in step.
-struct DevChallenger {
-  uint32_t st[16];
-  uint32_t in[8];
-  int32_t nin;
-  uint32_t out[8];
-  int32_t nout;
-};
-void challenge_perm(const DevChallenger* ch, const uint32_t* root, PermChallenges* out,
-                    hipStream_t st);
+// Device transcript step after the main commit: the DuplexChallenger state `ch` (device
+// memory, updated in place) observes the 8-word root and samples the LogUp alpha and beta
+// (prover.rs:269-272); out receives alpha and beta^0..7.  The host replays the same step when
+// it fetches the root later, so its transcript stays in step.
+void challenge_perm(DevChallenger* ch, const uint32_t* root, PermChallenges* out, hipStream_t st);
 
 void ef_inclusive_scan(kb::EF* data, size_t n, hipStream_t st);
 

@@ -249,36 +249,16 @@ __global__ __launch_bounds__(256) void k_write_phi(const EF* __restrict__ local,
   if (t == n - 1) *cumsum = v;
 }
 
-// One 16-lane row runs the DuplexChallenger of prover.hip (Challenger) on the device: lane l
-// holds state word l, lanes 0..7 the input and output buffers; nin / nout are uniform.
-__global__ __launch_bounds__(64) void k_challenge_perm(const DevChallenger* __restrict__ c,
+// The LogUp challenges on the device (challenger.h): observe the main root, sample alpha, beta.
+__global__ __launch_bounds__(64) void k_challenge_perm(DevChallenger* __restrict__ c,
                                                        const uint32_t* __restrict__ root,
                                                        PermChallenges* __restrict__ out) {
-  const int lane = threadIdx.x & 15;
-  const LaneConsts kc = lane_consts(lane);
-  uint32_t stv = c->st[lane], inv = lane < 8 ? c->in[lane] : 0u, outv = lane < 8 ? c->out[lane] : 0u;
-  int nin = c->nin, nout = c->nout;
-  auto duplex = [&]() {
-    if (lane < nin) stv = inv;
-    stv = poseidon2_permute_lane(stv, lane, kc);
-    outv = stv;
-    nout = 8;
-    nin = 0;
-  };
-  auto observe = [&](uint32_t v) {
-    nout = 0;
-    if (lane == nin) inv = v;
-    if (++nin == 8) duplex();
-  };
-  auto sample = [&]() {
-    if (nin > 0 || nout == 0) duplex();
-    --nout;
-    return (uint32_t)__shfl(outv, nout, 16);
-  };
-  for (int i = 0; i < 8; i++) observe(root[i]);
-  EF alpha, beta;
-  for (int e = 0; e < 4; e++) alpha.c[e] = sample();
-  for (int e = 0; e < 4; e++) beta.c[e] = sample();
+  LaneSponge sp;
+  sp.load(c);
+  for (int i = 0; i < 8; i++) sp.observe(root[i]);
+  const EF alpha = sp.sample_ef();
+  const EF beta = sp.sample_ef();
+  sp.store(c);
   if (threadIdx.x == 0) {
     out->alpha = alpha;
     EF p = ef_one();
@@ -289,8 +269,7 @@ __global__ __launch_bounds__(64) void k_challenge_perm(const DevChallenger* __re
   }
 }
 
-void challenge_perm(const DevChallenger* ch, const uint32_t* root, PermChallenges* out,
-                    hipStream_t st) {
+void challenge_perm(DevChallenger* ch, const uint32_t* root, PermChallenges* out, hipStream_t st) {
   hipLaunchKernelGGL(k_challenge_perm, dim3(1), dim3(64), 0, st, ch, root, out);
   KCHECK();
 }

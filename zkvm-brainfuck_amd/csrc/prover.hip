@@ -95,7 +95,8 @@ struct FriTail {
   const uint32_t* state;
   const EF* fin;
 };
-// packed = [root 0 .. root MAX-1 (8 words each) | state (16) | final layer (2 EF)]
+// packed = [root 0 .. root MAX-1 (8 words each) | state (16) | final layer (2 EF)]; nroots may
+// be 0 (state then unused)
 __global__ void k_pack_fri_tail(FriTail t, uint32_t* __restrict__ packed) {
   const int i = threadIdx.x;
   if (i < 8 * t.nroots) packed[i] = t.root[i >> 3][i & 7];
@@ -105,16 +106,32 @@ __global__ void k_pack_fri_tail(FriTail t, uint32_t* __restrict__ packed) {
 
 namespace {
 // BFZ_HOST_TRACE=1: host timestamps (us since the last mark 0) at the transcript points of each
-// proof on stderr -- splits the GPU's idle gaps into host work and launch latency.
+// proof, printed on stderr at exit -- splits the GPU's idle gaps into host work and launch
+// latency (scripts/hostgap.py).  The marks are kept in memory: an fprintf per mark cost tens
+// of microseconds on the GPU boxes and doubled the idle time it was measuring.
 struct HostTrace {
   bool on = std::getenv("BFZ_HOST_TRACE") != nullptr;
-  std::chrono::steady_clock::time_point t0;
+  struct Mark {
+    std::chrono::steady_clock::time_point t;
+    const char* what;  // string literals only
+    bool reset;
+  };
+  std::vector<Mark> marks;
+  HostTrace() {
+    if (on) marks.reserve(1 << 16);
+  }
   void mark(const char* what, bool reset = false) {
-    if (!on) return;
-    const auto now = std::chrono::steady_clock::now();
-    if (reset) t0 = now;
-    std::fprintf(stderr, "host %9.1f %s (abs %.1f)\n", std::chrono::duration<double, std::micro>(now - t0).count(), what,
-                 std::chrono::duration<double, std::micro>(now.time_since_epoch()).count());
+    if (!on || marks.size() >= (1u << 20)) return;
+    marks.push_back({std::chrono::steady_clock::now(), what, reset});
+  }
+  ~HostTrace() {
+    std::chrono::steady_clock::time_point t0{};
+    for (const Mark& m : marks) {
+      if (m.reset) t0 = m.t;
+      std::fprintf(stderr, "host %9.1f %s (abs %.1f)\n",
+                   std::chrono::duration<double, std::micro>(m.t - t0).count(), m.what,
+                   std::chrono::duration<double, std::micro>(m.t.time_since_epoch()).count());
+    }
   }
 };
 HostTrace& htrace() {
@@ -377,7 +394,6 @@ struct ProofScope {
   StageTimes local;
   StageTimes* tms;
   hipEvent_t e_total = nullptr;
-  std::vector<std::vector<EF>> keep;  // host buffers of async uploads live until the end
   ProofScope(bool timing, StageTimes* times) : tms(times ? times : &local) {
     ev.on = timing && times;
     ntt_probe().reset();
@@ -541,7 +557,6 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   hipStream_t st = stream();
   EvTimer& ev = ps.ev;
   StageTimes* tms = ps.tms;
-  std::vector<std::vector<EF>>& keep = ps.keep;
   DeviceTraces& dt = md.dt;
   const std::vector<int>& order = md.order;
   const std::vector<int>& chip = md.chip;
@@ -553,40 +568,31 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
 
   // ---- open (prover.rs:242-553), on a clone of the challenger (prover.rs:578)
   htrace().mark("open start");
-  PermChallenges pc;
-  EF perm_alpha;
-  auto host_perm_challenges = [&]() {  // prover.rs:265-272
-    ch.observe_digest(mainr.tree.root);
-    perm_alpha = ch.sample_ef();
-    const EF perm_beta = ch.sample_ef();
-    pc.alpha = perm_alpha;
-    pc.beta_pows[0] = ef_one();
-    for (int j = 1; j < 8; j++) pc.beta_pows[j] = ef_mul(pc.beta_pows[j - 1], perm_beta);
-  };
-  DBuf<PermChallenges> pc_d(1);
-  if (md.root_on_host) {
-    host_perm_challenges();
-    upload_async(pc_d.p, &pc, sizeof(pc), st);
-  } else {  // the root is still on the device: the same transcript step runs there, and the host
-            // replays it when the root comes back with the cumulative sums (no round trip here)
+  // The transcript steps up to zeta run on the device (challenger.h): the LogUp challenges after
+  // the main root and the quotient challenge after the permutation root, so neither stage waits
+  // for a host round trip.  The host fetches the three roots and the cumulative sums once, after
+  // the quotient commit, and replays the same steps before sampling zeta.
+  DBuf<DevChallenger> dc_d(1);
+  {
     DevChallenger dc;
     std::memcpy(dc.st, ch.st, sizeof(dc.st));
     std::memcpy(dc.in, ch.in, sizeof(dc.in));
     std::memcpy(dc.out, ch.out, sizeof(dc.out));
     dc.nin = ch.nin;
     dc.nout = ch.nout;
-    DBuf<DevChallenger> dc_d(1);
     upload_async(dc_d.p, &dc, sizeof(dc), st);
-    challenge_perm(dc_d.p, mainr.tree.layers.back().p, pc_d.p, st);
   }
+  DBuf<PermChallenges> pc_d(1);
+  challenge_perm(dc_d.p, mainr.tree.layers.back().p, pc_d.p, st);  // prover.rs:265-272
   htrace().mark("perm challenges");
 
   hipEvent_t e1 = ev.on ? ev.begin(st) : nullptr;
   Round permr;
   permr.mats.resize(nc);
-  DBuf<EF> cums_d(nc + 2);  // + the main root (8 words) when it is fetched with the sums
-  if (!md.root_on_host)
-    HIP_CHECK(hipMemcpyAsync(cums_d.p + nc, mainr.tree.layers.back().p, 32, hipMemcpyDeviceToDevice, st));
+  // cums_d: the chips' cumulative sums, then (fetched together before zeta) the main,
+  // permutation and quotient roots, 2 EF slots (8 words) each
+  DBuf<EF> cums_d(nc + 6);
+  HIP_CHECK(hipMemcpyAsync(cums_d.p + nc, mainr.tree.layers.back().p, 32, hipMemcpyDeviceToDevice, st));
   for (int k = 0; k < nc; k++) {
     const int c = chip[k];
     const int pw = perm_width(c);
@@ -598,46 +604,25 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     if (k == 0) htrace().mark("perm_rows launched");
     lde_into(permr.mats[k], pe.p, hn[k], 4 * pw, ONE, st, &ev, tms, &plan, &chip_next_cols(c).perm);
   }
-  permr.commit(st);
-  std::vector<EF> cums(nc + 2);
-  fetch(cums.data(), cums_d.p, (md.root_on_host ? nc : nc + 2) * sizeof(EF), st);
-  htrace().mark("cums fetched");
-  if (!md.root_on_host) {
-    std::memcpy(mainr.tree.root, &cums[nc], 32);
-    md.root_on_host = true;
-    host_perm_challenges();
-  }
-  cums.resize(nc);
+  permr.commit(st, /*fetch_root=*/false);
   if (ev.on) ev.end(e1, st, &tms->perm);
-  ch.observe_digest(permr.tree.root);
-  for (int k = 0; k < nc; k++) ch.observe_ef(cums[k]);
-  const EF alpha = ch.sample_ef();
-  htrace().mark("quotient challenge");
+  HIP_CHECK(hipMemcpyAsync(cums_d.p + nc + 2, permr.tree.layers.back().p, 32, hipMemcpyDeviceToDevice, st));
 
   // ---- quotient (prover.rs:344-412)
   hipEvent_t e2 = ev.on ? ev.begin(st) : nullptr;
   Round quotr;
   quotr.mats.resize(2 * nc);
   std::vector<DBuf<EF>> apows(nc);
-  std::vector<DBuf<uint32_t>> qv(nc);  // Q on 3 H_2n: 2 chunks x 4 columns of n rows
+  std::vector<QuotParams> qph(nc);  // the challenge-independent fields; the rest on the device
+  DBuf<QuotParams> qp_d(std::max(nc, 1));
+  QuotAlphaTargets tg{};
   for (int k = 0; k < nc; k++) {
-    const int c = chip[k];
     const size_t n = hn[k];
-    const int logn = log2i(n);
-    const int K = num_constraints(c);
-    keep.emplace_back(K);
-    std::vector<EF>& ap = keep.back();
-    EF p = ef_one();
-    for (int j = K - 1; j >= 0; j--) {
-      ap[j] = p;
-      p = ef_mul(p, alpha);
-    }
+    const int K = num_constraints(chip[k]);
     apows[k].reset(K);
-    upload_async(apows[k].p, ap.data(), K * sizeof(EF), st);
-    QuotParams qp;
-    qp.perm_alpha = perm_alpha;
-    for (int j = 0; j < 8; j++) qp.beta_pows[j] = pc.beta_pows[j];
-    qp.cumsum = cums[k];
+    tg.apows[k] = apows[k].p;
+    tg.K[k] = K;
+    QuotParams& qp = qph[k];
     qp.alpha_pows = apows[k].p;
     const uint32_t three = to_mont(3);
     const uint32_t sn = mpow(three, n);
@@ -645,8 +630,19 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     qp.zh_odd = msub(mneg(sn), ONE);
     qp.zh_even_inv = minv(qp.zh_even);
     qp.zh_odd_inv = minv(qp.zh_odd);
-    qp.wn_inv = minv(two_adic_gen(logn));
+    qp.wn_inv = minv(two_adic_gen(log2i(n)));
     qp.shift = three;
+  }
+  upload_async(qp_d.p, qph.data(), nc * sizeof(QuotParams), st);
+  challenge_quot(dc_d.p, permr.tree.layers.back().p, cums_d.p, nc, pc_d.p, qp_d.p, tg, st);
+  htrace().mark("quotient challenge");
+  std::vector<DBuf<uint32_t>> qv(nc);  // Q on 3 H_2n: 2 chunks x 4 columns of n rows
+  for (int k = 0; k < nc; k++) {
+    const int c = chip[k];
+    const size_t n = hn[k];
+    const int logn = log2i(n);
+    const uint32_t three = to_mont(3);
+    const QuotParams& qp = qph[k];
     const int pi = pk.idx_of_chip[c];
     const uint32_t* prep_lde = pi >= 0 ? pk.prep.mats[pi].lde.buf.p : nullptr;
     const CMat& mm = mainr.mats[k];
@@ -676,7 +672,8 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
       QuotRows in{mm.lde.buf.p, mm.lde.buf.p, pm.lde.buf.p, pm.lde.buf.p, prep_lde, N, 0, N, {}, {}};
       for (int j = 0; j < 64; j++) in.nmain[j] = in.nperm[j] = (uint8_t)j;
       quotient_into(c, in, logn + 1, qp,
-                    QuotOut{{quotr.mats[2 * k].lde.buf.p, quotr.mats[2 * k + 1].lde.buf.p + n}, N}, st);
+                    QuotOut{{quotr.mats[2 * k].lde.buf.p, quotr.mats[2 * k + 1].lde.buf.p + n}, N}, st,
+                    qp_d.p + k);
       continue;
     }
     // sharded: this rank's points only; next rows from the next-residue shards
@@ -685,7 +682,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
                 mm.stride(), mm.row0, mm.blk, {}, {}};
     std::copy(mm.nmap.begin(), mm.nmap.end(), in.nmain);
     std::copy(pm.nmap.begin(), pm.nmap.end(), in.nperm);
-    quotient_rows(c, in, logn + 1, qp, qv[k].p, st);
+    quotient_rows(c, in, logn + 1, qp, qv[k].p, st, qp_d.p + k);
   }
   if (plan.on()) gather_quotients(mainr, hn, qv, plan, *shard, st);
   for (int k = 0; k < nc; k++) {  // the next-row shards are done with
@@ -717,11 +714,27 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     }
   }
   qv.clear();
-  quotr.commit(st);
+  quotr.commit(st, /*fetch_root=*/false);
   if (ev.on) ev.end(e2, st, &tms->quotient);
+  HIP_CHECK(hipMemcpyAsync(cums_d.p + nc + 4, quotr.tree.layers.back().p, 32, hipMemcpyDeviceToDevice, st));
+  std::vector<EF> cums(nc + 6);
+  fetch(cums.data(), cums_d.p, (nc + 6) * sizeof(EF), st);
+  htrace().mark("roots fetched");
+  std::memcpy(mainr.tree.root, &cums[nc], 32);
+  std::memcpy(permr.tree.root, &cums[nc + 2], 32);
+  std::memcpy(quotr.tree.root, &cums[nc + 4], 32);
+  md.root_on_host = true;
+  cums.resize(nc);
+  // the host transcript replays the device steps (prover.rs:265-272, 336-342, 413-416)
+  ch.observe_digest(mainr.tree.root);
+  (void)ch.sample_ef();  // LogUp alpha
+  (void)ch.sample_ef();  // LogUp beta
+  ch.observe_digest(permr.tree.root);
+  for (int k = 0; k < nc; k++) ch.observe_ef(cums[k]);
+  (void)ch.sample_ef();  // quotient alpha
   ch.observe_digest(quotr.tree.root);
-  htrace().mark("quotient root fetched");
   const EF zeta = ch.sample_ef();
+  htrace().mark("zeta");
 
   // ---- PCS open: opened values (prover.rs:417-470)
   hipEvent_t e3 = ev.on ? ev.begin(st) : nullptr;
@@ -1169,56 +1182,18 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     len = h;
   }
   flush_fold();
-  // one device-to-host copy for the commit-phase roots, the transcript state and the final
-  // layer (small copies each cost a copy-kernel launch)
   const int nt = (int)trees.size();
   if (nt > MAX_FRI_ROUNDS) throw std::runtime_error("FRI: too many rounds");
-  FriTail tail{};
-  for (int i = 0; i < nt; i++) tail.root[i] = trees[i].layers.back().p;
-  tail.nroots = nt;
-  tail.state = dstate.p;
-  tail.fin = layers.back().v.p;
-  DBuf<uint32_t> packed(8 * MAX_FRI_ROUNDS + 16 + 8);
-  hipLaunchKernelGGL(k_pack_fri_tail, dim3(1), dim3(256), 0, st, tail, packed.p);
-  KCHECK();
-  std::vector<uint32_t> hp(packed.n);
-  fetch(hp.data(), packed.p, packed.n * 4, st);
-  htrace().mark("fri tail fetched");
-  for (int i = 0; i < nt; i++) std::memcpy(trees[i].root, &hp[8 * i], 32);
-  uint32_t st_after[16];
-  std::memcpy(st_after, &hp[8 * MAX_FRI_ROUNDS], 64);
-  EF fin[2];
-  std::memcpy(fin, &hp[8 * MAX_FRI_ROUNDS + 16], sizeof(fin));
-  if (!trees.empty()) {  // host challenger = state after the last round's duplex, 4 outputs left
-    for (int i = 0; i < 16; i++) ch.st[i] = st_after[i];
-    for (int i = 0; i < 8; i++) ch.out[i] = st_after[i];
-    ch.nout = 4;
-    ch.nin = 0;
-  }
-  if (!ef_eq(fin[0], fin[1]) && !(shard && shard->solo))
-    throw std::runtime_error("FRI: final polynomial is not constant (trace violates the AIR)");
-  ch.observe_ef(fin[0]);
-  GrindState gs;
-  for (int i = 0; i < 16; i++) gs.st[i] = ch.st[i];
-  for (int i = 0; i < 8; i++) gs.in[i] = ch.in[i];
-  gs.nin = ch.nin;
-  htrace().mark("grind");
-  const uint32_t witness = grind(gs, POW_BITS, st);
-  htrace().mark("grind done");
-  if (!ch.check_witness(POW_BITS, witness)) throw std::runtime_error("grind: bad witness");
   const int nq = opt.num_queries;
-  std::vector<uint32_t> qidx(nq);
-  for (int q = 0; q < nq; q++) qidx[q] = ch.sample_bits(Lmax);
-  if (after) *after = ch;  // the transcript is complete: MachineProver::open's &mut challenger
 
-  // ---- query openings: gather every opened word in proof order
+  // ---- query openings: every opened word in proof order
   // Opening segments in serialization order (same for every query; see GatherSeg).
   auto owner_shift = [](const MerkleTree& t, int L) {  // layer L of a sharded tree
     const int nl = (int)t.layers.size() - 1;
     return L < t.sharded_below ? nl - L - t.shard_log : -1;
   };
   std::vector<GatherSeg> segs;
-  const int ncommit = (int)trees.size();
+  const int ncommit = nt;
   // The segments follow the serialized query layout, its length words included as literal
   // segments (base == nullptr: count words of value xr), so the gathered words are the query
   // section of the proof as is.
@@ -1250,9 +1225,68 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
       segs.push_back({trees[i].layers[L].p, 1, (uint32_t)(i + 1 + L), 1, 8, 8,
                       owner_shift(trees[i], L), 0});
   }
-  size_t nwords = 0;
-  uint32_t* words = gather_queries(segs, qidx, nwords, shard, st);
+  const size_t nwords = query_words(segs) * (size_t)nq;
+
+  // ---- the transcript tail on the device: observe the final constant, grind, sample the
+  // query indices (fri_transcript_tail), then the gather; one device-to-host copy returns the
+  // commit-phase roots, the final layer, the challenger, the witness and the query words.
+  // tail = [roots (8 MAX_FRI_ROUNDS) | FRI state (16) | final layer (8) | challenger | witness,
+  //         ok | qidx (nq) | query words]
+  constexpr size_t T_CH = 8 * MAX_FRI_ROUNDS + 16 + 8;
+  constexpr size_t T_RES = T_CH + sizeof(DevChallenger) / 4;
+  constexpr size_t T_Q = T_RES + 2;
+  static_assert(sizeof(DevChallenger) % 4 == 0, "DevChallenger: whole words");
+  const size_t T_W = T_Q + (size_t)nq, tail_n = T_W + nwords;
+  DBuf<uint32_t> tailbuf(tail_n);
+  DevChallenger* dch = reinterpret_cast<DevChallenger*>(tailbuf.p + T_CH);
+  if (!nt) {  // no commit-phase round: the host challenger as it stands
+    DevChallenger hc;
+    std::memcpy(hc.st, ch.st, 64);
+    std::memcpy(hc.in, ch.in, 32);
+    std::memcpy(hc.out, ch.out, 32);
+    hc.nin = ch.nin;
+    hc.nout = ch.nout;
+    upload_async(dch, &hc, sizeof(hc), st);
+  }
+  FriTail tail{};
+  for (int i = 0; i < nt; i++) tail.root[i] = trees[i].layers.back().p;
+  tail.nroots = nt;
+  tail.state = dstate.p;
+  tail.fin = layers.back().v.p;
+  hipLaunchKernelGGL(k_pack_fri_tail, dim3(1), dim3(256), 0, st, tail, tailbuf.p);
+  KCHECK();
+  htrace().mark("grind");
+  fri_transcript_tail(dch, nt ? dstate.p : nullptr, layers.back().v.p, POW_BITS, nq, Lmax,
+                      tailbuf.p + T_Q, tailbuf.p + T_RES, st);
+  gather_queries(segs, tailbuf.p + T_Q, nq, tailbuf.p + T_W, shard, st);
+  static uint32_t* tbox = nullptr;  // pinned: the tail of the proof
+  static size_t tcap = 0;
+  if (tail_n > tcap) {  // no copy into it is pending: every proof waits for its tail
+    if (tbox) HIP_CHECK(hipHostFree(tbox));
+    tcap = tail_n + tail_n / 4;
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&tbox), tcap * 4, hipHostMallocDefault));
+  }
+  HIP_CHECK(hipMemcpyAsync(tbox, tailbuf.p, tail_n * 4, hipMemcpyDeviceToHost, st));
+  spin_sync(st);
   htrace().mark("queries gathered");
+  for (int i = 0; i < nt; i++) std::memcpy(trees[i].root, &tbox[8 * i], 32);
+  EF fin[2];
+  std::memcpy(fin, &tbox[8 * MAX_FRI_ROUNDS + 16], sizeof(fin));
+  if (!ef_eq(fin[0], fin[1]) && !(shard && shard->solo))
+    throw std::runtime_error("FRI: final polynomial is not constant (trace violates the AIR)");
+  const uint32_t witness = tbox[T_RES];
+  if (tbox[T_RES + 1] != 1) throw std::runtime_error("grind: bad witness");
+  {  // the host challenger = the device's after the last query index
+    DevChallenger dc;
+    std::memcpy(&dc, &tbox[T_CH], sizeof(dc));
+    std::memcpy(ch.st, dc.st, 64);
+    std::memcpy(ch.in, dc.in, 32);
+    std::memcpy(ch.out, dc.out, 32);
+    ch.nin = dc.nin;
+    ch.nout = dc.nout;
+  }
+  if (after) *after = ch;  // the transcript is complete: MachineProver::open's &mut challenger
+  const uint32_t* words = tbox + T_W;
   if (ev.on) ev.end(e4, st, &tms->fri);
 
   // ---- serialize (BFZ1 normal form)

@@ -2,6 +2,7 @@
 #pragma once
 #include "gpu.h"
 #include "machine.h"
+#include "logup.h"
 
 namespace bfz {
 
@@ -35,8 +36,9 @@ struct QuotRows {
   size_t stride, t0, count;
   uint8_t nmain[64], nperm[64];  // column c's next row: main_n / perm_n column nmain[c] / nperm[c]
 };
+// qp_dev: the same parameters in device memory (nullptr: qp is uploaded for the launch).
 void quotient_rows(int chip, const QuotRows& in, int logN, const QuotParams& qp, uint32_t* qout,
-                   hipStream_t st);
+                   hipStream_t st, const QuotParams* qp_dev = nullptr);
 // Output placement: chunk k's coefficient column e at chunk[k] + e * stride (row = position
 // within the chunk).  qout above is {qout, qout + 4n}, stride n; the single-GPU prover writes
 // each chunk straight into its own half of the chunk's LDE buffer ({lde0, lde1 + n}, stride 2n).
@@ -45,6 +47,18 @@ struct QuotOut {
   size_t stride;
 };
 void quotient_into(int chip, const QuotRows& in, int logN, const QuotParams& qp, const QuotOut& out,
-                   hipStream_t st);
+                   hipStream_t st, const QuotParams* qp_dev = nullptr);
+// The quotient challenge on the device after the LogUp commit (see k_challenge_quot): ch is the
+// device sponge (updated), root the permutation root, cums the chips' cumulative sums, pc the
+// LogUp challenges; qps[k]'s perm_alpha / beta_pows / cumsum and apows[k] (K[k] powers) are
+// written.  The host replays the step when it fetches the roots.
+constexpr int QUOT_MAX_CHIPS = 8;
+struct QuotAlphaTargets {
+  kb::EF* apows[QUOT_MAX_CHIPS];
+  int K[QUOT_MAX_CHIPS];
+};
+void challenge_quot(DevChallenger* ch, const uint32_t* root, const kb::EF* cums, int nc,
+                    const PermChallenges* pc, QuotParams* qps, const QuotAlphaTargets& tg,
+                    hipStream_t st);
 
 }  // namespace bfz

@@ -35,8 +35,18 @@ struct PowAcc {
   static constexpr uint32_t C32 = (1u << 25) - 2;  // 2^32 mod p
   uint64_t a64[4];
   int units;
-  const EF* __restrict__ ap;
+  // alpha powers, read through the constant address space: the pointer now comes from device
+  // memory (QuotParams), and through a generic pointer the reads became vector flat loads (+19
+  // VGPRs, k_quotient<0> 930 -> 1031 us); as constant-space loads they stay scalar.
+  const __attribute__((address_space(4))) uint32_t* ap;
   int k;
+  __device__ __forceinline__ EF pow_k() {
+    EF a;
+#pragma unroll
+    for (int e = 0; e < 4; e++) a.c[e] = ap[4 * k + e];
+    k++;
+    return a;
+  }
   __device__ __forceinline__ void fold() {
 #pragma unroll
     for (int e = 0; e < 4; e++) a64[e] = (uint64_t)(uint32_t)(a64[e] >> 32) * C32 + (uint32_t)a64[e];
@@ -44,14 +54,14 @@ struct PowAcc {
   }
   __device__ __forceinline__ void emit(uint32_t c) {
     if (units + 1 > 4) fold();
-    const EF a = ap[k++];
+    const EF a = pow_k();
 #pragma unroll
     for (int e = 0; e < 4; e++) a64[e] += (uint64_t)a.c[e] * c;
     units += 1;
   }
   __device__ __forceinline__ void emit_ext(const EF& c) {
     if (units + 2 > 4) fold();
-    const EF r = ef_mul(ap[k++], c);
+    const EF r = ef_mul(pow_k(), c);
 #pragma unroll
     for (int e = 0; e < 4; e++) a64[e] += (uint64_t)r.c[e] << 32;
     units += 2;
@@ -88,10 +98,12 @@ __global__ __launch_bounds__(256) void k_sel_inv(int logN, uint32_t shift, uint3
 // Register budget sized for 3 blocks per CU (4 spilled and was slower,
 // profiles/r02/ab_quotient_occupancy.txt).
 template <int CHIP>
-__global__ __launch_bounds__(256, 3) void k_quotient(QuotRows in, int logN, QuotParams qp,
+__global__ __launch_bounds__(256, 3) void k_quotient(QuotRows in, int logN,
+                                                  const QuotParams* __restrict__ qpp,
                                                   const uint32_t* __restrict__ twf,
                                                   const uint32_t* __restrict__ sel_inv,
                                                   QuotOut qo) {
+  const QuotParams qp = *qpp;  // device memory (the challenges are sampled on the device)
   constexpr int MW = QMAIN_W[CHIP];
   constexpr int PWD = QPREP_W[CHIP] > 0 ? QPREP_W[CHIP] : 1;
   constexpr int PMW = QPERM_W[CHIP];
@@ -130,7 +142,8 @@ __global__ __launch_bounds__(256, 3) void k_quotient(QuotRows in, int logN, Quot
   const uint32_t zi = mmul(zh, inv_ab);
   const uint32_t is_first = mmul(zi, b), is_last = mmul(zi, a), is_trans = b;
 
-  PowAcc acc{{0, 0, 0, 0}, 0, qp.alpha_pows, 0};
+  PowAcc acc{{0, 0, 0, 0}, 0,
+             (const __attribute__((address_space(4))) uint32_t*)qp.alpha_pows, 0};
   Air<BaseOps, PowAcc> air{L, Nx, PL, PN, is_first, is_last, is_trans, acc};
   air.template eval_air<CHIP>();
   air.template eval_perm<CHIP>(pl, pn, qp.perm_alpha, qp.beta_pows, qp.cumsum, ef_base(is_first),
@@ -142,10 +155,10 @@ __global__ __launch_bounds__(256, 3) void k_quotient(QuotRows in, int logN, Quot
 }
 
 template <int CHIP>
-static void launch_q(const QuotRows& in, int logN, const QuotParams& qp, const uint32_t* sel,
+static void launch_q(const QuotRows& in, int logN, const QuotParams* qp_dev, const uint32_t* sel,
                      const QuotOut& qo, hipStream_t st) {
   hipLaunchKernelGGL(k_quotient<CHIP>, dim3(ceil_div(in.count, 256)), dim3(256), 0, st, in, logN,
-                     qp, (const uint32_t*)twiddles().fwd.p, sel, qo);
+                     qp_dev, (const uint32_t*)twiddles().fwd.p, sel, qo);
   KCHECK();
 }
 
@@ -174,26 +187,80 @@ void quotient(int chip, const uint32_t* mainc, const uint32_t* prepc, const uint
 }
 
 void quotient_rows(int chip, const QuotRows& in, int logN, const QuotParams& qp, uint32_t* qout,
-                   hipStream_t st) {
+                   hipStream_t st, const QuotParams* qp_dev) {
   const size_t n = (size_t)1 << (logN - 1);
-  quotient_into(chip, in, logN, qp, QuotOut{{qout, qout + 4 * n}, n}, st);
+  quotient_into(chip, in, logN, qp, QuotOut{{qout, qout + 4 * n}, n}, st, qp_dev);
 }
 
 void quotient_into(int chip, const QuotRows& in, int logN, const QuotParams& qp, const QuotOut& qout,
-                   hipStream_t st) {
+                   hipStream_t st, const QuotParams* qp_dev) {
   twiddles().ensure(logN);
   const uint32_t* sel = sel_inv_table(logN, qp, st);
+  DBuf<QuotParams> up;
+  if (!qp_dev) {  // the host's parameters, uploaded (stream-ordered: freed after the launch is fine)
+    up.reset(1);
+    upload_async(up.p, &qp, sizeof(qp), st);
+    qp_dev = up.p;
+  }
   switch (chip) {
-    case CHIP_CPU: launch_q<CHIP_CPU>(in, logN, qp, sel, qout, st); break;
-    case CHIP_PROGRAM: launch_q<CHIP_PROGRAM>(in, logN, qp, sel, qout, st); break;
-    case CHIP_ADDSUB: launch_q<CHIP_ADDSUB>(in, logN, qp, sel, qout, st); break;
-    case CHIP_JUMP: launch_q<CHIP_JUMP>(in, logN, qp, sel, qout, st); break;
-    case CHIP_MEMORY: launch_q<CHIP_MEMORY>(in, logN, qp, sel, qout, st); break;
-    case CHIP_BYTE: launch_q<CHIP_BYTE>(in, logN, qp, sel, qout, st); break;
-    case CHIP_MEMINSTRS: launch_q<CHIP_MEMINSTRS>(in, logN, qp, sel, qout, st); break;
-    case CHIP_IO: launch_q<CHIP_IO>(in, logN, qp, sel, qout, st); break;
+    case CHIP_CPU: launch_q<CHIP_CPU>(in, logN, qp_dev, sel, qout, st); break;
+    case CHIP_PROGRAM: launch_q<CHIP_PROGRAM>(in, logN, qp_dev, sel, qout, st); break;
+    case CHIP_ADDSUB: launch_q<CHIP_ADDSUB>(in, logN, qp_dev, sel, qout, st); break;
+    case CHIP_JUMP: launch_q<CHIP_JUMP>(in, logN, qp_dev, sel, qout, st); break;
+    case CHIP_MEMORY: launch_q<CHIP_MEMORY>(in, logN, qp_dev, sel, qout, st); break;
+    case CHIP_BYTE: launch_q<CHIP_BYTE>(in, logN, qp_dev, sel, qout, st); break;
+    case CHIP_MEMINSTRS: launch_q<CHIP_MEMINSTRS>(in, logN, qp_dev, sel, qout, st); break;
+    case CHIP_IO: launch_q<CHIP_IO>(in, logN, qp_dev, sel, qout, st); break;
     default: throw std::runtime_error("quotient: bad chip");
   }
+}
+
+// The quotient challenge on the device (challenger.h): the sponge observes the permutation
+// root and every chip's cumulative sum, samples alpha (prover.rs:336-342); each chip's alpha
+// powers alpha^(K-1-j) and the challenge fields of its QuotParams are written.
+// Every 16-lane row runs the sponge (the same values); the powers are then spread over the whole
+// block, one (chip, j) pair per thread (64 threads looping over the chips took 28 us).
+constexpr int QCH_THREADS = 1024;
+__global__ __launch_bounds__(QCH_THREADS) void k_challenge_quot(DevChallenger* __restrict__ c,
+                                                                const uint32_t* __restrict__ root,
+                                                                const EF* __restrict__ cums, int nc,
+                                                                const PermChallenges* __restrict__ pc,
+                                                                QuotParams* __restrict__ qps,
+                                                                QuotAlphaTargets tg) {
+  __shared__ EF s_alpha;
+  if (threadIdx.x < 64) {  // one wave: the sponge
+    LaneSponge sp;
+    sp.load(c);
+    for (int i = 0; i < 8; i++) sp.observe(root[i]);
+    for (int k = 0; k < nc; k++)
+      for (int e = 0; e < 4; e++) sp.observe(cums[k].c[e]);
+    const EF alpha = sp.sample_ef();
+    sp.store(c);
+    if (threadIdx.x == 0) s_alpha = alpha;
+  }
+  __syncthreads();
+  const EF a = s_alpha;
+  int total = 0;
+  for (int k = 0; k < nc; k++) total += tg.K[k];
+  for (int t = threadIdx.x; t < total; t += blockDim.x) {
+    int k = 0, j = t;
+    while (j >= tg.K[k]) j -= tg.K[k++];
+    tg.apows[k][j] = ef_pow(a, (uint64_t)(tg.K[k] - 1 - j));
+  }
+  if (threadIdx.x < nc) {
+    QuotParams& q = qps[threadIdx.x];
+    q.perm_alpha = pc->alpha;
+    for (int j = 0; j < 8; j++) q.beta_pows[j] = pc->beta_pows[j];
+    q.cumsum = cums[threadIdx.x];
+  }
+}
+
+void challenge_quot(DevChallenger* ch, const uint32_t* root, const EF* cums, int nc,
+                    const PermChallenges* pc, QuotParams* qps, const QuotAlphaTargets& tg,
+                    hipStream_t st) {
+  if (nc > QUOT_MAX_CHIPS) throw std::runtime_error("challenge_quot: too many chips");
+  hipLaunchKernelGGL(k_challenge_quot, dim3(1), dim3(QCH_THREADS), 0, st, ch, root, cums, nc, pc, qps, tg);
+  KCHECK();
 }
 
 }  // namespace bfz
