@@ -287,6 +287,26 @@ def events_path(pk, prog, stdin, ref_proof, steps=3):
                     "HipProver::prove path, upload included"}
 
 
+SHARDED_EXTRA_LIMIT_S = 240
+
+
+def run_with_limit(fn, seconds):
+    """fn() in a daemon thread; its result, or None if it has not returned within `seconds`."""
+    import threading
+    box = {}
+
+    def body():
+        try:
+            box["r"] = fn()
+        except Exception as e:  # noqa: BLE001 - reported in the bench line
+            box["r"] = {"error": f"{type(e).__name__}: {e}"}
+
+    th = threading.Thread(target=body, daemon=True)
+    th.start()
+    th.join(seconds)
+    return None if th.is_alive() else box.get("r")
+
+
 def sharded_latency(dist, pk, rec, rank, world, device, ref_proof, steps=3):
     """Latency of ONE proof split over all ranks (bfz_record_prove_sharded: every rank hashes
     its subtree of each large Merkle tree; the subtree roots are all-gathered and the query
@@ -523,8 +543,15 @@ def main():
     if not sharded and args.sustain_s > 0:
         extra["sustained"] = sustained(lambda: one(), args.sustain_s,
                                        sync=lambda: _lib.check(L.bfz_synchronize()))
+    hung = False
     if world > 1 and not sharded and not args.no_extra:  # every rank takes part
-        extra["sharded_proof"] = sharded_latency(dist, pk, rec, rank, world, device, proof)
+        # RCCL has no run on this pool's one-GPU boxes: a hang in it must not cost the replica
+        # line, so the attempt runs in a thread with a wall-clock limit of its own
+        res = run_with_limit(lambda: sharded_latency(dist, pk, rec, rank, world, device, proof),
+                             SHARDED_EXTRA_LIMIT_S)
+        hung = res is None
+        extra["sharded_proof"] = res if res is not None else {
+            "error": f"no result within {SHARDED_EXTRA_LIMIT_S} s (abandoned)"}
 
     if rank == 0:
         lde_gbs = tm.lde_bytes / (tm.lde_ms * 1e-3) / 1e9 if tm.lde_ms > 0 else 0.0
@@ -574,6 +601,10 @@ def main():
             except Exception as e:  # keep the GPU line even if the baseline fails
                 line["cpu_baseline"] = {"error": str(e)}
         print(json.dumps(line), flush=True)
+    if hung:  # a collective may still be blocked: skip teardown that would wait for it
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
     L.bfz_record_free(rec)
     if dist:
         dist.destroy_process_group()

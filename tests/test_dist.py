@@ -95,3 +95,18 @@ def test_shard_collectives_gloo(world):
         assert rc_ag == 0 and rc_ar == 0
         assert recv == gathered, f"rank {rank}: all-gather out of rank order"
         assert words == reduced, f"rank {rank}: owner-masked all-reduce"
+
+
+def test_run_with_limit_abandons_a_hung_extra():
+    """bench.py runs the N>1 RCCL sharded-proof extra under a wall-clock limit: a result comes
+    back as is, an exception as an error entry, and a call still blocked at the limit as None
+    (the bench then reports it and exits without the teardown that would wait for it)."""
+    import threading
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.run_with_limit(lambda: {"ms": 1.0}, 5) == {"ms": 1.0}
+    err = bench.run_with_limit(lambda: 1 // 0, 5)
+    assert "ZeroDivisionError" in err["error"]
+    gate = threading.Event()
+    assert bench.run_with_limit(gate.wait, 0.2) is None
+    gate.set()
