@@ -412,9 +412,13 @@ def run_pcs(args, rank, world, device, dist, coll):
     wl = W // world
     dev = torch.device("cuda", device)
     torch.cuda.set_device(dev)
-    g = torch.Generator(device=dev)
-    g.manual_seed(0x5EED + rank)
-    cols = torch.randint(0, P, (wl, 1 << log_n), dtype=torch.int32, device=dev, generator=g)
+
+    def rank_cols(r):  # rank r's columns: uniform words, seeded per rank
+        g = torch.Generator(device=dev)
+        g.manual_seed(0x5EED + r)
+        return torch.randint(0, P, (wl, 1 << log_n), dtype=torch.int32, device=dev, generator=g)
+
+    cols = rank_cols(rank)
     send = recv = None
     if world > 1:
         send = torch.empty((wl * (2 << log_n),), dtype=torch.int32, device=dev)
@@ -426,6 +430,16 @@ def run_pcs(args, rank, world, device, dist, coll):
     for _ in range(args.warmup):
         root, fri, fin = step()
     ms = timed_steps(step, args.steps, dist, sync=torch.cuda.synchronize)
+    root, fri, fin = step()  # collective: every rank takes part
+    exact = None
+    if world > 1 and rank == 0:
+        # the same trace committed by one rank alone (world = 1): the sharded root, FRI roots and
+        # final value must be identical
+        full = torch.cat([rank_cols(r) for r in range(world)])
+        r1, f1, fin1 = bfz_shard.commit_fri_sharded(full, log_n, None, 0)
+        exact = bool((r1 == root).all() and f1.shape == fri.shape and (f1 == fri).all()
+                     and (fin1 == fin).all())
+        del full
     if rank == 0:
         n = 1 << log_n
         lde_bytes = 12.0 * n * W  # coset LDE algorithmic bytes of the whole trace
@@ -441,6 +455,7 @@ def run_pcs(args, rank, world, device, dist, coll):
             "trace_cells_per_s": round(n * W / (ms * 1e-3), 1),
             "lde_equiv_gbs": round(lde_bytes / (ms * 1e-3) / 1e9, 1),
             "fri_rounds": int(len(fri)),
+            "bit_exact_vs_world1": exact,
             "root": [int(x) for x in root],
         }
         print(json.dumps(line), flush=True)
