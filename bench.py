@@ -287,7 +287,7 @@ def events_path(pk, prog, stdin, ref_proof, steps=3):
                     "HipProver::prove path, upload included"}
 
 
-SHARDED_EXTRA_LIMIT_S = 240
+SHARDED_EXTRA_LIMIT_S = 150
 
 
 def run_with_limit(fn, seconds):
