@@ -564,7 +564,8 @@ def main():
         # line, so the attempt runs in a thread with a wall-clock limit of its own
         res = run_with_limit(lambda: sharded_latency(dist, pk, rec, rank, world, device, proof),
                              SHARDED_EXTRA_LIMIT_S)
-        hung = res is None
+        # a failed or abandoned RCCL attempt may leave a communicator blocked: skip teardown
+        hung = res is None or "error" in res
         extra["sharded_proof"] = res if res is not None else {
             "error": f"no result within {SHARDED_EXTRA_LIMIT_S} s (abandoned)"}
 
