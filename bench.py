@@ -553,11 +553,23 @@ def main():
     proof = one(tm)
     client.verify(sdk.BfProofWithPublicValues(proof=proof, stdin=stdin), vk)
 
-    ms = timed_steps(lambda: one(), args.steps, dist, sync=lambda: _lib.check(L.bfz_synchronize()))
+    last = {}
+
+    def kept():  # the proof stays referenced; it is compared after the timed region
+        last["proof"] = one()
+
+    ms = timed_steps(kept, args.steps, dist, sync=lambda: _lib.check(L.bfz_synchronize()))
+    # every timed step proves the same record: the last one must be the verified proof's bytes
+    if last["proof"] != proof:
+        raise SystemExit("bench: the last timed proof differs from the verified proof")
     extra = {}
     if not sharded and args.sustain_s > 0:
-        extra["sustained"] = sustained(lambda: one(), args.sustain_s,
+        last.clear()
+        extra["sustained"] = sustained(kept, args.sustain_s,
                                        sync=lambda: _lib.check(L.bfz_synchronize()))
+        if last["proof"] != proof:
+            raise SystemExit("bench: the last sustained proof differs from the verified proof")
+        extra["sustained"]["last_proof_checked"] = True
     hung = False
     if world > 1 and not sharded and not args.no_extra:  # every rank takes part
         # RCCL has no run on this pool's one-GPU boxes: a hang in it must not cost the replica
@@ -600,6 +612,8 @@ def main():
             "poseidon2": poseidon2_roofline(tm),
             "openings": openings_roofline(tm),
             "proof_bytes": len(proof),
+            "proof_check": "host verifier accepted the proof; the last timed proof (and the last "
+                           "sustained one) are byte-identical to it",
         }
         if "sustained" in extra:
             line["sustained"] = extra["sustained"]
@@ -620,7 +634,10 @@ def main():
     if hung:  # a collective may still be blocked: skip teardown that would wait for it
         sys.stdout.flush()
         sys.stderr.flush()
-        os._exit(0)
+        # the replica line is printed; an abandoned attempt (a thread still blocked inside libbfz)
+        # is not a clean run, so the status says so; a collective that failed with an
+        # error has returned and leaves a clean exit
+        os._exit(3 if extra.get("sharded_proof", {}).get("error", "").startswith("no result") else 0)
     L.bfz_record_free(rec)
     if dist:
         dist.destroy_process_group()

@@ -181,6 +181,7 @@ extern "C" {
     pub fn bfz_device_name(buf: *mut c_char, cap: usize) -> c_int;
     pub fn bfz_free(p: *mut c_void);
     pub fn bfz_synchronize() -> c_int;
+    pub fn bfz_selftest(name: *const c_char) -> c_int;
 
     pub fn bfz_execute(elf: *const c_char, stdin_data: *const u8, nin: usize, out: *mut u8,
                        out_cap: usize, out_len: *mut usize, cycles: *mut u64) -> c_int;

@@ -86,6 +86,9 @@ const char* bfz_build_id(void);
 int bfz_device_name(char* buf, size_t cap);
 void bfz_free(void* p);
 int bfz_synchronize(void); /* hipDeviceSynchronize on the bound device */
+/* Host-only self-tests of the boundary's own bookkeeping (no device needed): "emit_rollback" =
+ * a batch hand-over that fails part-way releases the proofs already handed out. 0 = passed. */
+int bfz_selftest(const char* name);
 
 int bfz_execute(const char* elf, const uint8_t* stdin_data, size_t nin, uint8_t* out,
                 size_t out_cap, size_t* out_len, uint64_t* cycles);

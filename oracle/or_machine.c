@@ -434,7 +434,7 @@ void or_chip_lookups_get(int chip, or_chip_lookups* o) {
 #define SEND(l) o->sends[o->nsends++] = (l)
 #define RECV(l) o->recvs[o->nrecvs++] = (l)
   switch (chip) {
-    case CHIP_CPU: { /* cpu/air.rs:272-306 -> air/program.rs, air/memory.rs, air/u8_air.rs */
+    case CHIP_CPU: { /* cpu/air.rs:28-98 -> air/program.rs, air/memory.rs, air/u8_air.rs */
       or_vcol clk = vc_add_term(vc_m(0), SRC_MAIN, 1, 1u << 16);
       or_vcol clk1 = clk; clk1.c = 1;
       or_vcol clk2 = clk; clk2.c = 2;
@@ -506,7 +506,7 @@ void or_chip_lookups_get(int chip, or_chip_lookups* o) {
       RECV(lk(K_MEMINSTR, 5, v, vc_add_term(vc_m(38), SRC_MAIN, 39, 1)));
       break;
     }
-    case CHIP_IO: { /* io/mod.rs:374-388 */
+    case CHIP_IO: { /* io/mod.rs:127-141 */
       or_vcol op = vc_const(0);
       op = vc_add_term(op, SRC_MAIN, 3, OP_INPUT);
       op = vc_add_term(op, SRC_MAIN, 4, OP_OUTPUT);
@@ -563,7 +563,7 @@ static void word_range_check(or_folder* f, const ef* v, const ef* rc, ef is_real
   emit(f, M(M(is_real, rc[13]), A(A(v[0], v[1]), v[2])));
 }
 
-static void eval_cpu(or_folder* f) { /* cpu/air.rs:272-429 */
+static void eval_cpu(or_folder* f) { /* cpu/air.rs:28-186 */
   ef c65536 = E(1u << 16);
   ef clk = A(M(c65536, L(1)), L(0));
   /* eval_registers -> eval_memory_access(clk+1, mp, mv_access, mv_accessed) */
@@ -643,7 +643,7 @@ static void eval_meminstrs(or_folder* f) { /* memory/instructions/air.rs:25-76 *
   word_range_check(f, &L(20), &L(24), L(40));
 }
 
-static void eval_io(or_folder* f) { /* io/mod.rs:374-388 */
+static void eval_io(or_folder* f) { /* io/mod.rs:127-141 */
   emit(f, boolc(L(3)));
   emit(f, boolc(L(4)));
   emit(f, boolc(A(L(3), L(4))));

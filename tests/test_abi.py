@@ -422,3 +422,12 @@ def test_reference_patch_applies():
                         os.path.join(ROOT, "crates", "reference-patch", "0001-hip-core-prover.patch")],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_batch_handover_failure_releases_emitted_proofs():
+    """a bfz_prove_batch hand-over that fails part-way releases the proofs it already
+    handed out through bfz_free (they are library-owned vectors, not malloc'd) and clears every
+    slot; host-only, so it runs without a GPU."""
+    from bfz import _lib
+    assert _lib.lib().bfz_selftest(b"emit_rollback") == 0, _lib.lib().bfz_last_error()
+    assert _lib.lib().bfz_selftest(b"no_such_test") != 0

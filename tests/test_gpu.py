@@ -535,3 +535,19 @@ def test_logup_perm_trace_matches_oracle(prog, stdin):
             _lib.lib().bfz_free(out)
             assert np.array_equal(unmont(got).reshape(exp.shape), exp), (prog, chip, trial)
             assert unmont(list(cs)).tolist() == exp_cs, (prog, chip, trial)
+
+
+def test_device_transcript_divergence_is_an_error(client, monkeypatch):
+    """the LogUp alpha/beta, the quotient alpha, the FRI betas, the PoW check
+    and the query indices are sampled on the device and replayed by the host.  A device sponge
+    that is not the host's (fault injected into its uploaded state) must fail the proof with an
+    error naming the divergence -- not return a proof the verifier rejects -- and the library
+    must keep working afterwards."""
+    prog, stdin = guests.FIBO, [17]
+    pk, vk = client.setup(prog)
+    monkeypatch.setenv("BFZ_FAULT_DEVICE_CHALLENGER", "1")
+    with pytest.raises(_lib.BfzError, match="device transcript diverged"):
+        client.prove(pk, stdin).run()
+    monkeypatch.delenv("BFZ_FAULT_DEVICE_CHALLENGER")
+    pf = client.prove(pk, stdin).run()
+    assert pf.proof == O.prove(prog, stdin)

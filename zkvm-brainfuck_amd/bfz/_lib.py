@@ -69,6 +69,7 @@ SIGNATURES = [
     ("bfz_device_name", c_int, [c_char_p, c_size_t]),
     ("bfz_free", None, [c_void_p]),
     ("bfz_synchronize", c_int, []),
+    ("bfz_selftest", c_int, [c_char_p]),
     ("bfz_execute", c_int, [c_char_p, POINTER(c_uint8), c_size_t, POINTER(c_uint8), c_size_t,
                             POINTER(c_size_t), POINTER(c_uint64)]),
     ("bfz_trace", c_int, [c_char_p, POINTER(c_uint8), c_size_t, c_int, c_int,

@@ -71,7 +71,7 @@ constexpr VCol vword(uint8_t col) {  // Word::reduce (crates/stark/src/word.rs:6
                   {S_MAIN, (uint8_t)(col + 2), 1u << 16}, {S_MAIN, (uint8_t)(col + 3), 1u << 24}}, 0};
 }
 
-// Cpu: cpu/air.rs:272-336 -> air/program.rs:12-27, air/memory.rs:17-125, air/u8_air.rs:7-15.
+// Cpu: cpu/air.rs:28-98 -> air/program.rs:12-27, air/memory.rs:17-125, air/u8_air.rs:7-15.
 // clk = clk_16 + 2^16 clk_8 (cols 0,1).
 constexpr ChipLookups CPU_LOOKUPS = {16, {
   {K_PROGRAM, 7, true, {vm(2), vm(8), vm(8), vm(9), vm(10), vm(11), vm(12)}, vm(30)},
@@ -91,7 +91,7 @@ constexpr ChipLookups CPU_LOOKUPS = {16, {
   {K_MEMORY, 3, false, {vm2(0, 1, 1, 1u << 16, 1), vm(4), vm(14)}, vm(23)},  // (clk+1, mp, value)
   {K_MEMORY, 3, false, {vm2(0, 1, 1, 1u << 16, 2), vm(4), vm(19)}, vm(24)},  // (clk+2, ...)
 }};
-// Program: program/mod.rs:402-417 (receive_program: pc, opcode, opcode, op_a[0..4])
+// Program: program/mod.rs:152-163 (receive_program: pc, opcode, opcode, op_a[0..4])
 constexpr ChipLookups PROGRAM_LOOKUPS = {1, {
   {K_PROGRAM, 7, false, {vp(0), vp(1), vp(1), vp(2), vp(3), vp(4), vp(5)}, vm(0)},
 }};
@@ -107,7 +107,7 @@ constexpr ChipLookups ADDSUB_LOOKUPS = {5, {
 constexpr ChipLookups JUMP_LOOKUPS = {1, {
   {K_JUMP, 4, false, {vword(0), vword(18), vm2(43, 0, 44, 1), vm(40)}, vm2(43, 1, 44, 1)},
 }};
-// Memory: memory/memory.rs:240-253 (per entry: receive initial, send final)
+// Memory: memory/memory.rs:132-145 (per entry: receive initial, send final)
 constexpr ChipLookups MEMORY_LOOKUPS = {4, {
   {K_MEMORY, 3, true, {vm(2), vm(0), vm(4)}, vm(5)},
   {K_MEMORY, 3, true, {vm(8), vm(6), vm(10)}, vm(11)},
@@ -123,7 +123,7 @@ constexpr ChipLookups BYTE_LOOKUPS = {2, {
 constexpr ChipLookups MEMINSTRS_LOOKUPS = {1, {
   {K_MEMINSTR, 5, false, {vm(1), vm(0), vm2(38, 4, 39, 5), vword(2), vword(20)}, vm2(38, 1, 39, 1)},
 }};
-// IO: io/mod.rs:374-388
+// IO: io/mod.rs:127-141
 constexpr ChipLookups IO_LOOKUPS = {1, {
   {K_IO, 4, false, {vm(0), vm2(3, 6, 4, 7), vm(1), vm(2)}, vm2(3, 1, 4, 1)},
 }};
@@ -195,7 +195,7 @@ struct Air {
     acc.emit(mul(mul(is_real, rc[13]), add(add(v[0], v[1]), v[2])));
   }
 
-  // CpuChip::eval (cpu/air.rs:272-429)
+  // CpuChip::eval (cpu/air.rs:28-186)
   KB_HD void eval_cpu() {
     const T c16 = Ops::cst(MC(1u << 16));
     const T clk = add(mul(c16, L[1]), L[0]);
@@ -278,7 +278,7 @@ struct Air {
     word_range_check(&L[20], &L[24], L[40]);
   }
 
-  // IoChip::eval (io/mod.rs:374-388)
+  // IoChip::eval (io/mod.rs:127-141)
   KB_HD void eval_io() {
     acc.emit(boolc(L[3]));
     acc.emit(boolc(L[4]));

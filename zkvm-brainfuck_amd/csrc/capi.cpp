@@ -190,6 +190,60 @@ static int emit(std::vector<uint8_t>&& v, uint8_t** proof, size_t* len) {
   return 0;
 }
 
+// Hands every proof of a batch to the caller.  If one hand-over fails, the proofs already
+// handed out are released the way the caller would (bfz_free: they are emitted() vectors, not
+// malloc'd), every slot is cleared, and the error propagates.  fail_at injects that failure at
+// job fail_at (bfz_selftest only).
+static void emit_all(std::vector<std::vector<uint8_t>>& v, uint8_t** proofs, size_t* lens,
+                     size_t fail_at) {
+  for (size_t i = 0; i < v.size(); i++) {
+    try {
+      if (i == fail_at) throw std::runtime_error("emit: injected failure");
+      emit(std::move(v[i]), &proofs[i], &lens[i]);
+    } catch (...) {
+      for (size_t k = 0; k < i; k++) {
+        bfz_free(proofs[k]);
+        proofs[k] = nullptr;
+        lens[k] = 0;
+      }
+      throw;
+    }
+  }
+}
+
+int bfz_selftest(const char* name) {
+  return guarded([&] {
+    const std::string what = name ? name : "";
+    if (what == "emit_rollback") {
+      size_t before;
+      {
+        std::lock_guard<std::mutex> lk(emitted_mu());
+        before = emitted().size();
+      }
+      std::vector<std::vector<uint8_t>> v(4, std::vector<uint8_t>(1000, 7));
+      uint8_t* proofs[4] = {};
+      size_t lens[4] = {};
+      bool threw = false;
+      try {
+        emit_all(v, proofs, lens, 2);
+      } catch (const std::exception&) {
+        threw = true;
+      }
+      size_t after;
+      {
+        std::lock_guard<std::mutex> lk(emitted_mu());
+        after = emitted().size();
+      }
+      if (!threw) throw std::runtime_error("selftest emit_rollback: no failure raised");
+      for (int k = 0; k < 4; k++)
+        if (proofs[k] || lens[k]) throw std::runtime_error("selftest emit_rollback: slot not cleared");
+      if (after != before) throw std::runtime_error("selftest emit_rollback: emitted proofs leaked");
+      return 0;
+    }
+    throw std::runtime_error("bfz_selftest: unknown test '" + what + "'");
+  });
+}
+
 // Field-wise serialization of an event stream (no struct padding), for comparing executors.
 }  // extern "C"
 namespace {
@@ -575,14 +629,7 @@ int bfz_prove_batch(const bfz_pk* pk, const uint8_t* const* stdins, const size_t
     if (E < 1 || E > 64) throw std::runtime_error("exec_threads must be in 1..64");
     bfz::BatchStats bs;
     auto v = bfz::prove_batch(*pk->pk, jobs, opts(), E, &bs);
-    for (size_t i = 0; i < njobs; i++) {
-      try {
-        emit(std::move(v[i]), &proofs[i], &proof_lens[i]);
-      } catch (...) {
-        for (size_t k = 0; k < i; k++) std::free(proofs[k]);
-        throw;
-      }
-    }
+    emit_all(v, proofs, proof_lens, (size_t)-1);
     if (stats) {
       stats->wall_ms = bs.wall_ms;
       stats->exec_ms = bs.exec_ms;

@@ -302,7 +302,7 @@ void execute_into(const Program& prog, const uint8_t* in, size_t nin, HostEvents
 }
 
 void generate_dependencies(ExecutionRecord& rec) {
-  // CpuChip (cpu/trace.rs:58-79,182-243), MemoryAccessCols::populate_access
+  // CpuChip (cpu/trace.rs:58-79,86-150), MemoryAccessCols::populate_access
   // (memory/consistency/trace.rs:52-77), AddSubChip (alu/mod.rs:95-116; operations/add.rs:20-40).
   rec.u8_mult.assign(256, 0);
   rec.u16_mult.assign(65536, 0);
@@ -424,7 +424,7 @@ size_t main_trace(int chip, const ExecutionRecord& r, std::vector<uint32_t>& out
   out.assign(h * w, 0);
   const Program& prog = *r.program;
   switch (chip) {
-    case CHIP_CPU:  // cpu/trace.rs:28-55,182-243; layout cpu/cols.rs:29-71
+    case CHIP_CPU:  // cpu/trace.rs:28-55,86-150; layout cpu/cols.rs:29-71
       for (size_t i = 0; i < r.cpu.size(); i++) {
         const CpuEvent& e = r.cpu[i];
         uint32_t* c = &out[i * w];

@@ -580,6 +580,10 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     std::memcpy(dc.out, ch.out, sizeof(dc.out));
     dc.nin = ch.nin;
     dc.nout = ch.nout;
+    // fault injection for tests/test_gpu.py: a device sponge that is not the host's must end in
+    // an error at proving time, not in a proof the verifier rejects
+    if (const char* f = std::getenv("BFZ_FAULT_DEVICE_CHALLENGER"); f && *f == '1')
+      dc.st[0] = dc.st[0] ? dc.st[0] - 1 : 1;
     upload_async(dc_d.p, &dc, sizeof(dc), st);
   }
   DBuf<PermChallenges> pc_d(1);
@@ -590,9 +594,12 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   Round permr;
   permr.mats.resize(nc);
   // cums_d: the chips' cumulative sums, then (fetched together before zeta) the main,
-  // permutation and quotient roots, 2 EF slots (8 words) each
-  DBuf<EF> cums_d(nc + 6);
+  // permutation and quotient roots, 2 EF slots (8 words) each, then the device's samples of the
+  // LogUp alpha, beta and the quotient alpha (compared with the host replay below)
+  DBuf<EF> cums_d(nc + 9);
   HIP_CHECK(hipMemcpyAsync(cums_d.p + nc, mainr.tree.layers.back().p, 32, hipMemcpyDeviceToDevice, st));
+  HIP_CHECK(hipMemcpyAsync(cums_d.p + nc + 6, &pc_d.p->alpha, sizeof(EF), hipMemcpyDeviceToDevice, st));
+  HIP_CHECK(hipMemcpyAsync(cums_d.p + nc + 7, &pc_d.p->beta_pows[1], sizeof(EF), hipMemcpyDeviceToDevice, st));
   for (int k = 0; k < nc; k++) {
     const int c = chip[k];
     const int pw = perm_width(c);
@@ -616,6 +623,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   std::vector<QuotParams> qph(nc);  // the challenge-independent fields; the rest on the device
   DBuf<QuotParams> qp_d(std::max(nc, 1));
   QuotAlphaTargets tg{};
+  tg.alpha_out = cums_d.p + nc + 8;
   for (int k = 0; k < nc; k++) {
     const size_t n = hn[k];
     const int K = num_constraints(chip[k]);
@@ -717,21 +725,28 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   quotr.commit(st, /*fetch_root=*/false);
   if (ev.on) ev.end(e2, st, &tms->quotient);
   HIP_CHECK(hipMemcpyAsync(cums_d.p + nc + 4, quotr.tree.layers.back().p, 32, hipMemcpyDeviceToDevice, st));
-  std::vector<EF> cums(nc + 6);
-  fetch(cums.data(), cums_d.p, (nc + 6) * sizeof(EF), st);
+  std::vector<EF> cums(nc + 9);
+  fetch(cums.data(), cums_d.p, (nc + 9) * sizeof(EF), st);
   htrace().mark("roots fetched");
   std::memcpy(mainr.tree.root, &cums[nc], 32);
   std::memcpy(permr.tree.root, &cums[nc + 2], 32);
   std::memcpy(quotr.tree.root, &cums[nc + 4], 32);
+  const EF dev_perm_alpha = cums[nc + 6], dev_perm_beta = cums[nc + 7], dev_quot_alpha = cums[nc + 8];
   md.root_on_host = true;
   cums.resize(nc);
-  // the host transcript replays the device steps (prover.rs:265-272, 336-342, 413-416)
+  // The host transcript replays the device steps (prover.rs:265-272, 336-342, 413-416): the
+  // reference has one transcript, so the device's samples must be the host's (a drifted device
+  // sponge would otherwise surface only as a proof the verifier rejects).
+  auto same = [](const EF& dev, const EF& host, const char* what) {
+    if (!ef_eq(dev, host))
+      throw std::runtime_error(std::string("device transcript diverged from the host challenger: ") + what);
+  };
   ch.observe_digest(mainr.tree.root);
-  (void)ch.sample_ef();  // LogUp alpha
-  (void)ch.sample_ef();  // LogUp beta
+  same(dev_perm_alpha, ch.sample_ef(), "LogUp alpha");
+  same(dev_perm_beta, ch.sample_ef(), "LogUp beta");
   ch.observe_digest(permr.tree.root);
   for (int k = 0; k < nc; k++) ch.observe_ef(cums[k]);
-  (void)ch.sample_ef();  // quotient alpha
+  same(dev_quot_alpha, ch.sample_ef(), "quotient alpha");
   ch.observe_digest(quotr.tree.root);
   const EF zeta = ch.sample_ef();
   htrace().mark("zeta");
@@ -1276,14 +1291,25 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     throw std::runtime_error("FRI: final polynomial is not constant (trace violates the AIR)");
   const uint32_t witness = tbox[T_RES];
   if (tbox[T_RES + 1] != 1) throw std::runtime_error("grind: bad witness");
-  {  // the host challenger = the device's after the last query index
+  {  // The host replays the device's FRI transcript (fri::prover: observe each commit-phase
+     // root, sample its beta; observe the final constant; the witness check; the query indices)
+     // and must arrive at the device's challenger and the device's query indices.
+    for (int i = 0; i < nt; i++) {
+      ch.observe_digest(trees[i].root);
+      (void)ch.sample_ef();
+    }
+    ch.observe_ef(fin[0]);
+    if (!ch.check_witness(POW_BITS, witness))
+      throw std::runtime_error("device transcript diverged from the host challenger: PoW witness");
+    for (int q = 0; q < nq; q++)
+      if (ch.sample_bits(Lmax) != tbox[T_Q + q])
+        throw std::runtime_error("device transcript diverged from the host challenger: query index");
     DevChallenger dc;
     std::memcpy(&dc, &tbox[T_CH], sizeof(dc));
-    std::memcpy(ch.st, dc.st, 64);
-    std::memcpy(ch.in, dc.in, 32);
-    std::memcpy(ch.out, dc.out, 32);
-    ch.nin = dc.nin;
-    ch.nout = dc.nout;
+    if (std::memcmp(ch.st, dc.st, 64) != 0 || ch.nin != (int)dc.nin || ch.nout != (int)dc.nout ||
+        std::memcmp(ch.in, dc.in, 4 * (size_t)ch.nin) != 0 ||
+        std::memcmp(ch.out, dc.out, 4 * (size_t)ch.nout) != 0)
+      throw std::runtime_error("device transcript diverged from the host challenger: final state");
   }
   if (after) *after = ch;  // the transcript is complete: MachineProver::open's &mut challenger
   const uint32_t* words = tbox + T_W;

@@ -56,6 +56,7 @@ constexpr int QUOT_MAX_CHIPS = 8;
 struct QuotAlphaTargets {
   kb::EF* apows[QUOT_MAX_CHIPS];
   int K[QUOT_MAX_CHIPS];
+  kb::EF* alpha_out;  // optional: the sampled alpha itself (checked against the host replay)
 };
 void challenge_quot(DevChallenger* ch, const uint32_t* root, const kb::EF* cums, int nc,
                     const PermChallenges* pc, QuotParams* qps, const QuotAlphaTargets& tg,

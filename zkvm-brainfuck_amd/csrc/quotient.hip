@@ -236,7 +236,10 @@ __global__ __launch_bounds__(QCH_THREADS) void k_challenge_quot(DevChallenger* _
       for (int e = 0; e < 4; e++) sp.observe(cums[k].c[e]);
     const EF alpha = sp.sample_ef();
     sp.store(c);
-    if (threadIdx.x == 0) s_alpha = alpha;
+    if (threadIdx.x == 0) {
+      s_alpha = alpha;
+      if (tg.alpha_out) *tg.alpha_out = alpha;
+    }
   }
   __syncthreads();
   const EF a = s_alpha;

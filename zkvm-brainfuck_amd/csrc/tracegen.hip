@@ -74,7 +74,7 @@ __device__ __forceinline__ void bump16(uint32_t* lds16, uint32_t* g16, uint32_t 
   else atomicAdd(&g16[v], 1u);
 }
 
-// CpuChip (cpu/trace.rs:58-79,182-243) + AddSubChip (alu/mod.rs:95-116) byte lookups and
+// CpuChip (cpu/trace.rs:58-79,86-150) + AddSubChip (alu/mod.rs:95-116) byte lookups and
 // the Program chip's per-pc execution counts (program/mod.rs:100-135).
 __global__ __launch_bounds__(256) void k_deps(const CpuEvent* __restrict__ cpu, size_t ncpu,
                                               const AluEvent* __restrict__ alu, size_t nalu,
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(256) void k_deps(const CpuEvent* __restrict__ cpu, 
 }
 
 // ---------------------------------------------------------------- per-chip traces
-// CpuChip: cpu/trace.rs:28-55,182-243; layout cpu/cols.rs:29-71
+// CpuChip: cpu/trace.rs:28-55,86-150; layout cpu/cols.rs:29-71
 __global__ __launch_bounds__(256) void k_trace_cpu(const CpuEvent* __restrict__ ev, size_t n,
                                                    const Instruction* __restrict__ prog,
                                                    uint32_t* __restrict__ out, size_t h, int logh) {
