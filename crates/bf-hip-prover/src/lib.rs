@@ -184,6 +184,7 @@ fn access(a: &Option<MemoryRecordEnum>) -> sys::bfz_memory_access {
 }
 
 /// The record's event vectors (record.rs:15-34) in the bfz_*_event layouts.
+#[allow(dead_code)] // the full hand-over (bfz_record_from_events); prove uses CycleArrays
 struct EventArrays {
     cpu: Vec<sys::bfz_cpu_event>,
     add: Vec<sys::bfz_alu_event>,
@@ -194,6 +195,7 @@ struct EventArrays {
     memory: Vec<sys::bfz_memory_event>,
 }
 
+#[allow(dead_code)]
 impl EventArrays {
     fn new(r: &ExecutionRecord) -> Self {
         let alu = |e: &bf_core_executor::events::AluEvent| sys::bfz_alu_event {
@@ -291,6 +293,44 @@ impl EventArrays {
             n_memory_instr: self.memory_instr.len(),
             memory: self.memory.as_ptr(),
             n_memory: self.memory.len(),
+        }
+    }
+}
+
+/// The compact hand-over of `bfz_record_from_cycles`: one 16-byte `bfz_cycle` per CpuEvent
+/// plus the memory events.  The device rebuilds the CpuEvents' derived fields and every chip's
+/// events (add/jump/memory_instr/io are the cycles' own fields, executor.rs:196-239), so about
+/// 16 B per cycle cross PCIe instead of ~64 B.
+struct CycleArrays {
+    cycles: Vec<sys::bfz_cycle>,
+    memory: Vec<sys::bfz_memory_event>,
+}
+
+impl CycleArrays {
+    fn new(r: &ExecutionRecord) -> Self {
+        let cycle = |e: &bf_core_executor::events::CpuEvent| {
+            let (prev_ts, prev_value) = match e.mv_access {
+                None => (0, 0),
+                Some(MemoryRecordEnum::Read(a)) => (a.prev_timestamp, 0),
+                Some(MemoryRecordEnum::Write(a)) => (a.prev_timestamp, a.prev_value),
+            };
+            sys::bfz_cycle { pc: e.pc, mp: e.mp, prev_ts, mv: e.mv, prev_value, _pad: [0; 2] }
+        };
+        Self {
+            cycles: r.cpu_events.par_iter().map(cycle).collect(),
+            // HashMap-drain order (executor.rs:74); libbfz sorts it into the normal form
+            memory: r
+                .cpu_memory_access
+                .iter()
+                .map(|e| sys::bfz_memory_event {
+                    addr: e.addr,
+                    initial_timestamp: e.initial_mem_access.timestamp,
+                    final_timestamp: e.final_mem_access.timestamp,
+                    initial_value: e.initial_mem_access.value,
+                    final_value: e.final_mem_access.value,
+                    _pad: [0; 2],
+                })
+                .collect(),
         }
     }
 }
@@ -409,10 +449,20 @@ impl MachineProver<SC, A> for HipProver {
         #[cfg(feature = "debug")]
         self.machine().generate_dependencies(record, None);
         pk.observe_into(challenger); // prover.rs:572
-        let events = EventArrays::new(record);
-        let c_events = events.as_c();
+        // the compact hand-over (16 B per cycle); EventArrays + bfz_record_from_events remains
+        // for callers that hold the full event vectors
+        let events = CycleArrays::new(record);
         let mut rec = core::ptr::null_mut();
-        sys::check(unsafe { sys::bfz_record_from_events(pk.dev, &c_events, &mut rec) });
+        sys::check(unsafe {
+            sys::bfz_record_from_cycles(
+                pk.dev,
+                events.cycles.as_ptr(),
+                events.cycles.len(),
+                events.memory.as_ptr(),
+                events.memory.len(),
+                &mut rec,
+            )
+        });
         let rec = HipRecord(rec);
         drop(events); // the events are in HBM now
         let mut data = core::ptr::null_mut();

@@ -148,6 +148,18 @@ pub struct bfz_memory_event {
     pub final_value: u8,
     pub _pad: [u8; 2],
 }
+/// One `CpuEvent` in the compact hand-over of `bfz_record_from_cycles` (16 bytes): the rest of
+/// the record is rebuilt on the device (include/bfz.h).
+#[repr(C)]
+#[derive(Clone, Copy, Debug, Default)]
+pub struct bfz_cycle {
+    pub pc: u32,
+    pub mp: u32,
+    pub prev_ts: u32,
+    pub mv: u8,
+    pub prev_value: u8,
+    pub _pad: [u8; 2],
+}
 /// The `ExecutionRecord` event vectors (record.rs:15-34) as pointer + length pairs.
 #[repr(C)]
 #[derive(Clone, Copy, Debug)]
@@ -229,6 +241,9 @@ extern "C" {
                             proof_len: *mut usize, timings: *mut bfz_timings) -> c_int;
     pub fn bfz_record_free(rec: *mut bfz_record);
     pub fn bfz_record_from_events(pk: *const bfz_pk, events: *const bfz_events,
+                                  rec: *mut *mut bfz_record) -> c_int;
+    pub fn bfz_record_from_cycles(pk: *const bfz_pk, cycles: *const bfz_cycle, n_cycles: usize,
+                                  memory: *const bfz_memory_event, n_memory: usize,
                                   rec: *mut *mut bfz_record) -> c_int;
     pub fn bfz_record_prove_sharded(pk: *const bfz_pk, rec: *const bfz_record, rank: c_int,
                                     world: c_int, allgather: bfz_allgather_fn,

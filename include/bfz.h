@@ -264,6 +264,27 @@ typedef struct {
  * them.  Host pointers (pageable is fine). */
 int bfz_record_from_events(const bfz_pk* pk, const bfz_events* events, bfz_record** rec);
 
+/* The same record from a compact hand-over: one 16-byte bfz_cycle per CpuEvent (in
+ * record.cpu_events order) plus cpu_memory_access.  Everything else in the record is a function
+ * of these and the program: clk = 2 i (executor.rs:131), next_pc / next_mp = the next cycle's pc
+ * / mp (the last cycle's next_pc is the program length, its next_mp follows its opcode),
+ * next_mv and both access records follow the opcode (executor.rs:140-205: the read at clk + 1,
+ * the ALU write at clk + 2), and every add/jump/memory_instr/io event is the cycle's own fields
+ * (emit_events, executor.rs:196-239) -- so the device rebuilds them (tracegen.hip
+ * expand_cycles) instead of receiving ~64 B per cycle.  Cycles that no reference record holds
+ * (pc outside the program, an access on a memory step, prev_timestamp >= clk + 1, prev_value
+ * outside an Input, nonzero padding) are refused before any trace kernel runs. */
+typedef struct {
+  uint32_t pc;         /* CpuEvent::pc */
+  uint32_t mp;         /* CpuEvent::mp */
+  uint32_t prev_ts;    /* mv_access's prev_timestamp; 0 when mv_access is None (memory steps) */
+  uint8_t mv;          /* CpuEvent::mv */
+  uint8_t prev_value;  /* Input (mv_access is a Write): its prev_value; 0 otherwise */
+  uint8_t _pad[2];
+} bfz_cycle;
+int bfz_record_from_cycles(const bfz_pk* pk, const bfz_cycle* cycles, size_t n_cycles,
+                           const bfz_memory_event* memory, size_t n_memory, bfz_record** rec);
+
 /* One proof sharded over `world` GPUs (one process per GPU, every rank calls this with the
  * same record): each rank computes its residue-class row shard of every large LDE, hashes its
  * subtree of every large Merkle tree, evaluates the quotient at its points and computes its

@@ -308,7 +308,8 @@ def test_event_struct_layouts_match_header(tmp_path):
     import subprocess
     from bfz import events as E
     checks = {"bfz_cpu_event": E.CPU, "bfz_alu_event": E.ALU, "bfz_jump_event": E.JUMP,
-              "bfz_mem_instr_event": E.MEM_INSTR, "bfz_io_event": E.IO, "bfz_memory_event": E.MEMORY}
+              "bfz_mem_instr_event": E.MEM_INSTR, "bfz_io_event": E.IO, "bfz_memory_event": E.MEMORY,
+              "bfz_cycle": E.CYCLE}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{ROOT}/include/bfz.h"',
              "int main(void) {"]
     for st, dt in checks.items():

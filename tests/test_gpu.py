@@ -335,6 +335,7 @@ def test_fibo_x4_2pow22_bytes_match_oracle(client):
     rec = events.ExecutionRecordArrays.from_executor(guests.FIBO_X4, [255])
     assert len(rec.cpu) == 3767729
     assert _record_proof(pk, rec) == ref
+    assert _record_proof(pk, rec, cycles=True) == ref  # the compact hand-over (16 B per cycle)
     bc = sdk.proof_to_bincode(a.proof)
     client.verify_bincode(bc, vk)
     assert sdk.proof_from_bincode(bc) == a.proof
@@ -450,9 +451,10 @@ def test_pk_to_device_refuses_a_wrong_commit():
     assert dpk.commit == vk.commit
 
 
-def _record_proof(pk, rec):
+def _record_proof(pk, rec, cycles=False):
     from bfz import events
-    drec = events.record_from_events(pk, rec)
+    drec = (events.record_from_cycles(pk, events.cycles_from_record(rec), rec.memory) if cycles
+            else events.record_from_events(pk, rec))
     ptr = ctypes.POINTER(ctypes.c_uint8)()
     n = ctypes.c_size_t()
     _lib.check(_lib.lib().bfz_record_prove(ctypes.c_void_p(pk.handle), ctypes.c_void_p(drec.handle),
@@ -551,3 +553,47 @@ def test_device_transcript_divergence_is_an_error(client, monkeypatch):
     monkeypatch.delenv("BFZ_FAULT_DEVICE_CHALLENGER")
     pf = client.prove(pk, stdin).run()
     assert pf.proof == O.prove(prog, stdin)
+
+
+@pytest.mark.parametrize("name,prog,stdin", guests.REFERENCE_PROGRAMS + [("fibo255", guests.FIBO, [255])])
+def test_record_from_cycles_matches_oracle(client, name, prog, stdin):
+    """bfz_record_from_cycles: 16 B per cycle + the memory events; the device
+    rebuilds every CpuEvent field and the add/jump/memory_instr/io events (executor.rs:108-239)
+    and the proof is the oracle's -- also with the memory events in reverse order."""
+    from bfz import events
+    pk, vk = client.setup(prog)
+    rec = events.ExecutionRecordArrays.from_executor(prog, stdin)
+    want = O.prove(prog, stdin)
+    assert _record_proof(pk, rec, cycles=True) == want, name
+    if len(rec.memory) > 1:
+        rec.memory = np.ascontiguousarray(rec.memory[::-1])
+        assert _record_proof(pk, rec, cycles=True) == want, name
+
+
+def test_record_from_cycles_refuses_cycles_no_record_holds(client):
+    """Cycles a reference record cannot hold are refused before any trace kernel runs (pc past
+    the program, an access on a memory step, a previous timestamp at or after the cycle's own,
+    a prev_value outside an Input, padding), and the library keeps working."""
+    from bfz import events
+    prog, stdin = guests.FIBO, [17]
+    pk, vk = client.setup(prog)
+    rec = events.ExecutionRecordArrays.from_executor(prog, stdin)
+    cyc = events.cycles_from_record(rec)
+    ops = np.array([{"[": 0, "]": 1, "+": 2, "-": 3, ">": 4, "<": 5, ",": 6, ".": 7}[ch]
+                    for ch in prog if ch in "[]+-><,."])
+    op = ops[cyc["pc"]]
+    mem_step = int(np.flatnonzero((op == 4) | (op == 5))[0])
+    alu = int(np.flatnonzero((op == 2) | (op == 3))[3])
+    for idx, field, val in ((5, "pc", len(ops)), (mem_step, "mv", 1), (mem_step, "prev_ts", 1),
+                            (alu, "prev_ts", 2 * alu + 1), (alu, "prev_value", 9)):
+        bad = cyc.copy()
+        bad[idx][field] = val
+        with pytest.raises(_lib.BfzError, match="out of range"):
+            events.record_from_cycles(pk, bad, rec.memory)
+    raw = cyc.view(np.uint8).reshape(len(cyc), 16).copy()
+    raw[3, 15] = 1
+    with pytest.raises(_lib.BfzError, match="out of range"):
+        events.record_from_cycles(pk, raw.view(events.CYCLE).reshape(-1), rec.memory)
+    with pytest.raises(_lib.BfzError, match="no cycles"):
+        events.record_from_cycles(pk, cyc[:0], rec.memory)
+    assert _record_proof(pk, rec, cycles=True) == O.prove(prog, stdin)

@@ -43,6 +43,10 @@ IO = _dt([("pc", "<u4", 0), ("opcode", "u1", 4), ("mp", "<u4", 8), ("mv", "u1", 
 MEMORY = _dt([("addr", "<u4", 0), ("initial_timestamp", "<u4", 4), ("final_timestamp", "<u4", 8),
               ("initial_value", "u1", 12), ("final_value", "u1", 13)], 16)
 
+# bfz_cycle: the compact hand-over of bfz_record_from_cycles (16 B per cycle)
+CYCLE = _dt([("pc", "<u4", 0), ("mp", "<u4", 4), ("prev_ts", "<u4", 8), ("mv", "u1", 12),
+             ("prev_value", "u1", 13)], 16)
+
 # bfz_execute_events stream: the same fields packed (no padding), in declaration order
 _P_ACCESS = [("kind", "u1"), ("value", "u1"), ("prev_value", "u1"), ("timestamp", "<u4"),
              ("prev_timestamp", "<u4")]
@@ -125,6 +129,25 @@ class ExecutionRecordArrays:
         return ev
 
 
+INPUT = 6  # Opcode::Input (the only cycle whose mv_access is a write)
+
+
+def cycles_from_record(rec: "ExecutionRecordArrays") -> np.ndarray:
+    """The compact hand-over of bfz_record_from_cycles built from the record's cpu_events -- what
+    the Rust HipProver's CycleArrays::new does over record.cpu_events: pc, mp, mv, the
+    mv_access's prev_timestamp (0 when it is None) and, for a write (Input), its prev_value.
+    Everything else in the record is rebuilt on the device."""
+    cpu = rec.cpu
+    out = np.zeros(len(cpu), dtype=CYCLE)
+    out["pc"] = cpu["pc"]
+    out["mp"] = cpu["mp"]
+    out["mv"] = cpu["mv"]
+    out["prev_ts"] = cpu["mv_access_prev_timestamp"]
+    write = cpu["mv_access_kind"] == 2
+    out["prev_value"] = np.where(write, cpu["mv_access_prev_value"], 0)
+    return out
+
+
 class DeviceRecord:
     """bfz_record: the events resident in HBM (freed on drop)."""
 
@@ -144,5 +167,19 @@ def record_from_events(pk, rec: ExecutionRecordArrays) -> DeviceRecord:
     c = rec.as_c()
     out = ctypes.c_void_p()
     check(lib().bfz_record_from_events(ctypes.c_void_p(pk.handle), ctypes.byref(c),
+                                       ctypes.byref(out)))
+    return DeviceRecord(out.value)
+
+
+def record_from_cycles(pk, cycles: np.ndarray, memory: np.ndarray) -> DeviceRecord:
+    """bfz_record_from_cycles: the compact per-cycle hand-over (16 B per cycle) + the memory
+    events; the device rebuilds the CpuEvents and every chip's events, then validates them."""
+    _lib.init()
+    assert cycles.dtype == CYCLE and cycles.flags["C_CONTIGUOUS"]
+    assert memory.dtype == MEMORY and memory.flags["C_CONTIGUOUS"]
+    out = ctypes.c_void_p()
+    check(lib().bfz_record_from_cycles(ctypes.c_void_p(pk.handle),
+                                       cycles.ctypes.data if len(cycles) else None, len(cycles),
+                                       memory.ctypes.data if len(memory) else None, len(memory),
                                        ctypes.byref(out)))
     return DeviceRecord(out.value)

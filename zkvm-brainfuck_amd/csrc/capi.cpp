@@ -701,6 +701,31 @@ void put_events(bfz::DBuf<D>& d, const C* src, size_t n, hipStream_t st) {
   d.reset(std::max<size_t>(n, 1));
   bfz::upload_bulk(d.p, src, n * sizeof(D), st);
 }
+// cpu_memory_access in the normal form: sorted by address (the reference's order is that of a
+// HashMap drain, executor.rs:74); one event per address.  Returns the count.
+size_t put_memory_events(bfz::DeviceEvents& ev, const bfz_memory_event* src, size_t n, hipStream_t st) {
+  if (n && !src) throw std::runtime_error("record_from_events: null event array");
+  std::vector<bfz::MemoryEvent> mem(n);
+  if (n) std::memcpy(mem.data(), src, n * sizeof(bfz::MemoryEvent));
+  std::sort(mem.begin(), mem.end(), [](const bfz::MemoryEvent& a, const bfz::MemoryEvent& b) {
+    return a.addr < b.addr;
+  });
+  for (size_t i = 1; i < mem.size(); i++)
+    if (mem[i].addr == mem[i - 1].addr)
+      throw std::runtime_error("record_from_events: two memory events for one address");
+  put_events(ev.memory, mem.data(), mem.size(), st);
+  return mem.size();
+}
+const bfz::Program& put_program(bfz::DeviceEvents& ev, const bfz::Program& prog, hipStream_t st) {
+  ev.prog.reset(std::max<size_t>(prog.instructions.size(), 1));
+  HIP_CHECK(hipMemcpyAsync(ev.prog.p, prog.instructions.data(),
+                           prog.instructions.size() * sizeof(bfz::Instruction), hipMemcpyHostToDevice, st));
+  return prog;
+}
+static_assert(sizeof(bfz_cycle) == sizeof(bfz::Cycle) && offsetof(bfz_cycle, prev_ts) == offsetof(bfz::Cycle, prev_ts) &&
+                  offsetof(bfz_cycle, mv) == offsetof(bfz::Cycle, mv) &&
+                  offsetof(bfz_cycle, prev_value) == offsetof(bfz::Cycle, prev_value),
+              "bfz.h bfz_cycle must match machine.h Cycle");
 }  // namespace
 extern "C" {
 
@@ -726,36 +751,54 @@ int bfz_record_from_events(const bfz_pk* pk, const bfz_events* e, bfz_record** r
     put_events(ev.jump, e->jump, e->n_jump, st);
     put_events(ev.meminstr, e->memory_instr, e->n_memory_instr, st);
     put_events(ev.io, e->io, e->n_io, st);
-    // cpu_memory_access in the normal form: sorted by address (the reference's order is that of
-    // a HashMap drain, executor.rs:74); one event per address
-    if (e->n_memory && !e->memory) throw std::runtime_error("record_from_events: null event array");
-    std::vector<bfz::MemoryEvent> mem(e->n_memory);
-    if (e->n_memory) std::memcpy(mem.data(), e->memory, mem.size() * sizeof(bfz::MemoryEvent));
-    std::sort(mem.begin(), mem.end(), [](const bfz::MemoryEvent& a, const bfz::MemoryEvent& b) {
-      return a.addr < b.addr;
-    });
-    for (size_t i = 1; i < mem.size(); i++)
-      if (mem[i].addr == mem[i - 1].addr)
-        throw std::runtime_error("record_from_events: two memory events for one address");
-    put_events(ev.memory, mem.data(), mem.size(), st);
-    const bfz::Program& prog = pk->pk->program;
-    ev.prog.reset(std::max<size_t>(prog.instructions.size(), 1));
-    HIP_CHECK(hipMemcpyAsync(ev.prog.p, prog.instructions.data(),
-                             prog.instructions.size() * sizeof(bfz::Instruction),
-                             hipMemcpyHostToDevice, st));
+    const size_t nmem = put_memory_events(ev, e->memory, e->n_memory, st);
+    const bfz::Program& prog = put_program(ev, pk->pk->program, st);
     bfz::EventCounts n;
     n.cpu = e->n_cpu;
     n.alu = nalu;
     n.jump = e->n_jump;
     n.meminstr = e->n_memory_instr;
     n.io = e->n_io;
-    n.memory = mem.size();
+    n.memory = nmem;
     n.program = prog.instructions.size();
     bfz::set_event_meta(ev, n, e->n_cpu);
     if (const size_t bad = bfz::count_invalid_events(ev, st))
       throw std::runtime_error("record_from_events: " + std::to_string(bad) +
                                " events out of range (pc outside the program, opcode or access kind)");
     r->cycles = e->n_cpu;
+    *rec = r.release();
+    return 0;
+  });
+}
+
+int bfz_record_from_cycles(const bfz_pk* pk, const bfz_cycle* cycles, size_t n_cycles,
+                           const bfz_memory_event* memory, size_t n_memory, bfz_record** rec) {
+  return guarded([&] {
+    if (!pk || !rec) throw std::runtime_error("null argument");
+    if (n_cycles == 0) throw std::runtime_error("record_from_cycles: no cycles");
+    if (!cycles) throw std::runtime_error("record_from_cycles: null cycle array");
+    const size_t lim = (size_t)1 << 26;  // beyond any committable trace (2^23 rows)
+    if (n_cycles > lim || n_memory > 2 * lim)
+      throw std::runtime_error("record_from_cycles: event count out of range");
+    hipStream_t st = bfz::stream();
+    auto r = std::make_unique<bfz_record>();
+    bfz::DeviceEvents& ev = r->ev;
+    const bfz::Program& prog = put_program(ev, pk->pk->program, st);
+    ev.n[bfz::CHIP_PROGRAM] = prog.instructions.size();
+    bfz::DBuf<bfz::Cycle> d(n_cycles);
+    bfz::upload_bulk(d.p, cycles, n_cycles * sizeof(bfz::Cycle), st);
+    const size_t nmem = put_memory_events(ev, memory, n_memory, st);
+    bfz::EventCounts n;
+    size_t bad = 0;
+    bfz::expand_cycles(d.p, n_cycles, ev, n, &bad, st);
+    if (bad)
+      throw std::runtime_error("record_from_cycles: " + std::to_string(bad) +
+                               " cycles out of range (pc outside the program, or fields a "
+                               "reference record cannot hold)");
+    n.memory = nmem;
+    n.program = prog.instructions.size();
+    bfz::set_event_meta(ev, n, n_cycles);
+    r->cycles = n_cycles;
     *rec = r.release();
     return 0;
   });

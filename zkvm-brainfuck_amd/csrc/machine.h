@@ -39,6 +39,14 @@ struct JumpEvent { uint32_t pc, next_pc; uint8_t opcode; uint32_t dst; uint8_t m
 struct MemInstrEvent { uint32_t clk, pc; uint8_t opcode; uint32_t mp, next_mp; };
 struct IoEvent { uint32_t pc; uint8_t opcode; uint32_t mp; uint8_t mv; };
 struct MemoryEvent { uint32_t addr, init_ts, final_ts; uint8_t init_v, final_v; };
+// One executed cycle in the compact hand-over form (include/bfz.h bfz_cycle): every other field
+// of the CpuEvent and every chip event of the cycle follow from these, the next cycle and the
+// program (executor.rs:108-129,196-239); tracegen.hip expand_cycles rebuilds them on the device.
+struct Cycle {
+  uint32_t pc, mp, prev_ts;  // pc, mp, mv_access.prev_timestamp (0 without an access)
+  uint8_t mv, prev_value;    // mv; Input: the cell's value before the write
+  uint8_t pad[2];
+};
 
 struct ExecutionRecord {
   const Program* program = nullptr;

@@ -36,6 +36,15 @@ void set_event_meta(DeviceEvents& ev, const EventCounts& n, uint64_t global_clk)
 // not read -- a cpu pc outside the program (k_trace_cpu / k_deps index by it), an opcode or
 // memory-access kind out of range.  Counted on the device after the upload.
 size_t count_invalid_events(const DeviceEvents& ev, hipStream_t st);
+// The record's event vectors from the compact per-cycle form (bfz_record_from_cycles): d holds
+// n cycles in HBM, ev.prog the program (uploaded by the caller).  Fills ev.cpu, ev.alu, ev.jump,
+// ev.meminstr, ev.io on the device (chip events in cycle order, as the executor pushes them) and
+// returns their counts in n_out (cpu, alu, jump, meminstr, io); *invalid = cycles that are not
+// a reference record's (pc outside the program, a memory step with an access, a previous
+// timestamp at or after the cycle's own, a prev_value outside an Input, nonzero padding).  The
+// kernels never index the program with an out-of-range pc.
+void expand_cycles(const Cycle* d, size_t n, DeviceEvents& ev, EventCounts& n_out, size_t* invalid,
+                   hipStream_t st);
 // Pinned host memory for HostEvents (hipHostMalloc / hipHostFree).
 void* pinned_alloc(size_t bytes);
 void pinned_free(void* p);

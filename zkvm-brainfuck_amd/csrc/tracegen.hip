@@ -403,6 +403,197 @@ size_t count_invalid_events(const DeviceEvents& ev, hipStream_t st) {
   return h;
 }
 
+// ------------------------------------------------------------ compact cycles -> events
+namespace {
+constexpr int XB = 256;  // cycles per block of the expansion passes
+enum { CAT_ALU = 0, CAT_JUMP, CAT_MEM, CAT_IO, NCAT };
+__device__ __forceinline__ int cat_of(int op) {
+  return (op == OP_ADD || op == OP_SUB)              ? CAT_ALU
+         : (op == OP_LOOP_START || op == OP_LOOP_END) ? CAT_JUMP
+         : (op == OP_MEM_FWD || op == OP_MEM_BWD)     ? CAT_MEM
+                                                      : CAT_IO;
+}
+// A cycle the reference executor could have emitted (executor.rs:108-239): memory steps have
+// no access (mv = 0), only Input writes (prev_value), and an access's previous timestamp lies
+// before the cycle's first access at clk + 1.
+__device__ __forceinline__ bool cycle_ok(const Cycle& c, uint32_t clk, int cat, int op) {
+  if (c.pad[0] | c.pad[1]) return false;
+  if (cat == CAT_MEM) return c.mv == 0 && c.prev_ts == 0 && c.prev_value == 0;
+  if (op != OP_INPUT && c.prev_value != 0) return false;
+  return c.prev_ts <= clk;
+}
+__device__ __forceinline__ uint64_t lanes_below() {
+  return (1ull << __lane_id()) - 1ull;  // lane_id < 64
+}
+
+// Pass 1: each block's count per category; invalid cycles counted into cnt[NCAT].
+__global__ __launch_bounds__(XB) void k_cycles_count(const Cycle* __restrict__ cyc, size_t n,
+                                                     const Instruction* __restrict__ prog,
+                                                     uint32_t nprog, uint32_t* __restrict__ bc,
+                                                     uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t wc[XB / 64][NCAT];
+  const size_t i = (size_t)blockIdx.x * XB + threadIdx.x;
+  int cat = -1;
+  bool bad = false;
+  if (i < n) {
+    const Cycle c = cyc[i];
+    if (c.pc >= nprog) {
+      bad = true;
+    } else {
+      const int op = prog[c.pc].opcode;
+      cat = cat_of(op);
+      bad = !cycle_ok(c, (uint32_t)(2 * i), cat, op);
+    }
+  }
+  const int wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NCAT; k++) {
+    const uint32_t m = (uint32_t)__popcll(__ballot(cat == k));
+    if (__lane_id() == 0) wc[wv][k] = m;
+  }
+  const uint32_t nb = (uint32_t)__popcll(__ballot(bad));
+  if (__lane_id() == 0 && nb) atomicAdd(&cnt[NCAT], nb);
+  __syncthreads();
+  if (threadIdx.x < NCAT) {
+    uint32_t t = 0;
+    for (int w = 0; w < XB / 64; w++) t += wc[w][threadIdx.x];
+    bc[(size_t)blockIdx.x * NCAT + threadIdx.x] = t;
+  }
+}
+
+// Pass 2 (one block): exclusive scan of the block counts per category, totals into cnt[0..NCAT).
+__global__ __launch_bounds__(1024) void k_cycles_scan(uint32_t* __restrict__ bc, size_t nb,
+                                                      uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t part[1024][NCAT];
+  const size_t per = (nb + 1023) / 1024;
+  const size_t b0 = threadIdx.x * per, b1 = b0 + per < nb ? b0 + per : nb;
+  uint32_t s[NCAT] = {};
+  for (size_t b = b0; b < b1; b++)
+#pragma unroll
+    for (int k = 0; k < NCAT; k++) s[k] += bc[b * NCAT + k];
+#pragma unroll
+  for (int k = 0; k < NCAT; k++) part[threadIdx.x][k] = s[k];
+  __syncthreads();
+  if (threadIdx.x < NCAT) {  // 1024 chunk sums per category, serially (tiny)
+    uint32_t run = 0;
+    for (int t = 0; t < 1024; t++) {
+      const uint32_t v = part[t][threadIdx.x];
+      part[t][threadIdx.x] = run;
+      run += v;
+    }
+    cnt[threadIdx.x] = run;
+  }
+  __syncthreads();
+  uint32_t run[NCAT];
+#pragma unroll
+  for (int k = 0; k < NCAT; k++) run[k] = part[threadIdx.x][k];
+  for (size_t b = b0; b < b1; b++)
+#pragma unroll
+    for (int k = 0; k < NCAT; k++) {
+      const uint32_t v = bc[b * NCAT + k];
+      bc[b * NCAT + k] = run[k];
+      run[k] += v;
+    }
+}
+
+// Pass 3: the CpuEvent of every cycle and its chip event at its category's running position.
+__global__ __launch_bounds__(XB) void k_cycles_expand(const Cycle* __restrict__ cyc, size_t n,
+                                                      const Instruction* __restrict__ prog,
+                                                      uint32_t nprog, const uint32_t* __restrict__ bc,
+                                                      CpuEvent* __restrict__ cpu, AluEvent* __restrict__ alu,
+                                                      JumpEvent* __restrict__ jump,
+                                                      MemInstrEvent* __restrict__ mi,
+                                                      IoEvent* __restrict__ io) {
+  __shared__ uint32_t wc[XB / 64][NCAT];
+  const size_t i = (size_t)blockIdx.x * XB + threadIdx.x;
+  Cycle c{};
+  int op = 0, cat = -1;
+  if (i < n) {
+    c = cyc[i];
+    if (c.pc < nprog) {  // an out-of-range pc fails the whole call (pass 1): write nothing
+      op = prog[c.pc].opcode;
+      cat = cat_of(op);
+    }
+  }
+  const int wv = threadIdx.x >> 6;
+  uint32_t rank = 0;
+#pragma unroll
+  for (int k = 0; k < NCAT; k++) {
+    const uint64_t m = __ballot(cat == k);
+    if (cat == k) rank = (uint32_t)__popcll(m & lanes_below());
+    if (__lane_id() == 0) wc[wv][k] = (uint32_t)__popcll(m);
+  }
+  __syncthreads();
+  if (cat < 0) return;
+  uint32_t pos = bc[(size_t)blockIdx.x * NCAT + cat] + rank;
+  for (int w = 0; w < wv; w++) pos += wc[w][cat];
+  const uint32_t clk = (uint32_t)(2 * i);
+  const bool last = i + 1 == n;
+  const Cycle nx = last ? c : cyc[i + 1];
+  CpuEvent e{};
+  e.clk = clk;
+  e.pc = c.pc;
+  e.mp = c.mp;
+  e.mv = c.mv;
+  e.next_pc = last ? nprog : nx.pc;  // the run ends when pc reaches the program's end
+  e.next_mp = !last ? nx.mp : op == OP_MEM_FWD ? c.mp + 1 : op == OP_MEM_BWD ? c.mp - 1 : c.mp;
+  e.next_mv = op == OP_ADD ? (uint8_t)(c.mv + 1) : op == OP_SUB ? (uint8_t)(c.mv - 1) : (uint8_t)0;
+  if (cat != CAT_MEM) {  // rr_cpu / rw_cpu at clk + 1 (executor.rs:145-205)
+    e.mv_access.kind = op == OP_INPUT ? 2 : 1;
+    e.mv_access.value = c.mv;
+    e.mv_access.prev_value = op == OP_INPUT ? c.prev_value : c.mv;
+    e.mv_access.ts = clk + 1;
+    e.mv_access.prev_ts = c.prev_ts;
+  }
+  if (cat == CAT_ALU) {  // the write of next_mv at clk + 2 (executor.rs:148-158)
+    e.next_mv_access.kind = 2;
+    e.next_mv_access.value = e.next_mv;
+    e.next_mv_access.prev_value = c.mv;
+    e.next_mv_access.ts = clk + 2;
+    e.next_mv_access.prev_ts = clk + 1;
+  }
+  cpu[i] = e;
+  switch (cat) {  // emit_events (executor.rs:196-239)
+    case CAT_ALU: alu[pos] = AluEvent{c.pc, (uint8_t)op, e.next_mv, c.mv}; break;
+    case CAT_JUMP: jump[pos] = JumpEvent{c.pc, e.next_pc, (uint8_t)op, e.next_pc, c.mv}; break;
+    case CAT_MEM: mi[pos] = MemInstrEvent{clk, c.pc, (uint8_t)op, c.mp, e.next_mp}; break;
+    default: io[pos] = IoEvent{c.pc, (uint8_t)op, c.mp, c.mv}; break;
+  }
+}
+}  // namespace
+
+void expand_cycles(const Cycle* d, size_t n, DeviceEvents& ev, EventCounts& n_out, size_t* invalid,
+                   hipStream_t st) {
+  if (n == 0 || n > ((size_t)1 << 30)) throw std::runtime_error("expand_cycles: cycle count out of range");
+  const uint32_t nprog = (uint32_t)ev.n[CHIP_PROGRAM];
+  const size_t nb = ceil_div(n, XB);
+  DBuf<uint32_t> bc(nb * NCAT), cnt(NCAT + 1);
+  HIP_CHECK(hipMemsetAsync(cnt.p, 0, (NCAT + 1) * 4, st));
+  hipLaunchKernelGGL(k_cycles_count, dim3((unsigned)nb), dim3(XB), 0, st, d, n,
+                     (const Instruction*)ev.prog.p, nprog, bc.p, cnt.p);
+  KCHECK();
+  hipLaunchKernelGGL(k_cycles_scan, dim3(1), dim3(1024), 0, st, bc.p, nb, cnt.p);
+  KCHECK();
+  uint32_t h[NCAT + 1];
+  fetch(h, cnt.p, sizeof h, st);
+  *invalid = h[NCAT];
+  n_out.cpu = n;
+  n_out.alu = h[CAT_ALU];
+  n_out.jump = h[CAT_JUMP];
+  n_out.meminstr = h[CAT_MEM];
+  n_out.io = h[CAT_IO];
+  ev.cpu.reset(n);
+  ev.alu.reset(std::max<size_t>(n_out.alu, 1));
+  ev.jump.reset(std::max<size_t>(n_out.jump, 1));
+  ev.meminstr.reset(std::max<size_t>(n_out.meminstr, 1));
+  ev.io.reset(std::max<size_t>(n_out.io, 1));
+  if (*invalid) return;
+  hipLaunchKernelGGL(k_cycles_expand, dim3((unsigned)nb), dim3(XB), 0, st, d, n,
+                     (const Instruction*)ev.prog.p, nprog, (const uint32_t*)bc.p, ev.cpu.p, ev.alu.p,
+                     ev.jump.p, ev.meminstr.p, ev.io.p);
+  KCHECK();
+}
+
 void* pinned_alloc(size_t bytes) {
   void* p = nullptr;
   if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
