@@ -497,9 +497,11 @@ def main():
     ap.add_argument("--sustain-s", type=float, default=8.0,
                     help="replicas mode: seconds of back-to-back proofs after the timed steps "
                          "(0 = skip)")
-    ap.add_argument("--solo-world", type=int, default=0,
+    ap.add_argument("--solo-world", default="2,4,8",
                     help="replicas mode at N=1: also time each rank's share of an N-GPU sharded "
-                         "proof alone (bfz_record_prove_shard_solo), N = this value (0 = skip)")
+                         "proof alone (bfz_record_prove_shard_solo) for each N of this "
+                         "comma-separated list -- the predicted strong-scaling curve of one proof "
+                         "before collective time ('' or 0 = skip)")
     ap.add_argument("--log-n", type=int, default=24, help="pcs mode: trace rows = 2^log_n")
     ap.add_argument("--cols", type=int, default=64, help="pcs mode: trace columns")
     args = ap.parse_args()
@@ -639,8 +641,18 @@ def main():
             line["sustained"] = extra["sustained"]
         if world > 1 and not sharded and not args.no_extra and "sharded_proof" in extra:
             line["sharded_proof"] = extra["sharded_proof"]
-        if world == 1 and args.solo_world > 1:
-            line["shard_solo"] = shard_solo(pk, rec, args.solo_world)
+        solo = [int(x) for x in str(args.solo_world).split(",") if x.strip() and int(x) > 1]
+        if world == 1 and solo:
+            runs = {n: shard_solo(pk, rec, n) for n in solo}
+            curve = {"1": round(ms, 3)}
+            curve.update({str(n): runs[n]["max_rank_ms"] for n in solo})
+            line["shard_solo_curve"] = {
+                "ms_per_proof_by_gpus": curve,
+                "speedup_by_gpus": {k: round(ms / v, 2) for k, v in curve.items()},
+                "what": "one proof split over N GPUs, predicted: N = 1 is the timed single-GPU "
+                        "proof; N > 1 is the slowest rank's share run alone on this GPU with "
+                        "no-op exchanges (bfz_record_prove_shard_solo), before collective time",
+                "ranks": {str(n): runs[n]["ranks"] for n in solo}}
         if world == 1 and not args.no_extra:
             line["end_to_end"] = end_to_end(client, pk, prog, stdin)
             line["events_path"] = events_path(pk, prog, stdin, proof)

@@ -99,11 +99,13 @@ def test_sharded_proof_is_bit_exact(world, fri_min):
 
 
 @pytest.mark.slow
-def test_sharded_headline_two_ranks_is_bit_exact():
-    """The headline workload (FIBO_X4 stdin [255], Cpu 2^22 rows) sharded over 2 ranks: both
-    ranks return the unsharded proof byte for byte (which test_gpu.py checks against the
-    oracle)."""
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_sharded_headline_is_bit_exact(world):
+    """The headline workload (FIBO_X4 stdin [255], Cpu 2^22 rows) sharded over 2, 4 and 8 ranks
+    -- the SCALE shapes; at 4 and 8 ranks every quotient point's next row lies in another
+    residue class, so the next-residue LDE shards run at 2^22 -- every rank returns the
+    unsharded proof byte for byte (which test_gpu.py checks against the oracle)."""
     from bfz import guests
-    res = _run(2, [(guests.FIBO_X4, [255])])
-    assert res[0][0][0] == res[1][0][0], "ranks disagree"
+    res = _run(world, [(guests.FIBO_X4, [255])])
+    assert len({res[r][0][0] for r in range(world)}) == 1, "ranks disagree"
     assert res[0][0][0] == res[0][0][1], "sharded proof differs from the unsharded one"
