@@ -73,8 +73,8 @@ def test_poseidon2_lane_mode_parity():
     assert np.array_equal(got, O.poseidon2(st.reshape(-1)).reshape(-1, 16))
 
 
-@pytest.mark.parametrize("logn,w", [(0, 3), (1, 2), (4, 31), (5, 1), (10, 45), (13, 7), (16, 4),
-                                    (17, 9), (20, 2)])
+@pytest.mark.parametrize("logn,w", [(0, 3), (1, 2), (4, 31), (5, 1), (10, 45), (13, 7), (14, 5),
+                                    (16, 4), (17, 9), (18, 3), (20, 2), (22, 1)])
 def test_coset_lde_parity(logn, w):
     rng = np.random.default_rng(logn * 100 + w)
     n = 1 << logn
@@ -85,6 +85,37 @@ def test_coset_lde_parity(logn, w):
                                         out.ctypes.data_as(P32)))
     exp = O.coset_lde(m, 3)
     assert np.array_equal(unmont(out), exp)
+
+
+_MFMA_LDE_CHECK = """
+import sys, ctypes, numpy as np
+sys.path[:0] = [sys.argv[1] + "/zkvm-brainfuck_amd", sys.argv[1] + "/tests"]
+import oracle_lib as O
+from bfz import _lib
+_lib.init(0)
+P = O.P
+for logn, w in ((14, 3), (18, 3), (22, 1)):
+    n = 1 << logn
+    m = np.random.default_rng(logn).integers(0, P, size=(n, w), dtype=np.uint64).astype(np.uint32)
+    src = ((m.astype(np.uint64) << np.uint64(32)) % np.uint64(P)).astype(np.uint32)
+    out = np.zeros((2 * n, w), dtype=np.uint32)
+    P32 = ctypes.POINTER(ctypes.c_uint32)
+    _lib.check(_lib.lib().bfz_coset_lde(src.ctypes.data_as(P32), n, w, (3 << 32) % P,
+                                        out.ctypes.data_as(P32)))
+    got = ((out.astype(np.uint64) * np.uint64(pow(2, -32, P))) % np.uint64(P)).astype(np.uint32)
+    assert np.array_equal(got, O.coset_lde(m, 3)), (logn, w)
+print("ok")
+"""
+
+
+def test_mfma_tiles_lde_parity():
+    """The matrix-core 2^14 tile passes (BFZ_NTT_MFMA=1, the A/B alternative to the VALU tiles,
+    read once per process: hence a child process) against the oracle's coset LDE."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, "-c", _MFMA_LDE_CHECK, ROOT], capture_output=True,
+                       text=True, timeout=300, env=dict(os.environ, BFZ_NTT_MFMA="1"))
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
 
 
 def test_commit_root_parity():

@@ -64,6 +64,7 @@ bfz::ProveOptions opts() {
 template <class F>
 int guarded(F&& f) {
   std::lock_guard<std::mutex> lk(g_mu);
+  bfz::ApiLockScope held;  // open_impl's process-global pinned buffers rely on it
   try {
     return f();
   } catch (const bfz::HipError& e) {

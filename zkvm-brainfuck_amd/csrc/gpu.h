@@ -145,6 +145,13 @@ struct Twiddles {
 Twiddles& twiddles();
 
 hipStream_t stream();
+// Every C entry point runs under one process-wide API lock (capi.cpp guarded()); proof code
+// that keeps process-global state (open_impl's pinned mailboxes) checks that it is held.
+int& api_lock_depth();  // per thread
+struct ApiLockScope {
+  ApiLockScope() { api_lock_depth()++; }
+  ~ApiLockScope() { api_lock_depth()--; }
+};
 // Small host -> device copies inside a proof through a pinned arena (runtime.hip): no host
 // stall.  staging_reset() once no earlier copy can be pending (after a stream synchronize).
 void upload_async(void* dst, const void* src, size_t bytes, hipStream_t st);

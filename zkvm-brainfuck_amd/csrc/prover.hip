@@ -907,6 +907,10 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
                                                           rounds[r]->mats.back().lde.width);
     }
   std::vector<EF> opened(nvals);
+  // gev / gbox (and tbox below) are process-global and reallocated on the assumption that no
+  // copy into them is pending: safe only because every caller holds the API lock and every
+  // proof synchronizes before it returns.  A caller outside the lock is a bug.
+  if (api_lock_depth() == 0) throw std::logic_error("open_impl called outside the bfz API lock");
   static hipEvent_t gev[NGROUP] = {};
   static EF* gbox = nullptr;  // pinned: the groups' opened values
   static size_t gcap = 0;

@@ -222,6 +222,11 @@ Twiddles& twiddles() {
   return *t;
 }
 
+int& api_lock_depth() {
+  static thread_local int depth = 0;
+  return depth;
+}
+
 void Twiddles::ensure(int log_n) {
   if (log_n <= logmax) return;
   size_t N = (size_t)1 << log_n;
