@@ -276,8 +276,9 @@ def events_path(pk, prog, stdin, ref_proof, steps=3):
     conv = []
     for _ in range(3):
         t0 = _t.perf_counter()
-        cyc = _e.cycles_from_record(rec)
+        cyc = _e.cycles_from_record(rec, pinned=True)
         conv.append((_t.perf_counter() - t0) * 1e3)
+    cyc_pageable = _e.cycles_from_record(rec)
 
     def best(one):
         one()  # warm
@@ -290,6 +291,8 @@ def events_path(pk, prog, stdin, ref_proof, steps=3):
 
     ms, pf = best(lambda: prove(_e.record_from_cycles(pk, cyc, rec.memory)))
     assert pf == ref_proof, "compact-cycle proof differs from the record path"
+    ms_pageable, pf = best(lambda: prove(_e.record_from_cycles(pk, cyc_pageable, rec.memory)))
+    assert pf == ref_proof, "compact-cycle proof (pageable hand-over) differs from the record path"
     ms_full, pf = best(lambda: prove(_e.record_from_events(pk, rec)))
     assert pf == ref_proof, "events-path proof differs from the record path"
     nbytes = int(cyc.nbytes + rec.memory.nbytes)
@@ -299,12 +302,15 @@ def events_path(pk, prog, stdin, ref_proof, steps=3):
             "bytes_per_cycle": round(nbytes / len(rec.cpu), 2),
             "host_conversion_ms": round(min(conv), 3),
             "host_conversion_what": "cycles_from_record (numpy, one thread) over the record's "
-                                    f"{len(rec.cpu)} cpu_events",
+                                    f"{len(rec.cpu)} cpu_events, into bfz_host_alloc memory",
+            "pageable_ms": round(ms_pageable, 3),
             "full_events_ms": round(ms_full, 3), "full_event_bytes": full,
-            "what": "bfz_record_from_cycles (16 B per cycle + memory events from pageable host "
-                    f"memory, {nbytes / 1e6:.0f} MB) + bfz_record_prove: the Rust HipProver::prove "
-                    "path, upload and device event rebuild included; full_events_ms = the same "
-                    f"through bfz_record_from_events ({full / 1e6:.0f} MB)"}
+            "what": "bfz_record_from_cycles (16 B per cycle in page-locked bfz_host_alloc memory, "
+                    f"as the Rust CycleArrays builds it, + memory events; {nbytes / 1e6:.0f} MB) + "
+                    "bfz_record_prove: the Rust HipProver::prove path, upload and device event "
+                    "rebuild included; pageable_ms = the same hand-over from pageable memory "
+                    "(staged through the library's pinned chunks); full_events_ms = the full "
+                    f"events through bfz_record_from_events ({full / 1e6:.0f} MB, pageable)"}
 
 
 SHARDED_EXTRA_LIMIT_S = 150

@@ -297,12 +297,46 @@ impl EventArrays {
     }
 }
 
+/// `n` values of `T` in page-locked host memory (`bfz_host_alloc`): libbfz DMAs a hand-over
+/// array straight from it instead of staging it through its own pinned chunks.
+struct PinnedVec<T: Copy> {
+    ptr: *mut T,
+    len: usize,
+}
+
+impl<T: Copy> PinnedVec<T> {
+    fn new(len: usize) -> Self {
+        let mut p = core::ptr::null_mut();
+        sys::check(unsafe { sys::bfz_host_alloc(len.max(1) * core::mem::size_of::<T>(), &mut p) });
+        Self { ptr: p as *mut T, len }
+    }
+    fn as_ptr(&self) -> *const T {
+        self.ptr
+    }
+    fn len(&self) -> usize {
+        self.len
+    }
+    /// Every element is written before it is read (the caller fills the whole slice).
+    fn as_mut_slice(&mut self) -> &mut [T] {
+        unsafe { core::slice::from_raw_parts_mut(self.ptr, self.len) }
+    }
+}
+
+impl<T: Copy> Drop for PinnedVec<T> {
+    fn drop(&mut self) {
+        unsafe { sys::bfz_host_free(self.ptr as *mut core::ffi::c_void) };
+    }
+}
+
+unsafe impl<T: Copy + Send> Send for PinnedVec<T> {}
+
 /// The compact hand-over of `bfz_record_from_cycles`: one 16-byte `bfz_cycle` per CpuEvent
 /// plus the memory events.  The device rebuilds the CpuEvents' derived fields and every chip's
 /// events (add/jump/memory_instr/io are the cycles' own fields, executor.rs:196-239), so about
-/// 16 B per cycle cross PCIe instead of ~64 B.
+/// 16 B per cycle cross PCIe instead of ~64 B.  The cycles are written in parallel straight into
+/// page-locked memory, so the upload is one DMA.
 struct CycleArrays {
-    cycles: Vec<sys::bfz_cycle>,
+    cycles: PinnedVec<sys::bfz_cycle>,
     memory: Vec<sys::bfz_memory_event>,
 }
 
@@ -316,8 +350,14 @@ impl CycleArrays {
             };
             sys::bfz_cycle { pc: e.pc, mp: e.mp, prev_ts, mv: e.mv, prev_value, _pad: [0; 2] }
         };
+        let mut cycles = PinnedVec::new(r.cpu_events.len());
+        cycles
+            .as_mut_slice()
+            .par_iter_mut()
+            .zip(r.cpu_events.par_iter())
+            .for_each(|(o, e)| *o = cycle(e));
         Self {
-            cycles: r.cpu_events.par_iter().map(cycle).collect(),
+            cycles,
             // HashMap-drain order (executor.rs:74); libbfz sorts it into the normal form
             memory: r
                 .cpu_memory_access

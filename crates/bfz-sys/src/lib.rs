@@ -245,6 +245,8 @@ extern "C" {
     pub fn bfz_record_from_cycles(pk: *const bfz_pk, cycles: *const bfz_cycle, n_cycles: usize,
                                   memory: *const bfz_memory_event, n_memory: usize,
                                   rec: *mut *mut bfz_record) -> c_int;
+    pub fn bfz_host_alloc(bytes: usize, out: *mut *mut c_void) -> c_int;
+    pub fn bfz_host_free(p: *mut c_void);
     pub fn bfz_record_prove_sharded(pk: *const bfz_pk, rec: *const bfz_record, rank: c_int,
                                     world: c_int, allgather: bfz_allgather_fn,
                                     allreduce_sum: bfz_allreduce_u32_fn, ctx: *mut c_void,

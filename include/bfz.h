@@ -285,6 +285,15 @@ typedef struct {
 int bfz_record_from_cycles(const bfz_pk* pk, const bfz_cycle* cycles, size_t n_cycles,
                            const bfz_memory_event* memory, size_t n_memory, bfz_record** rec);
 
+/* Page-locked host memory for the hand-over arrays (the Rust CycleArrays builds its bfz_cycle
+ * vector in it): bfz_record_from_cycles / bfz_record_from_events then DMA straight from the
+ * caller's array instead of staging it through the library's pinned chunks (PCIe-bound: ~60 GB/s
+ * against ~35-40 GB/s staged).  Any host memory is still accepted; this only makes the upload
+ * faster.  Pairs with bfz_host_free (not bfz_free).  Host-side replacement of the reference's
+ * Vec allocation in ExecutionRecord hand-off (crates/core/machine/src/utils/prove.rs:44-46). */
+int bfz_host_alloc(size_t bytes, void** out);
+void bfz_host_free(void* p);
+
 /* One proof sharded over `world` GPUs (one process per GPU, every rank calls this with the
  * same record): each rank computes its residue-class row shard of every large LDE, hashes its
  * subtree of every large Merkle tree, evaluates the quotient at its points and computes its

@@ -482,10 +482,10 @@ def test_pk_to_device_refuses_a_wrong_commit():
     assert dpk.commit == vk.commit
 
 
-def _record_proof(pk, rec, cycles=False):
+def _record_proof(pk, rec, cycles=False, pinned=False):
     from bfz import events
-    drec = (events.record_from_cycles(pk, events.cycles_from_record(rec), rec.memory) if cycles
-            else events.record_from_events(pk, rec))
+    drec = (events.record_from_cycles(pk, events.cycles_from_record(rec, pinned=pinned), rec.memory)
+            if cycles else events.record_from_events(pk, rec))
     ptr = ctypes.POINTER(ctypes.c_uint8)()
     n = ctypes.c_size_t()
     _lib.check(_lib.lib().bfz_record_prove(ctypes.c_void_p(pk.handle), ctypes.c_void_p(drec.handle),
@@ -590,12 +590,14 @@ def test_device_transcript_divergence_is_an_error(client, monkeypatch):
 def test_record_from_cycles_matches_oracle(client, name, prog, stdin):
     """bfz_record_from_cycles: 16 B per cycle + the memory events; the device
     rebuilds every CpuEvent field and the add/jump/memory_instr/io events (executor.rs:108-239)
-    and the proof is the oracle's -- also with the memory events in reverse order."""
+    and the proof is the oracle's -- also with the memory events in reverse order, and with the
+    cycles in page-locked bfz_host_alloc memory (one DMA, no staging)."""
     from bfz import events
     pk, vk = client.setup(prog)
     rec = events.ExecutionRecordArrays.from_executor(prog, stdin)
     want = O.prove(prog, stdin)
     assert _record_proof(pk, rec, cycles=True) == want, name
+    assert _record_proof(pk, rec, cycles=True, pinned=True) == want, name
     if len(rec.memory) > 1:
         rec.memory = np.ascontiguousarray(rec.memory[::-1])
         assert _record_proof(pk, rec, cycles=True) == want, name

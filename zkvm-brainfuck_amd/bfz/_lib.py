@@ -68,6 +68,8 @@ SIGNATURES = [
     ("bfz_build_id", c_char_p, []),
     ("bfz_device_name", c_int, [c_char_p, c_size_t]),
     ("bfz_free", None, [c_void_p]),
+    ("bfz_host_alloc", c_int, [c_size_t, ctypes.POINTER(c_void_p)]),
+    ("bfz_host_free", None, [c_void_p]),
     ("bfz_synchronize", c_int, []),
     ("bfz_selftest", c_int, [c_char_p]),
     ("bfz_execute", c_int, [c_char_p, POINTER(c_uint8), c_size_t, POINTER(c_uint8), c_size_t,

@@ -132,13 +132,52 @@ class ExecutionRecordArrays:
 INPUT = 6  # Opcode::Input (the only cycle whose mv_access is a write)
 
 
-def cycles_from_record(rec: "ExecutionRecordArrays") -> np.ndarray:
+class _PinnedBuffer:
+    """bfz_host_alloc memory (page-locked), freed with bfz_host_free when the last array view of
+    it goes away."""
+
+    def __init__(self, nbytes: int):
+        _lib.init()
+        p = ctypes.c_void_p()
+        check(lib().bfz_host_alloc(max(int(nbytes), 1), ctypes.byref(p)))
+        self.ptr = p.value
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            lib().bfz_host_free(ctypes.c_void_p(self.ptr))
+            self.ptr = None
+
+
+class PinnedArray(np.ndarray):
+    """A numpy array over bfz_host_alloc memory (keeps the allocation alive, views included)."""
+
+    def __array_finalize__(self, obj):
+        self._owner = getattr(obj, "_owner", None)
+
+
+def pinned_empty(n: int, dtype) -> PinnedArray:
+    """An uninitialised array of n elements in page-locked host memory: bfz_record_from_cycles
+    DMAs straight from it (what the Rust CycleArrays does through bfz_host_alloc)."""
+    dtype = np.dtype(dtype)
+    buf = _PinnedBuffer(n * dtype.itemsize)
+    raw = (ctypes.c_uint8 * max(n * dtype.itemsize, 1)).from_address(buf.ptr)
+    arr = np.frombuffer(raw, dtype=dtype, count=n).view(PinnedArray)
+    arr._owner = buf
+    return arr
+
+
+def cycles_from_record(rec: "ExecutionRecordArrays", pinned: bool = False) -> np.ndarray:
     """The compact hand-over of bfz_record_from_cycles built from the record's cpu_events -- what
     the Rust HipProver's CycleArrays::new does over record.cpu_events: pc, mp, mv, the
     mv_access's prev_timestamp (0 when it is None) and, for a write (Input), its prev_value.
-    Everything else in the record is rebuilt on the device."""
+    Everything else in the record is rebuilt on the device.  pinned: build it in bfz_host_alloc
+    memory (the upload is then one DMA, no staging copy)."""
     cpu = rec.cpu
-    out = np.zeros(len(cpu), dtype=CYCLE)
+    if pinned:
+        out = pinned_empty(len(cpu), CYCLE)
+        out.view(np.uint32).reshape(-1, 4)[:, 3] = 0  # mv, prev_value, padding
+    else:
+        out = np.zeros(len(cpu), dtype=CYCLE)
     out["pc"] = cpu["pc"]
     out["mp"] = cpu["mp"]
     out["mv"] = cpu["mv"]

@@ -772,6 +772,23 @@ int bfz_record_from_events(const bfz_pk* pk, const bfz_events* e, bfz_record** r
   });
 }
 
+int bfz_host_alloc(size_t bytes, void** out) {
+  return guarded([&] {
+    if (!out) throw std::runtime_error("host_alloc: null argument");
+    *out = nullptr;
+    if (bytes == 0 || bytes > ((size_t)1 << 38)) throw std::runtime_error("host_alloc: size out of range");
+    void* p = bfz::pinned_alloc(bytes);
+    if (!p) throw std::runtime_error("host_alloc: hipHostMalloc failed");
+    *out = p;
+    return 0;
+  });
+}
+
+void bfz_host_free(void* p) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  bfz::pinned_free(p);
+}
+
 int bfz_record_from_cycles(const bfz_pk* pk, const bfz_cycle* cycles, size_t n_cycles,
                            const bfz_memory_event* memory, size_t n_memory, bfz_record** rec) {
   return guarded([&] {

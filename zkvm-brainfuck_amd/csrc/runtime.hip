@@ -162,6 +162,17 @@ void upload_bulk(void* dst, const void* src, size_t bytes, hipStream_t st) {
     return x;
   }();
   static CopyPool* pool = new CopyPool(NTHR);  // never destroyed: its threads end with the process
+  {  // a page-locked source (bfz_host_alloc, hipHostRegister): one DMA, no staging
+    hipPointerAttribute_t a{};
+    const hipError_t e = hipPointerGetAttributes(&a, src);
+    if (e == hipSuccess && a.type == hipMemoryTypeHost) {
+      HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st));
+      HIP_CHECK(hipEventRecord(b->done[0], st));
+      HIP_CHECK(hipEventSynchronize(b->done[0]));
+      return;
+    }
+    (void)hipGetLastError();  // pageable memory: the query fails, clear it
+  }
   if (bytes <= ((size_t)1 << 20)) {  // small: one staged copy
     const uint8_t* s = static_cast<const uint8_t*>(src);
     HIP_CHECK(hipEventSynchronize(b->done[0]));
