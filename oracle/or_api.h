@@ -12,6 +12,9 @@ int or_prove_record(const or_program* prog, or_record* rec, uint8_t** out, size_
 int or_verify_proof(const or_program* prog, const uint8_t* proof, size_t len);
 void or_set_num_queries(int q);
 void or_set_pcs_variant(int observe_openings);
+/* D1-D9 switches (or_hash.h or_variant_t) */
+void or_variant_reset(void);
+int or_variant_set(const char* name, uint32_t value);
 void or_setup_root(const or_program* p, uint32_t root[8]);
 int or_api_setup_root(const char* program, uint32_t root[8]);
 

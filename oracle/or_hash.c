@@ -27,8 +27,23 @@ static const uint32_t RC_RAW[30 * 16] = {
 #include "rc_16_30.inc"
 };
 
-static fp EXT_INIT[4][16], EXT_TERM[4][16], INT_RC[13], DIAG[16];
+static fp EXT_INIT[4][16], EXT_TERM[4][16], INT_RC[13], DIAG[16], DIAG_ALT[16];
 static int g_init = 0;
+
+or_variant_t or_variant = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+void or_variant_reset(void) {
+  or_variant_t d = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  or_variant = d;
+}
+int or_variant_set(const char* name, uint32_t v) {
+#define OR_VSET(f) if (!strcmp(name, #f)) { or_variant.f = (int)v; return 0; }
+  OR_VSET(observe_openings) OR_VSET(diag_alt) OR_VSET(m4_horizen) OR_VSET(no_initial_mds)
+  OR_VSET(inject_first) OR_VSET(fri_coeff_major) OR_VSET(query_extra_bits) OR_VSET(sample_front)
+  OR_VSET(selectors_normalized) OR_VSET(force_witness)
+#undef OR_VSET
+  if (!strcmp(name, "witness")) { or_variant.witness = v; return 0; }
+  return -1;
+}
 
 static void p2_init(void) {
   if (g_init) return;
@@ -46,6 +61,12 @@ static void p2_init(void) {
               inv256, inv8, inv2_24, fp_neg(inv256), fp_neg(inv8), fp_neg(inv16),
               fp_neg(inv2_24)};
   memcpy(DIAG, d, sizeof d);
+  /* D2 alternative: the 16-lane diagonal in the shape of Plonky3's BabyBear-16 vector
+   * [-2, 1, 2, 1/2, 3, 4, -1/2, -3, -4, 1/2^8, 1/4, 1/8, 1/2^27, -1/2^8, -1/16, -1/2^27] */
+  fp inv4 = fp_inv(4), inv2_27 = fp_inv(1u << 27);
+  fp da[16] = {fp_neg(2), 1, 2, inv2, 3, 4, fp_neg(inv2), fp_neg(3), fp_neg(4),
+               inv256, inv4, inv8, inv2_27, fp_neg(inv256), fp_neg(inv16), fp_neg(inv2_27)};
+  memcpy(DIAG_ALT, da, sizeof da);
   g_init = 1;
 }
 
@@ -54,6 +75,13 @@ static inline fp cube(fp x) { return fp_mul(fp_mul(x, x), x); }
 static void mds_light(fp s[16]) {
   for (int b = 0; b < 16; b += 4) {
     fp x0 = s[b], x1 = s[b + 1], x2 = s[b + 2], x3 = s[b + 3];
+    if (or_variant.m4_horizen) { /* D3a alternative: [5 7 1 3; 4 6 1 1; 1 3 5 7; 1 1 4 6] */
+      s[b] = fp_add(fp_add(fp_mul(5, x0), fp_mul(7, x1)), fp_add(x2, fp_mul(3, x3)));
+      s[b + 1] = fp_add(fp_add(fp_mul(4, x0), fp_mul(6, x1)), fp_add(x2, x3));
+      s[b + 2] = fp_add(fp_add(x0, fp_mul(3, x1)), fp_add(fp_mul(5, x2), fp_mul(7, x3)));
+      s[b + 3] = fp_add(fp_add(x0, x1), fp_add(fp_mul(4, x2), fp_mul(6, x3)));
+      continue;
+    }
     /* [2 3 1 1; 1 2 3 1; 1 1 2 3; 3 1 1 2] */
     fp y0 = fp_add(fp_add(fp_mul(2, x0), fp_mul(3, x1)), fp_add(x2, x3));
     fp y1 = fp_add(fp_add(x0, fp_mul(2, x1)), fp_add(fp_mul(3, x2), x3));
@@ -68,7 +96,8 @@ static void mds_light(fp s[16]) {
 
 void or_poseidon2_permute(fp s[16]) {
   p2_init();
-  mds_light(s);
+  const fp* diag = or_variant.diag_alt ? DIAG_ALT : DIAG;
+  if (!or_variant.no_initial_mds) mds_light(s);
   for (int r = 0; r < 4; r++) {
     for (int i = 0; i < 16; i++) s[i] = cube(fp_add(s[i], EXT_INIT[r][i]));
     mds_light(s);
@@ -77,7 +106,7 @@ void or_poseidon2_permute(fp s[16]) {
     s[0] = cube(fp_add(s[0], INT_RC[r]));
     fp sum = 0;
     for (int i = 0; i < 16; i++) sum = fp_add(sum, s[i]);
-    for (int i = 0; i < 16; i++) s[i] = fp_add(sum, fp_mul(DIAG[i], s[i]));
+    for (int i = 0; i < 16; i++) s[i] = fp_add(sum, fp_mul(diag[i], s[i]));
   }
   for (int r = 0; r < 4; r++) {
     for (int i = 0; i < 16; i++) s[i] = cube(fp_add(s[i], EXT_TERM[r][i]));
@@ -177,7 +206,8 @@ void or_merkle_build(or_merkle* t, or_mat* mats, int nmats) {
           for (size_t c = 0; c < M->width; c++) or_sponge_absorb(&sp, M->values[j * M->width + c]);
         }
         or_sponge_finish(&sp, rows);
-        or_compress(node, rows, node);
+        if (or_variant.inject_first) or_compress(rows, node, node); /* D4 alternative */
+        else or_compress(node, rows, node);
       }
       memcpy(&t->layers[L][8 * j], node, sizeof node);
     }
@@ -219,6 +249,7 @@ void or_ch_observe_ef(or_challenger* c, ef v) {
 }
 fp or_ch_sample(or_challenger* c) {
   if (c->nin > 0 || c->nout == 0) duplex(c);
+  if (or_variant.sample_front) return c->out[8 - c->nout--]; /* D7 alternative */
   return c->out[--c->nout];
 }
 ef or_ch_sample_ef(or_challenger* c) {
@@ -237,10 +268,17 @@ int or_ch_check_witness(or_challenger* c, int bits, fp w) {
 /* Grind: the reference uses rayon find_any (nondeterministic); the normal form is the
  * SMALLEST valid witness.  Leaves the challenger as check_witness(witness) would. */
 fp or_ch_grind(or_challenger* c, int bits) {
+  if (or_variant.force_witness == 1) { /* D9: a given witness (e.g. a reference proof's) */
+    or_ch_check_witness(c, bits, or_variant.witness);
+    return or_variant.witness;
+  }
+  /* force_witness == 2: the second-smallest valid witness (a stand-in for the reference's
+   * find_any returning another one; tests/test_localize.py) */
+  int skip = or_variant.force_witness == 2 ? 1 : 0;
   fp found = 0;
   for (fp w = 0; w < OR_P; w++) {
     or_challenger t = *c;
-    if (or_ch_check_witness(&t, bits, w)) { found = w; break; }
+    if (or_ch_check_witness(&t, bits, w) && skip-- == 0) { found = w; break; }
   }
   or_ch_check_witness(c, bits, found);
   return found;

@@ -3,6 +3,30 @@
 #define OR_HASH_H
 #include "or_field.h"
 
+/* The [p3-recalled] decisions of DESIGN.md §2 (D1-D9) as switches, oracle only: the default
+ * (all zero except observe_openings) is the product's choice; scripts/localize_parity.py flips
+ * them to find which combination reproduces a reference proof byte for byte.  Every switch is
+ * honoured by the oracle prover AND its verifier, so a proof made under a variant verifies
+ * under the same variant. */
+typedef struct {
+  int observe_openings;     /* D1: opened values observed before the FRI alpha (1, default) */
+  int diag_alt;             /* D2: 1 = the alternative internal diagonal (OR_DIAG_ALT) */
+  int m4_horizen;           /* D3a: 1 = HorizenLabs M4 [[5,7,1,3],[4,6,1,1],[1,3,5,7],[1,1,4,6]] */
+  int no_initial_mds;       /* D3b: 1 = no external linear layer before round 1 */
+  int inject_first;         /* D4: 1 = node = compress(injected digest, node) */
+  int fri_coeff_major;      /* D5: 1 = FRI leaf pair flattened coefficient-major */
+  int query_extra_bits;     /* D6: k > 0 = sample log_max_height + k bits, open index >> k */
+  int sample_front;         /* D7: 1 = samples pop from the front of the duplex outputs */
+  int selectors_normalized; /* D8: 1 = Lagrange-normalized first/last-row selectors */
+  int force_witness;        /* D9: 1 = use `witness` as the PoW witness (not the smallest);
+                               2 = the second-smallest valid witness */
+  uint32_t witness;
+} or_variant_t;
+extern or_variant_t or_variant;
+void or_variant_reset(void);
+/* by name ("observe_openings", "diag_alt", ...); 0 on success, -1 for an unknown name */
+int or_variant_set(const char* name, uint32_t value);
+
 void or_poseidon2_permute(fp s[16]);
 
 typedef struct { fp st[16]; int pos; } or_sponge;

@@ -30,8 +30,7 @@ static int g_num_queries = 84;
 void or_set_num_queries(int q) { g_num_queries = q; }
 /* Decision D1 ([p3-recalled] TwoAdicFriPcs::open): 1 = every opened value is
  * observed before the FRI batching challenge is sampled; 0 = the challenge is sampled first. */
-static int g_observe_openings = 1;
-void or_set_pcs_variant(int observe_openings) { g_observe_openings = observe_openings != 0; }
+void or_set_pcs_variant(int observe_openings) { or_variant.observe_openings = observe_openings != 0; }
 
 /* ------------------------------------------------------------------ byte buffer */
 typedef struct { uint8_t* p; size_t n, cap; } buf;
@@ -234,6 +233,11 @@ static void quotient(chipdata* cd, const cmat* prep_m, const cmat* main_m, const
     f.perm_alpha = perm_alpha; f.perm_beta = perm_beta; f.cumsum = cd->cumsum;
     f.is_first = ef_from_fp(fp_mul(zh, fp_inv(fp_sub(x, 1))));
     f.is_last = ef_from_fp(fp_mul(zh, fp_inv(fp_sub(x, wn_inv))));
+    if (or_variant.selectors_normalized) { /* D8 alternative: L_0 = Z/(n(x-1)), L_last = w^-1 Z/(n(x-w^-1)) */
+      fp ninv = fp_inv((fp)(n % OR_P));
+      f.is_first = ef_mul_fp(f.is_first, ninv);
+      f.is_last = ef_mul_fp(f.is_last, fp_mul(ninv, wn_inv));
+    }
     f.is_trans = ef_from_fp(fp_sub(x, wn_inv));
     f.alpha = alpha; f.acc = ef_zero();
     or_eval_chip(cd->chip, &f);
@@ -290,9 +294,20 @@ static void fri_prove(buf* b, or_challenger* ch, round_t* rounds, oround* orr, i
     R->nmats = 1;
     R->lm = calloc(1, sizeof(or_mat));
     R->lm[0].values = (fp*)folded; /* EF pairs flattened: width 8 base */
+    fp* cm = NULL;
+    if (or_variant.fri_coeff_major) { /* D5 alternative: [a0 b0 a1 b1 a2 b2 a3 b3] per leaf */
+      cm = malloc(sizeof(fp) * 4 * len);
+      for (size_t i = 0; i < len / 2; i++)
+        for (int k = 0; k < 4; k++) {
+          cm[8 * i + 2 * k] = folded[2 * i].c[k];
+          cm[8 * i + 2 * k + 1] = folded[2 * i + 1].c[k];
+        }
+      R->lm[0].values = cm;
+    }
     R->lm[0].height = len / 2;
     R->lm[0].width = 8;
     or_merkle_build(&R->tree, R->lm, 1);
+    if (cm) { free(cm); R->lm[0].values = (fp*)folded; }
     or_ch_observe_digest(ch, R->tree.root);
     ef beta = or_ch_sample_ef(ch);
     betas[ncommit] = beta;
@@ -325,7 +340,8 @@ static void fri_prove(buf* b, or_challenger* ch, round_t* rounds, oround* orr, i
   for (int i = 0; i < ncommit; i++) bdig(b, fr[i].tree.root);
   bu32(b, (uint32_t)g_num_queries);
   for (int q = 0; q < g_num_queries; q++) {
-    size_t index = or_ch_sample_bits(ch, lg_max);
+    size_t index = or_ch_sample_bits(ch, lg_max + or_variant.query_extra_bits) >>
+                   or_variant.query_extra_bits; /* D6 */
     bu32(b, (uint32_t)nrounds);
     for (int r = 0; r < nrounds; r++) {
       int lmr = or_log2(or_merkle_max_height(&rounds[r].tree));
@@ -454,7 +470,7 @@ int or_prove_record(const or_program* prog, or_record* rec, uint8_t** out, size_
       for (int p = 0; p < orr[r].npts[i]; p++) {
         orr[r].vals[i][p] = malloc(sizeof(ef) * c->w);
         or_eval_columns_at(c->evals, c->n, c->w, c->shift, orr[r].pts[i][p], orr[r].vals[i][p]);
-        if (g_observe_openings)
+        if (or_variant.observe_openings)
           for (size_t k = 0; k < c->w; k++) or_ch_observe_ef(&ch, orr[r].vals[i][p][k]);
       }
     }
@@ -588,7 +604,8 @@ static int verify_batch(const fp root[8], const dims* d, int nm, size_t index, f
         k++;
       }
       fp rh[8]; or_sponge_finish(&sp, rh);
-      or_compress(h, rh, h);
+      if (or_variant.inject_first) or_compress(rh, h, h); /* D4 alternative */
+      else or_compress(h, rh, h);
     }
   }
   return memcmp(h, root, 32) == 0 && k == nm;
@@ -685,7 +702,7 @@ int or_verify_proof(const or_program* prog, const uint8_t* proof, size_t len) {
     }
   }
   /* PCS verify: observe openings (decision D1), sample alpha */
-  if (g_observe_openings) for (int rr_ = 0; rr_ < 4; rr_++)
+  if (or_variant.observe_openings) for (int rr_ = 0; rr_ < 4; rr_++)
     for (int i = 0; i < vn[rr_]; i++)
       for (int p = 0; p < vm[rr_][i].np; p++)
         for (size_t k = 0; k < vm[rr_][i].w; k++) or_ch_observe_ef(&ch, vm[rr_][i].v[p][k]);
@@ -723,7 +740,8 @@ int or_verify_proof(const or_program* prog, const uint8_t* proof, size_t len) {
   int log_max_h = (int)ncommit + LOG_BLOWUP;
   r.off = qstart;
   for (uint32_t q = 0; q < nq; q++) {
-    size_t index = or_ch_sample_bits(&ch, log_max_h);
+    size_t index = or_ch_sample_bits(&ch, log_max_h + or_variant.query_extra_bits) >>
+                   or_variant.query_extra_bits; /* D6 */
     uint32_t nr = ru32(&r);
     if (nr != 4) goto fail;
     ef ro[32];
@@ -784,6 +802,8 @@ int or_verify_proof(const or_program* prog, const uint8_t* proof, size_t len) {
       ev[(idx & 1) ^ 1] = sib;
       fp row[8];
       memcpy(row, ev[0].c, 16); memcpy(row + 4, ev[1].c, 16);
+      if (or_variant.fri_coeff_major) /* D5 alternative */
+        for (int k = 0; k < 4; k++) { row[2 * k] = ev[0].c[k]; row[2 * k + 1] = ev[1].c[k]; }
       fp* rowp = row;
       dims d1 = {(size_t)1 << lfh, 8};
       if (!verify_batch(croots[s], &d1, 1, idx >> 1, &rowp, path, (int)pl_)) goto fail;
@@ -845,6 +865,11 @@ int or_verify_proof(const or_program* prog, const uint8_t* proof, size_t len) {
       f.perm_alpha = perm_alpha; f.perm_beta = perm_beta; f.cumsum = cum[i];
       f.is_first = ef_mul(zh, ef_inv(ef_sub(zeta, ef_one())));
       f.is_last = ef_mul(zh, ef_inv(ef_sub(zeta, ef_from_fp(gn_inv))));
+      if (or_variant.selectors_normalized) { /* D8 alternative */
+        fp ninv = fp_inv((fp)(((uint64_t)1 << log_n) % OR_P));
+        f.is_first = ef_mul_fp(f.is_first, ninv);
+        f.is_last = ef_mul_fp(f.is_last, fp_mul(ninv, gn_inv));
+      }
       f.is_trans = ef_sub(zeta, ef_from_fp(gn_inv));
       f.alpha = alpha; f.acc = ef_zero();
       or_eval_chip(c, &f);

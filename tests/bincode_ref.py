@@ -171,3 +171,80 @@ def encode_bincode(pf: dict, montgomery: bool = True) -> bytes:
         w.parts.append(CHIPS[c].encode())
         w.u64(i)
     return w.bytes()
+
+
+class _B:
+    """bincode reader (u64 lengths); field words converted out of Montgomery form if asked."""
+
+    def __init__(self, b, mont: bool):
+        self.b, self.o, self.mont = b, 0, mont
+        self.rinv = pow(R, -1, P)
+
+    def u32(self):
+        v = struct.unpack_from("<I", self.b, self.o)[0]
+        self.o += 4
+        return v
+
+    def u64(self):
+        v = struct.unpack_from("<Q", self.b, self.o)[0]
+        self.o += 8
+        return v
+
+    def fps(self, k):
+        v = list(struct.unpack_from("<%dI" % k, self.b, self.o))
+        self.o += 4 * k
+        if any(x >= P for x in v):
+            raise ValueError("field word out of range")
+        return [(x * self.rinv) % P for x in v] if self.mont else v
+
+    def efs(self):
+        return [self.fps(4) for _ in range(self.u64())]
+
+    def digests(self):
+        return [self.fps(8) for _ in range(self.u64())]
+
+
+def decode_bincode(b: bytes, montgomery: bool = True) -> dict:
+    """Inverse of encode_bincode: the same dict parse_bfz1 returns (canonical values).  The
+    chip_ordering map may come in any order (a Rust HashMap); chips are put in index order."""
+    r = _B(b, montgomery)
+    pf = {"roots": [r.fps(8) for _ in range(3)], "opened": []}
+    for _ in range(r.u64()):
+        o = {}
+        for key in ("prep_local", "prep_next", "main_local", "main_next", "perm_local",
+                    "perm_next"):
+            o[key] = r.efs()
+        if r.u64() != 2:
+            raise ValueError("quotient chunk count")
+        o["quotient"] = [r.efs(), r.efs()]
+        o["cumsum"] = r.fps(4)
+        o["log_degree"] = r.u64()
+        pf["opened"].append(o)
+    pf["commit_roots"] = r.digests()
+    queries = []
+    for _ in range(r.u64()):
+        inputs = []
+        for _ in range(r.u64()):
+            rows = [r.fps(r.u64()) for _ in range(r.u64())]
+            inputs.append({"rows": rows, "path": r.digests()})
+        steps = []
+        for _ in range(r.u64()):
+            sib = r.fps(4)
+            steps.append({"sibling": sib, "path": r.digests()})
+        queries.append({"inputs": inputs, "steps": steps})
+    pf["queries"] = queries
+    pf["final_poly"] = r.fps(4)
+    pf["pow_witness"] = r.fps(1)[0]
+    # chip_ordering: HashMap<String, usize>, written as (len, name bytes, u64 index) pairs
+    n = r.u64()
+    n_opened = len(pf["opened"])
+    order = {}
+    for _ in range(n):
+        ln = r.u64()
+        name = r.b[r.o:r.o + ln].decode()
+        r.o += ln
+        order[r.u64()] = CHIPS.index(name)
+    if r.o != len(r.b) or sorted(order) != list(range(n)) or n != n_opened:
+        raise ValueError("trailing bytes or malformed chip ordering")
+    pf["chips"] = [order[i] for i in range(n)]
+    return pf

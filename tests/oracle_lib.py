@@ -45,8 +45,29 @@ def lib():
         L.or_api_perm_trace.argtypes = [ctypes.c_int, P32, P32, ctypes.c_size_t, P32, P32, P32, P32]
         L.or_set_num_queries.argtypes = [ctypes.c_int]
         L.or_set_pcs_variant.argtypes = [ctypes.c_int]
+        L.or_variant_set.argtypes = [ctypes.c_char_p, ctypes.c_uint32]
+        L.or_variant_reset.argtypes = []
         _L = L
     return _L
+
+
+VARIANT_NAMES = ("diag_alt", "m4_horizen", "no_initial_mds", "inject_first", "fri_coeff_major",
+                 "query_extra_bits", "sample_front", "selectors_normalized", "force_witness",
+                 "witness")
+
+
+def set_variant(**kw):
+    """The oracle's [p3-recalled] switches D2-D9 (oracle/or_hash.h or_variant_t); D1 is the
+    observe_openings argument of prove / verify.  Unnamed switches are reset to the default."""
+    L = lib()
+    L.or_variant_reset()
+    for k, v in kw.items():
+        if L.or_variant_set(k.encode(), int(v)) != 0:
+            raise KeyError(k)
+
+
+def reset_variant():
+    lib().or_variant_reset()
 
 
 def execute(prog: str, stdin):
