@@ -658,7 +658,14 @@ def main():
                 "what": "one proof split over N GPUs, predicted: N = 1 is the timed single-GPU "
                         "proof; N > 1 is the slowest rank's share run alone on this GPU with "
                         "no-op exchanges (bfz_record_prove_shard_solo), before collective time",
-                "ranks": {str(n): runs[n]["ranks"] for n in solo}}
+                "ranks": {str(n): runs[n]["ranks"] for n in solo},
+                "logup_stage_parts": {
+                    "replicated": ["perm_rows_ms (permutation rows + cumulative-sum scan: whole "
+                                   "rows of the trace domain)",
+                                   "perm_idft_ms (iDFT of every permutation column)"],
+                    "split": ["perm_dft_ms (fold onto the rank's residue coset + forward DFT of "
+                              "size 2n/N, plus the next-residue shards at N >= 4)",
+                              "perm_hash_ms (this rank's Merkle subtree)"]}}
         if world == 1 and not args.no_extra:
             line["end_to_end"] = end_to_end(client, pk, prog, stdin)
             line["events_path"] = events_path(pk, prog, stdin, proof)

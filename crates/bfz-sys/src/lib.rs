@@ -55,6 +55,10 @@ pub struct bfz_timings {
     pub reduce_kernel_ms: f64,
     pub reduce_kernel_bytes: f64,
     pub reduce_kernel_launches: c_int,
+    pub perm_rows_ms: f64,
+    pub perm_idft_ms: f64,
+    pub perm_dft_ms: f64,
+    pub perm_hash_ms: f64,
 }
 
 #[repr(C)]

@@ -76,6 +76,11 @@ typedef struct {
   int open_kernel_launches;
   double reduce_kernel_ms, reduce_kernel_bytes;
   int reduce_kernel_launches;
+  /* The LogUp stage (perm_ms, prover.rs:280-334) in parts: permutation rows + cumulative-sum scan
+   * (replicated on every rank of a sharded proof), iDFT of the permutation columns (replicated;
+   * 0 unsharded), fold + forward DFT (this rank's residue and its next-residue shards when
+   * sharded; the whole coset LDE unsharded), Merkle hashing (split). */
+  double perm_rows_ms, perm_idft_ms, perm_dft_ms, perm_hash_ms;
 } bfz_timings;
 
 int bfz_init(int device);

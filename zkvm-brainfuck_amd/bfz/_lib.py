@@ -29,6 +29,8 @@ class Timings(ctypes.Structure):
         ("open_kernel_ms", c_double), ("open_kernel_bytes", c_double), ("open_kernel_launches", c_int),
         ("reduce_kernel_ms", c_double), ("reduce_kernel_bytes", c_double),
         ("reduce_kernel_launches", c_int),
+        ("perm_rows_ms", c_double), ("perm_idft_ms", c_double), ("perm_dft_ms", c_double),
+        ("perm_hash_ms", c_double),
     ]
 
     def as_dict(self) -> dict:

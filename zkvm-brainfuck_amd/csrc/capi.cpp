@@ -848,6 +848,10 @@ void fill_timings(const bfz::StageTimes& st, bfz_timings* t) {
   t->reduce_kernel_ms = st.reduce_kernel_ms;
   t->reduce_kernel_bytes = st.reduce_kernel_bytes;
   t->reduce_kernel_launches = st.reduce_kernel_launches;
+  t->perm_rows_ms = st.perm_rows;
+  t->perm_idft_ms = st.perm_idft;
+  t->perm_dft_ms = st.perm_dft;
+  t->perm_hash_ms = st.perm_hash;
 }
 struct ShardScope {  // installs the shard context for one proof
   explicit ShardScope(bfz::ShardCtx* c) { bfz::shard_ctx() = c; }

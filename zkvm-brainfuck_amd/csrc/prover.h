@@ -88,6 +88,8 @@ struct StageTimes {          // milliseconds, measured with HIP events on the pr
   int open_kernel_launches = 0;
   double reduce_kernel_ms = 0, reduce_kernel_bytes = 0;  // k_reduce
   int reduce_kernel_launches = 0;
+  // the LogUp stage in parts (bfz.h bfz_timings)
+  double perm_rows = 0, perm_idft = 0, perm_dft = 0, perm_hash = 0;
 };
 
 std::unique_ptr<ProvingKey> setup(const std::string& program_src);

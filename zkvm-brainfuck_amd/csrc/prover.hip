@@ -272,9 +272,16 @@ static const NextCols& chip_next_cols(int chip) {
 // plan != nullptr and a height it shards: this rank's residue-class shard of the LDE from the
 // interpolant's coefficients (kept in cm.coef), plus -- for G >= 4 -- the shard of the next-row
 // residue class for the columns in next_cols (the quotient reads only those at row i + 2).
+// split (timed proofs only): where the iDFT and the fold + forward DFT time go (the LogUp
+// stage's parts); the unsharded coset LDE counts as forward DFT
+struct LdeSplit {
+  double* idft;
+  double* dft;
+};
 static void lde_into(CMat& cm, const uint32_t* evals, size_t n, int w, uint32_t domain_shift,
                      hipStream_t st, EvTimer* tm, StageTimes* times, const Plan* plan = nullptr,
-                     const std::vector<int>* next_cols = nullptr) {
+                     const std::vector<int>* next_cols = nullptr, const LdeSplit* split = nullptr) {
+  const bool timed = split && tm && tm->on;
   for (int c = 0; c < 64; c++) cm.nmap[c] = (uint8_t)c;
   cm.n = n;
   cm.log_n = log2i(n);
@@ -290,7 +297,10 @@ static void lde_into(CMat& cm, const uint32_t* evals, size_t n, int w, uint32_t 
     cm.row0 = plan->row0(2 * n);
     cm.coef.reset(n * (size_t)w);
     cm.lde.buf.reset(cm.blk * (size_t)w);
+    hipEvent_t b0 = timed ? tm->begin(st) : nullptr;
     lde_coefficients(evals, n, w, cm.coef.p, st);
+    if (timed) tm->end(b0, st, split->idft);
+    hipEvent_t b1 = timed ? tm->begin(st) : nullptr;
     coset_residue(cm.coef.p, n, w, lde_shift, plan->lg, plan->r, cm.lde.buf.p, st);
     cm.nxt_row0 = (size_t)plan->k2 * cm.blk;  // = row0 for G = 2
     if (next_cols && !next_cols->empty() && plan->G >= 4) {
@@ -299,6 +309,7 @@ static void lde_into(CMat& cm, const uint32_t* evals, size_t n, int w, uint32_t 
       cm.nmap.fill(0);  // columns not read at the next row: any valid column
       for (size_t y = 0; y < next_cols->size(); y++) cm.nmap[(*next_cols)[y]] = (uint8_t)y;
     }
+    if (timed) tm->end(b1, st, split->dft);
     return;
   }
   cm.blk = 2 * n;
@@ -306,7 +317,9 @@ static void lde_into(CMat& cm, const uint32_t* evals, size_t n, int w, uint32_t 
   cm.lde.buf.reset(2 * n * (size_t)w);
   hipEvent_t b = nullptr;
   if (tm && tm->on) b = tm->begin(st);
+  hipEvent_t bs = timed ? tm->begin(st) : nullptr;
   coset_lde(evals, n, w, lde_shift, cm.lde.buf.p, st);
+  if (timed) tm->end(bs, st, split->dft);
   if (tm && tm->on) {
     tm->end(b, st, &times->lde_ms);
     times->lde_bytes += 12.0 * (double)n * w;
@@ -607,11 +620,17 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     const int pi = pk.idx_of_chip[c];
     const uint32_t* prep = pi >= 0 ? pk.prep_evals[pi].p : nullptr;
     if (k == 0) htrace().mark("perm_rows buffers");
+    hipEvent_t br = ev.on ? ev.begin(st) : nullptr;
     perm_trace(c, dt.evals[order[k]].p, prep, hn[k], pc_d.p, pe.p, cums_d.p + k, st);
+    if (ev.on) ev.end(br, st, &tms->perm_rows);
     if (k == 0) htrace().mark("perm_rows launched");
-    lde_into(permr.mats[k], pe.p, hn[k], 4 * pw, ONE, st, &ev, tms, &plan, &chip_next_cols(c).perm);
+    LdeSplit split{tms ? &tms->perm_idft : nullptr, tms ? &tms->perm_dft : nullptr};
+    lde_into(permr.mats[k], pe.p, hn[k], 4 * pw, ONE, st, &ev, tms, &plan, &chip_next_cols(c).perm,
+             tms ? &split : nullptr);
   }
+  hipEvent_t bh = ev.on ? ev.begin(st) : nullptr;
   permr.commit(st, /*fetch_root=*/false);
+  if (ev.on) ev.end(bh, st, &tms->perm_hash);
   if (ev.on) ev.end(e1, st, &tms->perm);
   HIP_CHECK(hipMemcpyAsync(cums_d.p + nc + 2, permr.tree.layers.back().p, 32, hipMemcpyDeviceToDevice, st));
 
