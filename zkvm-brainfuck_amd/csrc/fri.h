@@ -46,10 +46,18 @@ struct OpenDesc {
   kb::EF* out_b;
   uint32_t chunk0, col0, nchunks, pad;
   uint64_t part_off;
+  // zeta != nullptr: the point lives on the device (sampled there) and k_open_final_batch
+  // computes the scales itself: scale_a = (zeta^n - 3^n) * zc with n = 2^zlog, zc = 1/(3^n n);
+  // scale_b = scale_a * zb ((zeta w_n)^n = zeta^n; zb = w_n^-1 when invd_b is derived, else 1)
+  const kb::EF* zeta;
+  int zlog;
+  uint32_t z3n, zc, zb;
 };
 // Every descriptor of ds is opened at np (1 or 2) points: one partial-sum launch over all of
 // their row chunks, one final launch over all of their columns.
 void open_batch(std::vector<OpenDesc>& ds, int np, hipStream_t st);
+// 1 / (x_t - z) over the whole 2^logH coset with z read from device memory (sampled there)
+void inv_denoms_dev(const kb::EF* z, int logH, kb::EF* out, hipStream_t st);
 // ro[t] = (sum_c ca_c v_c[t] - ya) invd_a[t] + (sum_m kb_m sum_(c in m) ca_c v_c[t] - yb) invd_b[t]
 // for the positions [t0, t0 + count) of a height-`height` LDE (all of it, or a shard's range);
 // cols / mats: device descriptor arrays of one height (RedMat::first indexes cols); every

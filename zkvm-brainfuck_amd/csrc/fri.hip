@@ -36,11 +36,14 @@ __device__ __forceinline__ size_t prev2_pos(size_t t, int logH) {
 constexpr int INV_CHUNK = 8;
 
 // out[t - t0] = 1 / (x_t - z) for t in [t0, t0 + count)
-__global__ __launch_bounds__(256) void k_inv_denoms(EF z, int logH, size_t t0, size_t count,
+// zp != nullptr: the point is read from device memory (sampled on the device)
+__global__ __launch_bounds__(256) void k_inv_denoms(EF z, const EF* __restrict__ zp, int logH,
+                                                    size_t t0, size_t count,
                                                     const uint32_t* __restrict__ twf,
                                                     EF* __restrict__ out) {
   const size_t base = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * INV_CHUNK;
   if (base >= count) return;
+  if (zp) z = *zp;
   EF d[INV_CHUNK], pre[INV_CHUNK];
   const int cnt = (int)min((size_t)INV_CHUNK, count - base);
   EF run = ef_one();
@@ -231,8 +234,15 @@ __global__ __launch_bounds__(256) void k_open_final_batch(const OpenDesc* __rest
   int m = 0;
   while (m + 1 < nd && d[m + 1].col0 <= blockIdx.x) m++;
   const OpenDesc& o = d[m];
-  open_final<NP>(partial + o.part_off, (int)o.nchunks, o.w, (int)(blockIdx.x - o.col0), o.scale_a,
-                 o.scale_b, o.out_a, o.out_b);
+  EF sa = o.scale_a, sb = o.scale_b;
+  if (o.zeta) {  // the point was sampled on the device: (zeta^n - 3^n) / (3^n n), n = 2^zlog
+    EF zn = *o.zeta;
+    for (int i = 0; i < o.zlog; i++) zn = ef_mul(zn, zn);
+    sa = ef_mul_base(ef_sub(zn, ef_base(o.z3n)), o.zc);
+    sb = ef_mul_base(sa, o.zb);
+  }
+  open_final<NP>(partial + o.part_off, (int)o.nchunks, o.w, (int)(blockIdx.x - o.col0), sa, sb,
+                 o.out_a, o.out_b);
 }
 
 // ------------------------------------------------------------------ reduced openings
@@ -564,8 +574,17 @@ void inv_denoms(const EF& z, int logH, EF* out, hipStream_t st) {
 void inv_denoms_range(const EF& z, int logH, size_t t0, size_t count, EF* out, hipStream_t st) {
   twiddles().ensure(std::max(logH, 1));
   const size_t nthreads = (count + INV_CHUNK - 1) / INV_CHUNK;
-  hipLaunchKernelGGL(k_inv_denoms, dim3(ceil_div(nthreads, 256)), dim3(256), 0, st, z, logH, t0,
-                     count, (const uint32_t*)twiddles().fwd.p, out);
+  hipLaunchKernelGGL(k_inv_denoms, dim3(ceil_div(nthreads, 256)), dim3(256), 0, st, z,
+                     (const EF*)nullptr, logH, t0, count, (const uint32_t*)twiddles().fwd.p, out);
+  KCHECK();
+}
+
+void inv_denoms_dev(const EF* z, int logH, EF* out, hipStream_t st) {
+  twiddles().ensure(std::max(logH, 1));
+  const size_t count = (size_t)1 << logH;
+  const size_t nthreads = (count + INV_CHUNK - 1) / INV_CHUNK;
+  hipLaunchKernelGGL(k_inv_denoms, dim3(ceil_div(nthreads, 256)), dim3(256), 0, st, ef_zero(), z,
+                     logH, (size_t)0, count, (const uint32_t*)twiddles().fwd.p, out);
   KCHECK();
 }
 

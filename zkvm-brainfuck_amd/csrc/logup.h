@@ -22,6 +22,10 @@ void perm_trace(int chip, const uint32_t* mainc, const uint32_t* prepc, size_t n
 // (prover.rs:269-272); out receives alpha and beta^0..7.  The host replays the same step when
 // it fetches the root later, so its transcript stays in step.
 void challenge_perm(DevChallenger* ch, const uint32_t* root, PermChallenges* out, hipStream_t st);
+// The out-of-domain point after the quotient commit (prover.rs:415 challenger.sample_ext_element
+// after observing the quotient root), on the device: observe root, *zeta = sample_ef.  The host
+// replays it when the roots come back and fails on a mismatch.
+void challenge_zeta(DevChallenger* ch, const uint32_t* root, kb::EF* zeta, hipStream_t st);
 
 void ef_inclusive_scan(kb::EF* data, size_t n, hipStream_t st);
 

@@ -274,4 +274,20 @@ void challenge_perm(DevChallenger* ch, const uint32_t* root, PermChallenges* out
   KCHECK();
 }
 
+__global__ __launch_bounds__(64) void k_challenge_zeta(DevChallenger* __restrict__ c,
+                                                       const uint32_t* __restrict__ root,
+                                                       EF* __restrict__ zeta) {
+  LaneSponge sp;
+  sp.load(c);
+  for (int i = 0; i < 8; i++) sp.observe(root[i]);
+  const EF z = sp.sample_ef();
+  sp.store(c);
+  if (threadIdx.x == 0) *zeta = z;
+}
+
+void challenge_zeta(DevChallenger* ch, const uint32_t* root, EF* zeta, hipStream_t st) {
+  hipLaunchKernelGGL(k_challenge_zeta, dim3(1), dim3(64), 0, st, ch, root, zeta);
+  KCHECK();
+}
+
 }  // namespace bfz

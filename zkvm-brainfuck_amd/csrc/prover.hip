@@ -189,6 +189,36 @@ struct EvTimer {
   }
 };
 
+// An asynchronous device -> host copy into a pinned buffer, waited for later by spinning on its
+// event (fetch() waits at once).  Process-global instances rely on the API lock.
+struct Mailbox {
+  uint8_t* box = nullptr;
+  size_t cap = 0;
+  hipEvent_t ev = nullptr;
+  bool pending = false;
+  void post(const void* src, size_t bytes, hipStream_t st) {
+    if (!ev) HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    if (pending) HIP_CHECK(hipEventSynchronize(ev));  // a post never waited for (an error path)
+    if (bytes > cap) {
+      if (box) HIP_CHECK(hipHostFree(box));
+      cap = std::max(bytes, (size_t)4096);
+      HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&box), cap, hipHostMallocDefault));
+    }
+    HIP_CHECK(hipMemcpyAsync(box, src, bytes, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipEventRecord(ev, st));
+    pending = true;
+  }
+  void wait(void* dst, size_t bytes) {
+    for (;;) {
+      const hipError_t e = hipEventQuery(ev);
+      if (e == hipSuccess) break;
+      if (e != hipErrorNotReady) HIP_CHECK(e);
+    }
+    pending = false;
+    std::memcpy(dst, box, bytes);
+  }
+};
+
 void to_canon_digest(const uint32_t* d, uint32_t* o) {
   for (int i = 0; i < 8; i++) o[i] = from_mont(d[i]);
 }
@@ -606,10 +636,10 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   hipEvent_t e1 = ev.on ? ev.begin(st) : nullptr;
   Round permr;
   permr.mats.resize(nc);
-  // cums_d: the chips' cumulative sums, then (fetched together before zeta) the main,
-  // permutation and quotient roots, 2 EF slots (8 words) each, then the device's samples of the
-  // LogUp alpha, beta and the quotient alpha (compared with the host replay below)
-  DBuf<EF> cums_d(nc + 9);
+  // cums_d: the chips' cumulative sums, then (fetched together) the main, permutation and
+  // quotient roots, 2 EF slots (8 words) each, then the device's samples of the LogUp alpha,
+  // beta, the quotient alpha and (single GPU) zeta -- compared with the host replay below
+  DBuf<EF> cums_d(nc + 10);
   HIP_CHECK(hipMemcpyAsync(cums_d.p + nc, mainr.tree.layers.back().p, 32, hipMemcpyDeviceToDevice, st));
   HIP_CHECK(hipMemcpyAsync(cums_d.p + nc + 6, &pc_d.p->alpha, sizeof(EF), hipMemcpyDeviceToDevice, st));
   HIP_CHECK(hipMemcpyAsync(cums_d.p + nc + 7, &pc_d.p->beta_pows[1], sizeof(EF), hipMemcpyDeviceToDevice, st));
@@ -744,31 +774,43 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   quotr.commit(st, /*fetch_root=*/false);
   if (ev.on) ev.end(e2, st, &tms->quotient);
   HIP_CHECK(hipMemcpyAsync(cums_d.p + nc + 4, quotr.tree.layers.back().p, 32, hipMemcpyDeviceToDevice, st));
-  std::vector<EF> cums(nc + 9);
-  fetch(cums.data(), cums_d.p, (nc + 9) * sizeof(EF), st);
-  htrace().mark("roots fetched");
-  std::memcpy(mainr.tree.root, &cums[nc], 32);
-  std::memcpy(permr.tree.root, &cums[nc + 2], 32);
-  std::memcpy(quotr.tree.root, &cums[nc + 4], 32);
-  const EF dev_perm_alpha = cums[nc + 6], dev_perm_beta = cums[nc + 7], dev_quot_alpha = cums[nc + 8];
-  md.root_on_host = true;
-  cums.resize(nc);
-  // The host transcript replays the device steps (prover.rs:265-272, 336-342, 413-416): the
-  // reference has one transcript, so the device's samples must be the host's (a drifted device
-  // sponge would otherwise surface only as a proof the verifier rejects).
-  auto same = [](const EF& dev, const EF& host, const char* what) {
-    if (!ef_eq(dev, host))
-      throw std::runtime_error(std::string("device transcript diverged from the host challenger: ") + what);
+  // Single GPU: zeta is sampled on the device too (prover.rs:415), so the openings below are
+  // queued behind the quotient commit with no host round trip; the host reads the roots and the
+  // device's samples back through a mailbox while the GPU works, replays the transcript and fails
+  // on any mismatch before it uses anything that depends on them.
+  const bool dev_zeta = !plan.on();
+  EF* const zeta_d = cums_d.p + nc + 9;
+  if (dev_zeta) challenge_zeta(dc_d.p, quotr.tree.layers.back().p, zeta_d, st);
+  static Mailbox roots_box;  // process-global: the API lock is held (see open_impl's gbox)
+  roots_box.post(cums_d.p, (nc + 10) * sizeof(EF), st);
+  EF zeta = ef_zero();
+  std::vector<EF> cums(nc + 10);  // [0, nc): the chips' cumulative sums (written into the proof)
+  auto replay = [&] {
+    roots_box.wait(cums.data(), (nc + 10) * sizeof(EF));
+    htrace().mark("roots fetched");
+    std::memcpy(mainr.tree.root, &cums[nc], 32);
+    std::memcpy(permr.tree.root, &cums[nc + 2], 32);
+    std::memcpy(quotr.tree.root, &cums[nc + 4], 32);
+    md.root_on_host = true;
+    // The host transcript replays the device steps (prover.rs:265-272, 336-342, 413-416): the
+    // reference has one transcript, so the device's samples must be the host's (a drifted device
+    // sponge would otherwise surface only as a proof the verifier rejects).
+    auto same = [](const EF& dev, const EF& host, const char* what) {
+      if (!ef_eq(dev, host))
+        throw std::runtime_error(std::string("device transcript diverged from the host challenger: ") + what);
+    };
+    ch.observe_digest(mainr.tree.root);
+    same(cums[nc + 6], ch.sample_ef(), "LogUp alpha");
+    same(cums[nc + 7], ch.sample_ef(), "LogUp beta");
+    ch.observe_digest(permr.tree.root);
+    for (int k = 0; k < nc; k++) ch.observe_ef(cums[k]);
+    same(cums[nc + 8], ch.sample_ef(), "quotient alpha");
+    ch.observe_digest(quotr.tree.root);
+    zeta = ch.sample_ef();
+    if (dev_zeta) same(cums[nc + 9], zeta, "zeta");
+    htrace().mark("zeta");
   };
-  ch.observe_digest(mainr.tree.root);
-  same(dev_perm_alpha, ch.sample_ef(), "LogUp alpha");
-  same(dev_perm_beta, ch.sample_ef(), "LogUp beta");
-  ch.observe_digest(permr.tree.root);
-  for (int k = 0; k < nc; k++) ch.observe_ef(cums[k]);
-  same(dev_quot_alpha, ch.sample_ef(), "quotient alpha");
-  ch.observe_digest(quotr.tree.root);
-  const EF zeta = ch.sample_ef();
-  htrace().mark("zeta");
+  if (!dev_zeta) replay();
 
   // ---- PCS open: opened values (prover.rs:417-470)
   hipEvent_t e3 = ev.on ? ev.begin(st) : nullptr;
@@ -826,7 +868,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   DBuf<EF> invd_zeta;
   if (!plan.on()) {
     invd_zeta.reset((size_t)1 << Lmax);
-    inv_denoms(zeta, Lmax, invd_zeta.p, st);
+    inv_denoms_dev(zeta_d, Lmax, invd_zeta.p, st);
   }
   std::map<int, Invd> invd;
   for (const auto& [lh, two] : two_at) {
@@ -897,13 +939,8 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
                           out_b, st);
         continue;
       }
-      const EF three_n = ef_base(mpow(to_mont(3), m.n));
+      const uint32_t three_n = mpow(to_mont(3), m.n);
       const uint32_t n_f = to_mont((uint32_t)(m.n % P));
-      EF scale[2];
-      for (int j = 0; j < mp[r][i].npts; j++) {
-        const EF zn = ef_pow(mp[r][i].pts[j], m.n);
-        scale[j] = ef_mul(ef_sub(zn, three_n), ef_inv(ef_mul_base(three_n, n_f)));
-      }
       const Invd& d = invd.at(lh);
       OpenDesc o{};
       o.mat = m.lde.buf.p;
@@ -912,9 +949,20 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
       o.logH = lh;
       o.invd_a = d.full_a();
       o.invd_b = two ? d.full_b() : o.invd_a;  // nullptr: derived from the zeta table
-      o.scale_a = scale[0];
-      o.scale_b = two ? scale[1] : scale[0];
-      if (two && !o.invd_b) o.scale_b = ef_mul_base(o.scale_b, minv(two_adic_gen(m.log_n)));
+      // scale = (z^n - 3^n) / (3^n n), the same for both points ((zeta w_n)^n = zeta^n); with
+      // derived second-point denominators it also carries w_n^-1 (see k_reduce)
+      const uint32_t zb = two && !o.invd_b ? minv(two_adic_gen(m.log_n)) : ONE;
+      if (dev_zeta) {  // computed by k_open_final_batch from the device's zeta
+        o.zeta = zeta_d;
+        o.zlog = m.log_n;
+        o.z3n = three_n;
+        o.zc = minv(mmul(three_n, n_f));
+        o.zb = zb;
+      } else {
+        const EF zn = ef_pow(zeta, m.n);
+        o.scale_a = ef_mul_base(ef_sub(zn, ef_base(three_n)), minv(mmul(three_n, n_f)));
+        o.scale_b = ef_mul_base(o.scale_a, zb);
+      }
       o.out_a = out_a;
       o.out_b = two ? out_b : out_a;
       (two ? open2g : open1g)[group_of(r)].push_back(o);
@@ -952,6 +1000,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
                                hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipEventRecord(gev[g], st));
   }
+  if (dev_zeta) replay();  // the openings are queued: now the host's transcript catches up
   if (plan.on()) {  // one all-gather; sharded matrices' slices summed, replicated ones kept
     DBuf<EF> all(nvals * plan.G);
     HIP_CHECK(hipStreamSynchronize(st));
