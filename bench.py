@@ -41,6 +41,11 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03", "pmc_summary.json")
 # ISA of k_ntt_tile<false,14,true> + k_lde_mid<22> + k_ntt_tile<true,14> (scripts/ntt_isa.py ->
 # profiles/r02/ntt_isa_mix.txt).  Smaller chips' LDEs use the same kernels' shapes within ~5%.
 NTT_UNITS_PER_ELEM_STAGE = 7.023
+# Dynamic counters of the same kernels at a known element-stage count (scripts/gpu_ntt_counters.sh
+# -> scripts/ntt_counters.py): SQ_INSTS_VALU x 64 per element-stage, SQ wave-state fractions.
+NTT_COUNTERS = os.path.join(ROOT, "profiles", "r04", "ntt_counters.json")
+# element-stage shares of a 2^22 coset LDE: DIT tile 14, k_lde_mid<22> 3 x 8, DIF tile 2 x 14 (of 66)
+NTT_FAMILY_SHARE = {"dit_tile": 14 / 66, "lde_mid": 24 / 66, "dif_tile": 28 / 66}
 
 
 def ntt_traffic():
@@ -96,19 +101,41 @@ def ntt_roofline(tm):
 
 
 def ntt_valu(tm):
-    """VALU-issue roofline of the same NTT kernels: units per element-stage (ISA) x the proof's
-    element-stages (3*n*log2(n)*w per LDE) / NTT kernel time, against 78.6 T units/s."""
+    """VALU issue of the same NTT kernels FROM COUNTERS: the measured VALU
+    wave-instructions per element-stage of each kernel (profiles/r04/ntt_counters.json, rocprofv3
+    SQ_INSTS_VALU at a known element-stage count), weighted by its share of a 2^22 coset LDE, x the
+    proof's element-stages / NTT kernel time = lane-instructions/s, against the 78.6 T lane-ops/s
+    issue peak.  frac_units weights the instructions by the ISA's half-rate share (units per
+    instruction, profiles/r02/ntt_isa_mix.txt); wait_any / wait_inst / valu_active are the SQ
+    wave-state fractions of the same run: where the other cycles go."""
     if tm.ntt_kernel_ms <= 0 or tm.lde_elem_stages <= 0:
         return None
-    tops = NTT_UNITS_PER_ELEM_STAGE * tm.lde_elem_stages / (tm.ntt_kernel_ms * 1e-3) / 1e12
-    return {"bound": "valu", "units_per_element_stage": NTT_UNITS_PER_ELEM_STAGE,
-            "element_stages_per_proof": int(tm.lde_elem_stages), "achieved": round(tops, 1),
-            "peak": round(VALU_PEAK_TOPS, 1), "unit": "T full-rate VALU lane-ops/s",
-            "frac": round(tops / VALU_PEAK_TOPS, 4),
-            # 2^22 LDE at 100% VALU issue: 66 element-stages and 12 B per input element
-            "hbm_frac_at_valu_peak": round(12.0 * VALU_PEAK_TOPS * 1e12
-                                           / (NTT_UNITS_PER_ELEM_STAGE * 66) / (HBM_PEAK_GBS * 1e9), 4),
-            "source": "profiles/r02/ntt_isa_mix.txt (scripts/ntt_isa.py 22)"}
+    try:
+        ks = json.load(open(NTT_COUNTERS))["kernels"].values()
+        fam = {k["family"]: k for k in ks}
+        w = NTT_FAMILY_SHARE
+        instr = sum(w[f] * fam[f]["valu_per_elem_stage"] for f in w)
+        sq = {key: round(sum(w[f] * fam[f][key + "_per_wave_cycle"] for f in w), 3)
+              for key in ("wait_any", "wait_inst_any", "active_inst_any", "valu_active")}
+        per_kernel = {f: {"valu_instr_per_elem_stage": fam[f]["valu_per_elem_stage"],
+                          "lds_instr_per_elem_stage": fam[f]["lds_per_elem_stage"],
+                          "salu_instr_per_elem_stage": fam[f]["salu_per_elem_stage"],
+                          "valu_issue_frac": fam[f]["valu_issue_frac"]} for f in w}
+    except (OSError, KeyError, ValueError):
+        return None
+    lane_instr_s = instr * tm.lde_elem_stages / (tm.ntt_kernel_ms * 1e-3)
+    units_per_instr = NTT_UNITS_PER_ELEM_STAGE / instr
+    frac = lane_instr_s / (VALU_PEAK_TOPS * 1e12)
+    return {"bound": "valu (latency / barrier-limited: see wait fractions)",
+            "valu_instr_per_element_stage": round(instr, 3),
+            "element_stages_per_proof": int(tm.lde_elem_stages),
+            "achieved": round(lane_instr_s / 1e12, 1), "peak": round(VALU_PEAK_TOPS, 1),
+            "unit": "T VALU lane-instructions/s", "frac": round(frac, 4),
+            "frac_units": round(frac * units_per_instr, 4),
+            "units_per_instruction_isa": round(units_per_instr, 3),
+            "sq_fractions_of_wave_cycles": sq, "per_kernel": per_kernel,
+            "source": "profiles/r04/ntt_counters.json (scripts/gpu_ntt_counters.sh: ubench_ntt "
+                      "lde 22 8 under rocprofv3 --pmc)"}
 
 
 def poseidon2_roofline(tm):

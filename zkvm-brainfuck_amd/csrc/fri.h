@@ -64,9 +64,29 @@ void inv_denoms_dev(const kb::EF* z, int logH, kb::EF* out, hipStream_t st);
 // pointer is indexed by the global position.  invd_b == nullptr with has_b: the second point is zeta w_n and its
 // denominators are read from invd_a at the position of natural index i - 2 -- the caller has
 // folded w_n^-1 into every RedMat::kb and into yb.
+// yab: DEVICE pointer to {ya, yb} (reduce_prep writes them)
 void reduce_range(const RedCol* cols, const RedMat* mats, int nmats, size_t height, size_t t0,
-                  size_t count, const kb::EF* invd_a, const kb::EF* invd_b, const kb::EF& ya,
-                  const kb::EF& yb, bool has_b, kb::EF* ro, hipStream_t st, int ncols = 0);
+                  size_t count, const kb::EF* invd_a, const kb::EF* invd_b, const kb::EF* yab,
+                  bool has_b, kb::EF* ro, hipStream_t st, int ncols = 0);
+// The alpha-dependent fields of the reduced-opening descriptors, computed on the device once the
+// FRI batching challenge alpha is known (the host builds the rest while the openings run):
+//   column c: ca = alpha^e0 (its position in the height's reduction order), and the job's
+//   ya = sum ca y_a, yb = yb_fold * sum ca alpha^w(m) y_b  (y from the opened-value buffer);
+//   matrix m: kb = alpha^w * fold.
+struct RedColPrep {
+  uint32_t e0, ia, ib;  // ib = UINT32_MAX: the matrix is opened at one point
+  uint32_t w;           // the column's matrix width (alpha^w for the second point)
+};
+struct RedMatPrep {
+  uint32_t w, fold;     // kb = alpha^w * fold (fold: Montgomery base-field factor)
+};
+struct RedJobPrep {
+  uint32_t col0, ncols, mat0, nmats;
+  uint32_t yb_fold, pad[3];
+};
+void reduce_prep(RedCol* cols, const RedColPrep* cp, RedMat* mats, const RedMatPrep* mp,
+                 const RedJobPrep* jp, int njobs, const kb::EF* opened, const kb::EF* alpha,
+                 kb::EF* yab, hipStream_t st);
 // The transcript after the commit phase, on the device (prover.rs:470 open -> TwoAdicFriPcs
 // [p3-recalled]: observe the final constant, grind, sample the query indices) with no host round
 // trip.  c: the challenger, in device memory -- taken as is when fri_state is null (no FRI round),

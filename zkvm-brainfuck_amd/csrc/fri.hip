@@ -256,8 +256,10 @@ constexpr int RED_STEP = BFZ_RED_STEP;
 __global__ __launch_bounds__(256) void k_reduce(const RedCol* __restrict__ cols,
                                                 const RedMat* __restrict__ mats, int nmats,
                                                 size_t t0, size_t t1, const EF* __restrict__ invd_a,
-                                                const EF* __restrict__ invd_b, EF ya, EF yb,
-                                                int has_b, int logH, EF* __restrict__ ro) {
+                                                const EF* __restrict__ invd_b,
+                                                const EF* __restrict__ yab, int has_b, int logH,
+                                                EF* __restrict__ ro) {
+  const EF ya = yab[0], yb = yab[1];
   for (size_t t = t0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < t1;
        t += (size_t)gridDim.x * blockDim.x) {
     EF sa = ef_zero(), sb = ef_zero();
@@ -662,17 +664,78 @@ void open_batch(std::vector<OpenDesc>& ds, int np, hipStream_t st) {
   KCHECK();
 }
 
+// One block per reduction job (LDE height): the columns' alpha powers and the job's ya / yb
+// (block sum), and its matrices' kb.
+__device__ __forceinline__ EF ef_pow_u32(EF a, uint32_t e) {
+  EF r = ef_one();
+  while (e) {
+    if (e & 1) r = ef_mul(r, a);
+    a = ef_mul(a, a);
+    e >>= 1;
+  }
+  return r;
+}
+__global__ __launch_bounds__(256) void k_reduce_prep(RedCol* __restrict__ cols,
+                                                     const RedColPrep* __restrict__ cp,
+                                                     RedMat* __restrict__ mats,
+                                                     const RedMatPrep* __restrict__ mp,
+                                                     const RedJobPrep* __restrict__ jp,
+                                                     const EF* __restrict__ opened,
+                                                     const EF* __restrict__ alpha_p,
+                                                     EF* __restrict__ yab) {
+  const RedJobPrep j = jp[blockIdx.x];
+  const EF alpha = *alpha_p;
+  EF ya = ef_zero(), yb = ef_zero();
+  for (uint32_t i = threadIdx.x; i < j.ncols; i += blockDim.x) {
+    const RedColPrep p = cp[j.col0 + i];
+    const EF ca = ef_pow_u32(alpha, p.e0);
+    cols[j.col0 + i].ca = ca;
+    ya = ef_add(ya, ef_mul(ca, opened[p.ia]));
+    if (p.ib != 0xffffffffu) yb = ef_add(yb, ef_mul(ef_mul(ca, ef_pow_u32(alpha, p.w)), opened[p.ib]));
+  }
+  for (uint32_t i = threadIdx.x; i < j.nmats; i += blockDim.x) {
+    const RedMatPrep m = mp[j.mat0 + i];
+    mats[j.mat0 + i].kb = ef_mul_base(ef_pow_u32(alpha, m.w), m.fold);
+  }
+  __shared__ EF sh[2][4];
+  ya = wave_sum(ya);
+  yb = wave_sum(yb);
+  if ((threadIdx.x & 63) == 0) {
+    sh[0][threadIdx.x >> 6] = ya;
+    sh[1][threadIdx.x >> 6] = yb;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    EF a = sh[0][0], b = sh[1][0];
+    for (int q = 1; q < (int)(blockDim.x >> 6); q++) {
+      a = ef_add(a, sh[0][q]);
+      b = ef_add(b, sh[1][q]);
+    }
+    yab[2 * blockIdx.x] = a;
+    yab[2 * blockIdx.x + 1] = ef_mul_base(b, j.yb_fold);
+  }
+}
+
+void reduce_prep(RedCol* cols, const RedColPrep* cp, RedMat* mats, const RedMatPrep* mp,
+                 const RedJobPrep* jp, int njobs, const EF* opened, const EF* alpha, EF* yab,
+                 hipStream_t st) {
+  if (njobs <= 0) return;
+  hipLaunchKernelGGL(k_reduce_prep, dim3(njobs), dim3(256), 0, st, cols, cp, mats, mp, jp, opened,
+                     alpha, yab);
+  KCHECK();
+}
+
 #ifndef BFZ_RED_GRID  // k_reduce's grid-stride cap in workgroups (A/B builds)
 #define BFZ_RED_GRID 32768
 #endif
 void reduce_range(const RedCol* cols, const RedMat* mats, int nmats, size_t height, size_t t0,
-                  size_t count, const EF* invd_a, const EF* invd_b, const EF& ya, const EF& yb,
+                  size_t count, const EF* invd_a, const EF* invd_b, const EF* yab,
                   bool has_b, EF* ro, hipStream_t st, int ncols) {
   const unsigned grid = std::min<unsigned>(ceil_div(count, 256), BFZ_RED_GRID);
   KernelProbe& probe = reduce_probe();
   hipEvent_t ev0 = probe.on ? probe.begin(st) : nullptr;
   hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(256), 0, st, cols, mats, nmats, t0, t0 + count,
-                     invd_a, invd_b, ya, yb, has_b ? 1 : 0, log2i(height), ro);
+                     invd_a, invd_b, yab, has_b ? 1 : 0, log2i(height), ro);
   KCHECK();
   // the columns' words, the denominator tables read (one or two points) and ro written
   if (probe.on) probe.end(ev0, st, (double)count * (4.0 * ncols + 16.0 * (has_b ? 3 : 2)));

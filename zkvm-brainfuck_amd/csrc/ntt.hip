@@ -108,7 +108,10 @@ constexpr int R16_TILE_LOG = 14;
 constexpr int MID_CMAX = 5;
 // k_lde_mid reads every twiddle of a stage from the table instead of multiplying one loaded
 // base by the small roots (a load replaces a Montgomery product).
-constexpr bool MID_TW_LOAD = true;
+#ifndef BFZ_MID_TW_LOAD
+#define BFZ_MID_TW_LOAD 1
+#endif
+constexpr bool MID_TW_LOAD = BFZ_MID_TW_LOAD;
 
 __device__ __forceinline__ int lds_pad(int idx, int c) { return c < 5 ? idx + (idx >> 4) : idx; }
 

@@ -1000,6 +1000,74 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
                                hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipEventRecord(gev[g], st));
   }
+  // ---- reduced-opening descriptors (TwoAdicFriPcs::open, prover.rs:460-470), built while the
+  // openings run: per LDE height, every column of every matrix opened there in round order; the
+  // alpha-dependent parts (column coefficients alpha^k, the matrices' alpha^w, the job's ya / yb)
+  // are filled by reduce_prep on the device once alpha is known, so the host's work after the
+  // last opened value is observing it and sampling alpha.
+  struct RedJob {
+    int lh;
+    size_t col0, mat0, ncols;
+    int nmats;
+    bool has_b;
+  };
+  std::vector<RedCol> red_cols;
+  std::vector<RedMat> red_mats;
+  std::vector<RedJob> red_jobs;
+  std::vector<RedColPrep> col_prep;
+  std::vector<RedMatPrep> mat_prep;
+  std::vector<RedJobPrep> job_prep;
+  for (int lh = Lmax; lh >= 1; lh--) {
+    const size_t col0 = red_cols.size(), mat0 = red_mats.size();
+    uint32_t e = 0;  // the reduction order: point a's columns, then point b's, matrix by matrix
+    bool has_b = false;
+    for (int r = 0; r < 4; r++)
+      for (size_t i = 0; i < rounds[r]->mats.size(); i++) {
+        const CMat& m = rounds[r]->mats[i];
+        if (m.log_n + LOG_BLOWUP != lh) continue;
+        const int w = m.lde.width;
+        const bool two = mp[r][i].npts == 2;
+        RedMat rm{};
+        rm.first = (int)(red_cols.size() - col0);
+        rm.count = w;
+        rm.has_b = two ? 1 : 0;
+        for (int c = 0; c < w; c++) {
+          RedCol rc{};
+          rc.col = m.rows() + (size_t)c * m.stride();
+          red_cols.push_back(rc);
+          col_prep.push_back({e + (uint32_t)c, (uint32_t)(mp[r][i].off[0] + c),
+                              two ? (uint32_t)(mp[r][i].off[1] + c) : 0xffffffffu, (uint32_t)w});
+        }
+        // the second point's coefficients are the first point's times alpha^w; single GPU: its
+        // denominators come from the zeta table times w_n^-1 (reduce_range), folded into kb / yb
+        mat_prep.push_back({(uint32_t)w, two && !plan.on() ? minv(two_adic_gen(m.log_n)) : ONE});
+        red_mats.push_back(rm);
+        e += (uint32_t)(mp[r][i].npts * w);
+        has_b |= two;
+      }
+    if (red_cols.size() == col0) continue;
+    const size_t ncols = red_cols.size() - col0, nm = red_mats.size() - mat0;
+    red_jobs.push_back({lh, col0, mat0, ncols, (int)nm, has_b});
+    RedJobPrep jp{};
+    jp.col0 = (uint32_t)col0;
+    jp.ncols = (uint32_t)ncols;
+    jp.mat0 = (uint32_t)mat0;
+    jp.nmats = (uint32_t)nm;
+    jp.yb_fold = has_b && !plan.on() ? minv(two_adic_gen(lh - LOG_BLOWUP)) : ONE;
+    job_prep.push_back(jp);
+  }
+  DBuf<RedCol> red_cols_d(std::max<size_t>(red_cols.size(), 1));
+  DBuf<RedMat> red_mats_d(std::max<size_t>(red_mats.size(), 1));
+  DBuf<RedColPrep> col_prep_d(std::max<size_t>(col_prep.size(), 1));
+  DBuf<RedMatPrep> mat_prep_d(std::max<size_t>(mat_prep.size(), 1));
+  DBuf<RedJobPrep> job_prep_d(std::max<size_t>(job_prep.size(), 1));
+  upload_async(red_cols_d.p, red_cols.data(), red_cols.size() * sizeof(RedCol), st);
+  upload_async(red_mats_d.p, red_mats.data(), red_mats.size() * sizeof(RedMat), st);
+  upload_async(col_prep_d.p, col_prep.data(), col_prep.size() * sizeof(RedColPrep), st);
+  upload_async(mat_prep_d.p, mat_prep.data(), mat_prep.size() * sizeof(RedMatPrep), st);
+  upload_async(job_prep_d.p, job_prep.data(), job_prep.size() * sizeof(RedJobPrep), st);
+  htrace().mark("reduce descriptors");
+
   if (dev_zeta) replay();  // the openings are queued: now the host's transcript catches up
   if (plan.on()) {  // one all-gather; sharded matrices' slices summed, replicated ones kept
     DBuf<EF> all(nvals * plan.G);
@@ -1022,6 +1090,15 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
             opened[o] = v;
           }
       }
+  }
+  // the opened values reduce_prep reads: the openings' own buffer (single GPU) or, sharded, the
+  // rank-summed values assembled above
+  DBuf<EF> opened_sum_d;
+  const EF* opened_dev = opened_d.p;
+  if (plan.on()) {
+    opened_sum_d.reset(std::max<size_t>(nvals, 1));
+    upload_async(opened_sum_d.p, opened.data(), nvals * sizeof(EF), st);
+    opened_dev = opened_sum_d.p;
   }
   auto wait_group = [&](int g) {  // the group's values in `opened`
     for (;;) {
@@ -1054,90 +1131,23 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   const EF fri_alpha = ch.sample_ef();
   htrace().mark("fri alpha");
 
-  // ---- reduced openings per LDE height: every height's column descriptors go up in one copy
-  // (a sharded height: the rank's positions only, ro holding that range)
+  // ---- reduced openings: the alpha-dependent coefficients of the descriptors built above, then
+  // one k_reduce launch per LDE height
+  DBuf<EF> alpha_yab(1 + 2 * std::max<size_t>(red_jobs.size(), 1));  // alpha, then {ya, yb} per job
+  upload_async(alpha_yab.p, &fri_alpha, sizeof(EF), st);
+  reduce_prep(red_cols_d.p, col_prep_d.p, red_mats_d.p, mat_prep_d.p, job_prep_d.p,
+              (int)red_jobs.size(), opened_dev, alpha_yab.p, alpha_yab.p + 1, st);
   std::map<int, DBuf<EF>> ro;
-  struct RedJob {
-    int lh;
-    size_t col0, mat0;
-    int nmats;
-    EF ya, yb;
-    bool has_b;
-  };
-  std::vector<RedCol> red_cols;
-  std::vector<RedMat> red_mats;
-  std::vector<RedJob> red_jobs;
-  std::map<int, EF> alpha_pow_w;  // alpha^w by matrix width
-  auto alpha_pow = [&](int w) {
-    auto it = alpha_pow_w.find(w);
-    if (it == alpha_pow_w.end()) it = alpha_pow_w.emplace(w, ef_pow(fri_alpha, (uint64_t)w)).first;
-    return it->second;
-  };
-  for (int lh = Lmax; lh >= 1; lh--) {
-    std::vector<RedCol> cols;
-    std::vector<RedMat> rmats;
-    EF ya = ef_zero(), yb = ef_zero();
-    EF a = ef_one();  // alpha^(number of reduced columns so far at this height)
-    bool has_b = false;
-    for (int r = 0; r < 4; r++)
-      for (size_t i = 0; i < rounds[r]->mats.size(); i++) {
-        const CMat& m = rounds[r]->mats[i];
-        if (m.log_n + LOG_BLOWUP != lh) continue;
-        const int w = m.lde.width;
-        const size_t base = cols.size();
-        for (int c = 0; c < w; c++) {
-          RedCol rc{};
-          rc.col = m.rows() + (size_t)c * m.stride();
-          cols.push_back(rc);
-        }
-        RedMat rm{};
-        rm.first = (int)base;
-        rm.count = w;
-        // point j's coefficients are alpha^(num_red + k): those of the second point are the
-        // first point's times alpha^w (they follow it directly in the reduction order)
-        for (int j = 0; j < mp[r][i].npts; j++) {
-          for (int c = 0; c < w; c++) {
-            const EF y = opened[mp[r][i].off[j] + c];
-            if (j == 0) {
-              cols[base + c].ca = a;
-              ya = ef_add(ya, ef_mul(a, y));
-            } else {
-              yb = ef_add(yb, ef_mul(a, y));
-              has_b = true;
-            }
-            a = ef_mul(a, fri_alpha);
-          }
-        }
-        if (mp[r][i].npts == 2) {
-          rm.has_b = 1;
-          rm.kb = alpha_pow(w);
-          // single GPU: the second point's denominators come from the zeta table times w_n^-1
-          // (reduce_range), folded in here and into yb below
-          if (!plan.on()) rm.kb = ef_mul_base(rm.kb, minv(two_adic_gen(m.log_n)));
-        }
-        rmats.push_back(rm);
-      }
-    if (cols.empty()) continue;
-    if (has_b && !plan.on()) yb = ef_mul_base(yb, minv(two_adic_gen(lh - LOG_BLOWUP)));
-    red_jobs.push_back({lh, red_cols.size(), red_mats.size(), (int)rmats.size(), ya, yb, has_b});
-    red_cols.insert(red_cols.end(), cols.begin(), cols.end());
-    red_mats.insert(red_mats.end(), rmats.begin(), rmats.end());
-  }
-  DBuf<RedCol> red_cols_d(std::max<size_t>(red_cols.size(), 1));
-  DBuf<RedMat> red_mats_d(std::max<size_t>(red_mats.size(), 1));
-  htrace().mark("reduce descriptors");
-  upload_async(red_cols_d.p, red_cols.data(), red_cols.size() * sizeof(RedCol), st);
-  upload_async(red_mats_d.p, red_mats.data(), red_mats.size() * sizeof(RedMat), st);
   for (size_t ji = 0; ji < red_jobs.size(); ji++) {
     const RedJob& j = red_jobs[ji];
-    const size_t ncols = (ji + 1 < red_jobs.size() ? red_jobs[ji + 1].col0 : red_cols.size()) - j.col0;
     const size_t H = (size_t)1 << j.lh;
     const bool sh = plan.sharded(H);
     const size_t t0 = sh ? plan.row0(H) : 0, cnt = sh ? plan.blk(H) : H;
     DBuf<EF> r(cnt);
     const Invd& d = invd.at(j.lh);
     reduce_range(red_cols_d.p + j.col0, red_mats_d.p + j.mat0, j.nmats, H, t0, cnt, d.pa(),
-                 j.has_b ? d.pb() : nullptr, j.ya, j.yb, j.has_b, r.p - t0, st, (int)ncols);
+                 j.has_b ? d.pb() : nullptr, alpha_yab.p + 1 + 2 * ji, j.has_b, r.p - t0, st,
+                 (int)j.ncols);
     ro.emplace(j.lh, std::move(r));
   }
   if (ev.on) ev.end(e3, st, &tms->open);
