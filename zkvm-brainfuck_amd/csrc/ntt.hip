@@ -260,20 +260,23 @@ __device__ __forceinline__ constexpr int tile_off(int i) { return (i << G0) + ((
 // it when the source rows are 16-byte aligned.
 // R: 2^R elements per thread and R stages per register window (R = 5, three windows of a 2^14
 // tile at 512 threads, measured DIT neutral / DIF +2%: R = 4 everywhere).
-template <bool DIF, int B, bool DIN = false, int R = 4>
+// PERSIST: a grid of a few blocks per CU walks the launch's tiles (column-major order), and each
+// block issues the HBM loads of its NEXT tile into registers before working on the current one,
+// so the load latency of a tile hides behind the previous tile's windows instead of stalling
+// all of a block's waves at its start (tiles_per_col / ntiles describe the launch).
+template <bool DIF, int B, bool DIN = false, int R = 4, bool PERSIST = false>
 __global__ __launch_bounds__(1 << (B - R)) void k_ntt_tile(const uint32_t* __restrict__ src,
                                                            uint32_t* __restrict__ dst,
                                                            size_t src_stride, size_t dst_stride,
-                                                           const uint32_t* __restrict__ tw) {
+                                                           const uint32_t* __restrict__ tw,
+                                                           uint32_t tiles_per_col = 0,
+                                                           uint32_t ntiles = 0) {
   static_assert(B >= 8 && B <= R16_TILE_LOG, "tile");
   constexpr int E = 1 << R;  // elements per thread
   constexpr int T = 1 << (B - R);
   constexpr int NW = (B + R - 1) / R;
   extern __shared__ uint32_t lds[];
   const int tid = threadIdx.x;
-  const size_t base = (size_t)blockIdx.x << B;
-  const uint32_t* S = src + (size_t)blockIdx.y * src_stride + base;
-  uint32_t* D = dst + (size_t)blockIdx.y * dst_stride + base;
   const int tpad = tid + (tid >> R);
   // A DIT's last window (g0 = B - R) holds elements tid + i T: those go straight from registers
   // to HBM (one coalesced 256-byte segment per wave instruction; -2.4% per pass).  The DIF's
@@ -286,58 +289,100 @@ __global__ __launch_bounds__(1 << (B - R)) void k_ntt_tile(const uint32_t* __res
 #endif
   constexpr bool DIRECT = BFZ_NTT_REPS == 1;
   static_assert(!DIN || (!DIF && BFZ_NTT_REPS == 1), "direct first window: DIT passes only");
-  uint32_t x[E];
-  if constexpr (DIN) {
-    const uint4* s4 = reinterpret_cast<const uint4*>(S + (tid << R));
+  static_assert(!PERSIST || BFZ_NTT_REPS == 1, "persistent tiles: production builds only");
+  uint32_t tile = PERSIST ? blockIdx.x : 0;
+  auto src_of = [&](uint32_t t) {
+    const size_t col = PERSIST ? t / tiles_per_col : blockIdx.y;
+    const size_t tx = PERSIST ? t % tiles_per_col : blockIdx.x;
+    return src + col * src_stride + (tx << B);
+  };
+  auto dst_of = [&](uint32_t t) {
+    const size_t col = PERSIST ? t / tiles_per_col : blockIdx.y;
+    const size_t tx = PERSIST ? t % tiles_per_col : blockIdx.x;
+    return dst + col * dst_stride + (tx << B);
+  };
+  // the tile's words as the first window wants them: DIN 16 consecutive words per thread, else
+  // words tid + i T (staged through LDS)
+  uint32_t pf[E];
+  auto load = [&](uint32_t t) {
+    const uint32_t* S = src_of(t);
+    if constexpr (DIN) {
+      const uint4* s4 = reinterpret_cast<const uint4*>(S + (tid << R));
 #pragma unroll
-    for (int q = 0; q < E / 4; q++) {
-      const uint4 v = s4[q];
-      x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
+      for (int q = 0; q < E / 4; q++) {
+        const uint4 v = s4[q];
+        pf[4 * q] = v.x; pf[4 * q + 1] = v.y; pf[4 * q + 2] = v.z; pf[4 * q + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < E; i++) pf[i] = S[i * T + tid];
     }
-  } else {
+  };
+  load(tile);
+  for (;;) {
+    uint32_t* D = dst_of(tile);
+    // the stage twiddles are the same for every tile: re-read per tile (an opaque offset) rather
+    // than hoisted out of the tile loop into ~70 registers (which halves the occupancy)
+    const uint32_t* twl = tw;
+    if constexpr (PERSIST) {
+      uint32_t z = 0;
+      asm volatile("" : "+v"(z));
+      twl = tw + z;
+    }
+    uint32_t x[E];
+    if constexpr (DIN) {
 #pragma unroll
-    for (int i = 0; i < E; i++) lds[i * (T + T / E) + tpad] = S[i * T + tid];
-  }
+      for (int i = 0; i < E; i++) x[i] = pf[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < E; i++) lds[i * (T + T / E) + tpad] = pf[i];
+    }
+    const uint32_t next = tile + gridDim.x;
+    if (PERSIST && next < ntiles) load(next);  // in flight while this tile's windows run
 #pragma nounroll
-  for (int rep = 0; rep < BFZ_NTT_REPS; rep++) {
-  int done_lo = 0, done_hi = B;
+    for (int rep = 0; rep < BFZ_NTT_REPS; rep++) {
+    int done_lo = 0, done_hi = B;
 #pragma unroll
-  for (int w = 0; w < NW; w++) {
-    const int g0 = DIF ? (B - R - R * w > 0 ? B - R - R * w : 0) : (R * w < B - R ? R * w : B - R);
-    const uint32_t m_low = tid & ((1 << g0) - 1);
-    const uint32_t m_base = m_low | ((uint32_t)(tid >> g0) << (g0 + R));
-    const uint32_t pb = m_base + (m_base >> R);
-    const bool direct_out = DIRECT && !DIF && w == NW - 1;
-    if (!DIN || w > 0) {
+    for (int w = 0; w < NW; w++) {
+      const int g0 = DIF ? (B - R - R * w > 0 ? B - R - R * w : 0) : (R * w < B - R ? R * w : B - R);
+      const uint32_t m_low = tid & ((1 << g0) - 1);
+      const uint32_t m_base = m_low | ((uint32_t)(tid >> g0) << (g0 + R));
+      const uint32_t pb = m_base + (m_base >> R);
+      const bool direct_out = DIRECT && !DIF && w == NW - 1;
+      if (!DIN || w > 0) {
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < E; i++) x[i] = lds[pb + (i << g0) + ((i << g0) >> R)];
+      }
+      int kk_lo = 0, kk_hi = R;
+      if (DIF) {
+        kk_hi = done_hi - g0 < R ? done_hi - g0 : R;
+        done_hi = g0;
+      } else {
+        kk_lo = done_lo - g0 > 0 ? done_lo - g0 : 0;
+        done_lo = g0 + R;
+      }
+      if (g0 == 0)
+        r16_window<DIF, true, false, R>(x, g0, kk_lo, kk_hi, 0, m_low, 0, twl);
+      else
+        r16_window<DIF, false, true, R>(x, g0, kk_lo, kk_hi, 0, m_low, 0, twl);
+      if (direct_out) {
+#pragma unroll
+        for (int i = 0; i < E; i++) D[i * T + tid] = x[i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < E; i++) lds[pb + (i << g0) + ((i << g0) >> R)] = x[i];
+      }
+    }
+    }
+    if (DIF || !DIRECT) {
       __syncthreads();
 #pragma unroll
-      for (int i = 0; i < E; i++) x[i] = lds[pb + (i << g0) + ((i << g0) >> R)];
+      for (int i = 0; i < E; i++) D[i * T + tid] = lds[i * (T + T / E) + tpad];
     }
-    int kk_lo = 0, kk_hi = R;
-    if (DIF) {
-      kk_hi = done_hi - g0 < R ? done_hi - g0 : R;
-      done_hi = g0;
-    } else {
-      kk_lo = done_lo - g0 > 0 ? done_lo - g0 : 0;
-      done_lo = g0 + R;
-    }
-    if (g0 == 0)
-      r16_window<DIF, true, false, R>(x, g0, kk_lo, kk_hi, 0, m_low, 0, tw);
-    else
-      r16_window<DIF, false, true, R>(x, g0, kk_lo, kk_hi, 0, m_low, 0, tw);
-    if (direct_out) {
-#pragma unroll
-      for (int i = 0; i < E; i++) D[i * T + tid] = x[i];
-    } else {
-#pragma unroll
-      for (int i = 0; i < E; i++) lds[pb + (i << g0) + ((i << g0) >> R)] = x[i];
-    }
-  }
-  }
-  if (DIF || !DIRECT) {
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < E; i++) D[i * T + tid] = lds[i * (T + T / E) + tpad];
+    if (!PERSIST || next >= ntiles) break;
+    tile = next;
+    __syncthreads();  // every wave is done with this tile's LDS before the next one's writes
   }
 }
 
@@ -807,24 +852,50 @@ static void r16_attrs() {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<false, R16_TILE_LOG, true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<true, R16_TILE_LOG, false, 4, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<false, R16_TILE_LOG, true, 4, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   done = true;
 }
 
+// BFZ_TILE_PERSIST=1: the 2^14 tiles run persistent with a prefetched next tile (A/B switch)
+static bool tile_persist() {
+  static const bool on = [] {
+    const char* e = std::getenv("BFZ_TILE_PERSIST");
+    return e && *e == '1';
+  }();
+  return on;
+}
 template <bool DIF, int B>
 static void tile_launch(dim3 grid, const uint32_t* in, size_t is, uint32_t* dst, size_t ds,
                         const uint32_t* tw, hipStream_t st) {
   constexpr int R = 4;
   const size_t lds = ((size_t)1 << B) + ((size_t)1 << (B - R));
   const dim3 block(1 << (B - R));
+  const bool din = !DIF && BFZ_NTT_REPS == 1 && ((uintptr_t)in & 15) == 0 && (is & 3) == 0;
+  if constexpr (B == R16_TILE_LOG && BFZ_NTT_REPS == 1) {
+    const uint32_t ntiles = grid.x * grid.y;
+    if (tile_persist() && ntiles > 512) {  // 2 blocks per CU (LDS-bound) x 256 CUs
+      const dim3 pgrid(512);
+      if (din)
+        hipLaunchKernelGGL((k_ntt_tile<false, B, true, R, true>), pgrid, block, lds * 4, st, in, dst,
+                           is, ds, tw, grid.x, ntiles);
+      else
+        hipLaunchKernelGGL((k_ntt_tile<DIF, B, false, R, true>), pgrid, block, lds * 4, st, in, dst,
+                           is, ds, tw, grid.x, ntiles);
+      return;
+    }
+  }
   if constexpr (!DIF && BFZ_NTT_REPS == 1) {
-    if (((uintptr_t)in & 15) == 0 && (is & 3) == 0) {
+    if (din) {
       hipLaunchKernelGGL((k_ntt_tile<false, B, true, R>), grid, block, lds * 4, st, in, dst, is,
-                         ds, tw);
+                         ds, tw, 0u, 0u);
       return;
     }
   }
   hipLaunchKernelGGL((k_ntt_tile<DIF, B, false, R>), grid, block, lds * 4, st, in, dst, is, ds,
-                     tw);
+                     tw, 0u, 0u);
 }
 
 template <bool DIF>
