@@ -173,10 +173,15 @@ def cycles_from_record(rec: "ExecutionRecordArrays", pinned: bool = False) -> np
     Everything else in the record is rebuilt on the device.  pinned: build it in bfz_host_alloc
     memory (the upload is then one DMA, no staging copy)."""
     cpu = rec.cpu
-    n = len(cpu)
-    out = pinned_empty(n, CYCLE) if pinned else np.empty(n, dtype=CYCLE)
-    if n == 0:
-        return out
+    out = pinned_empty(len(cpu), CYCLE) if pinned else np.empty(len(cpu), dtype=CYCLE)
+    out["pc"] = cpu["pc"]
+    out["mp"] = cpu["mp"]
+    out["prev_ts"] = cpu["mv_access_prev_timestamp"]
+    out["mv"] = cpu["mv"]
+    write = cpu["mv_access_kind"] == 2
+    out["prev_value"] = np.where(write, cpu["mv_access_prev_value"], 0)
+    out.view(np.uint8).reshape(-1, 16)[:, 14:16] = 0  # padding
+    return out
     # word views: a CpuEvent is 12 words (pc = 1, mp = 3, mv = low byte of 5; mv_access: kind /
     # prev_value = bytes 0 / 2 of word 6, prev_timestamp = word 8), a bfz_cycle 4 words
     src = cpu.view(np.uint32).reshape(n, CPU.itemsize // 4)
