@@ -126,9 +126,12 @@ __device__ __forceinline__ int lds_pad(int idx, int c) { return c < 5 ? idx + (i
 // table slice below 2^14 is L2-resident) instead of multiplying one loaded base by the small
 // roots -- a load replaces a Montgomery product.
 // R is the window size in stages (2^R elements per thread); every launch uses R = 4.
-template <bool DIF, bool CONST_TW, bool TW_LOAD = false, int R = 4>
+// PRE: the stage twiddles were loaded ahead into pre[(1 << kk) - 1 + l] (load_window_tw, issued
+// one window earlier so their latency hides behind that window's butterflies).
+template <bool DIF, bool CONST_TW, bool TW_LOAD = false, int R = 4, bool PRE = false>
 __device__ __forceinline__ void r16_window(uint32_t (&x)[1 << R], int g0, int kk_lo, int kk_hi, int s0,
-                                           uint32_t m_low, uint32_t lo_g, const uint32_t* __restrict__ tw) {
+                                           uint32_t m_low, uint32_t lo_g, const uint32_t* __restrict__ tw,
+                                           const uint32_t* pre = nullptr) {
   // performs stages t = g0 + kk for kk in [kk_lo, kk_hi), ascending (DIT) or descending (DIF)
   constexpr int E = 1 << R, H = E / 2;
 #pragma unroll
@@ -140,6 +143,10 @@ __device__ __forceinline__ void r16_window(uint32_t (&x)[1 << R], int g0, int kk
 #pragma unroll
       for (int l = 0; l < H; l++)
         if (l < (1 << kk)) tws[l] = DIF ? SMALL.f[(1 << kk) + l] : SMALL.i[(1 << kk) + l];
+    } else if (PRE) {
+#pragma unroll
+      for (int l = 0; l < H; l++)
+        if (l < (1 << kk)) tws[l] = pre[(1 << kk) - 1 + l];
     } else if (TW_LOAD) {  // one table load per twiddle instead of a load and a multiply
       const uint32_t* tt = tw + (1u << (s0 + g0 + kk)) + ((size_t)m_low << s0) + lo_g;
 #pragma unroll
@@ -172,6 +179,21 @@ __device__ __forceinline__ void r16_window(uint32_t (&x)[1 << R], int g0, int kk
         x[j] = lazy ? d + P : umin(d, d + P);
       }
     }
+  }
+}
+
+// The table twiddles of one tile window (s0 = lo_g = 0): pre[(1 << kk) - 1 + l] = the twiddle of
+// stage g0 + kk at position m_low + l 2^g0, for kk in [kk_lo, kk_hi).
+template <int R>
+__device__ __forceinline__ void load_window_tw(uint32_t (&pre)[(1 << R) - 1], int g0, int kk_lo,
+                                               int kk_hi, uint32_t m_low,
+                                               const uint32_t* __restrict__ tw) {
+#pragma unroll
+  for (int kk = 0; kk < R; kk++) {
+    if (kk < kk_lo || kk >= kk_hi) continue;
+#pragma unroll
+    for (int l = 0; l < (1 << kk); l++)
+      pre[(1 << kk) - 1 + l] = tw[(1u << (g0 + kk)) + m_low + ((uint32_t)l << g0)];
   }
 }
 
@@ -264,7 +286,10 @@ __device__ __forceinline__ constexpr int tile_off(int i) { return (i << G0) + ((
 // block issues the HBM loads of its NEXT tile into registers before working on the current one,
 // so the load latency of a tile hides behind the previous tile's windows instead of stalling
 // all of a block's waves at its start (tiles_per_col / ntiles describe the launch).
-template <bool DIF, int B, bool DIN = false, int R = 4, bool PERSIST = false>
+// TWPF: each window's table twiddles are loaded one window ahead (into registers, double
+// buffered) instead of at the window's start, where every wave of the block would wait for the
+// L2 round trip at the same time (the waves run in lockstep between the LDS exchanges).
+template <bool DIF, int B, bool DIN = false, int R = 4, bool PERSIST = false, bool TWPF = false>
 __global__ __launch_bounds__(1 << (B - R)) void k_ntt_tile(const uint32_t* __restrict__ src,
                                                            uint32_t* __restrict__ dst,
                                                            size_t src_stride, size_t dst_stride,
@@ -339,12 +364,38 @@ __global__ __launch_bounds__(1 << (B - R)) void k_ntt_tile(const uint32_t* __res
     }
     const uint32_t next = tile + gridDim.x;
     if (PERSIST && next < ntiles) load(next);  // in flight while this tile's windows run
+    // window w: first stage g0(w) and its stage range [kk_lo, kk_hi) (compile-time after unrolling)
+    auto win_g0 = [](int w) {
+      return DIF ? (B - R - R * w > 0 ? B - R - R * w : 0) : (R * w < B - R ? R * w : B - R);
+    };
+    auto win_range = [&](int w, int& lo, int& hi) {
+      int done_lo = 0, done_hi = B;
+      for (int v = 0; v <= w; v++) {
+        const int g = win_g0(v);
+        lo = 0;
+        hi = R;
+        if (DIF) {
+          hi = done_hi - g < R ? done_hi - g : R;
+          done_hi = g;
+        } else {
+          lo = done_lo - g > 0 ? done_lo - g : 0;
+          done_lo = g + R;
+        }
+      }
+    };
+    uint32_t pre[2][(1 << R) - 1];
+    if constexpr (TWPF) {
+      if (win_g0(0) != 0) {
+        int lo, hi;
+        win_range(0, lo, hi);
+        load_window_tw<R>(pre[0], win_g0(0), lo, hi, tid & ((1 << win_g0(0)) - 1), twl);
+      }
+    }
 #pragma nounroll
     for (int rep = 0; rep < BFZ_NTT_REPS; rep++) {
-    int done_lo = 0, done_hi = B;
 #pragma unroll
     for (int w = 0; w < NW; w++) {
-      const int g0 = DIF ? (B - R - R * w > 0 ? B - R - R * w : 0) : (R * w < B - R ? R * w : B - R);
+      const int g0 = win_g0(w);
       const uint32_t m_low = tid & ((1 << g0) - 1);
       const uint32_t m_base = m_low | ((uint32_t)(tid >> g0) << (g0 + R));
       const uint32_t pb = m_base + (m_base >> R);
@@ -354,16 +405,20 @@ __global__ __launch_bounds__(1 << (B - R)) void k_ntt_tile(const uint32_t* __res
 #pragma unroll
         for (int i = 0; i < E; i++) x[i] = lds[pb + (i << g0) + ((i << g0) >> R)];
       }
-      int kk_lo = 0, kk_hi = R;
-      if (DIF) {
-        kk_hi = done_hi - g0 < R ? done_hi - g0 : R;
-        done_hi = g0;
-      } else {
-        kk_lo = done_lo - g0 > 0 ? done_lo - g0 : 0;
-        done_lo = g0 + R;
+      int kk_lo, kk_hi;
+      win_range(w, kk_lo, kk_hi);
+      if constexpr (TWPF) {  // the next window's twiddles, in flight during this window
+        if (w + 1 < NW && win_g0(w + 1) != 0) {
+          int lo, hi;
+          win_range(w + 1, lo, hi);
+          load_window_tw<R>(pre[(w + 1) & 1], win_g0(w + 1), lo, hi,
+                            tid & ((1 << win_g0(w + 1)) - 1), twl);
+        }
       }
       if (g0 == 0)
         r16_window<DIF, true, false, R>(x, g0, kk_lo, kk_hi, 0, m_low, 0, twl);
+      else if (TWPF)
+        r16_window<DIF, false, true, R, true>(x, g0, kk_lo, kk_hi, 0, m_low, 0, twl, pre[w & 1]);
       else
         r16_window<DIF, false, true, R>(x, g0, kk_lo, kk_hi, 0, m_low, 0, twl);
       if (direct_out) {
@@ -852,6 +907,10 @@ static void r16_attrs() {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<false, R16_TILE_LOG, true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<true, R16_TILE_LOG, false, 4, false, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<false, R16_TILE_LOG, true, 4, false, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<true, R16_TILE_LOG, false, 4, true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<false, R16_TILE_LOG, true, 4, true>),
@@ -867,6 +926,16 @@ static bool tile_persist() {
   }();
   return on;
 }
+// Table twiddles loaded one window ahead in the 2^14 DIF tiles (profiles/r04/ab_twiddle_prefetch.txt:
+// DIF pass 198 -> 185 us per 2^26 elements, DIT neutral, so DIF only); BFZ_TW_PREFETCH=0 / 1
+// forces it off / on for both directions (A/B switch).
+static int tw_prefetch() {
+  static const int mode = [] {
+    const char* e = std::getenv("BFZ_TW_PREFETCH");
+    return e ? (*e == '1' ? 1 : 0) : 2;  // 2: DIF only
+  }();
+  return mode;
+}
 template <bool DIF, int B>
 static void tile_launch(dim3 grid, const uint32_t* in, size_t is, uint32_t* dst, size_t ds,
                         const uint32_t* tw, hipStream_t st) {
@@ -874,6 +943,17 @@ static void tile_launch(dim3 grid, const uint32_t* in, size_t is, uint32_t* dst,
   const size_t lds = ((size_t)1 << B) + ((size_t)1 << (B - R));
   const dim3 block(1 << (B - R));
   const bool din = !DIF && BFZ_NTT_REPS == 1 && ((uintptr_t)in & 15) == 0 && (is & 3) == 0;
+  if constexpr (B == R16_TILE_LOG && BFZ_NTT_REPS == 1) {
+    if (tw_prefetch() == 1 || (DIF && tw_prefetch() == 2)) {
+      if (din)
+        hipLaunchKernelGGL((k_ntt_tile<false, B, true, R, false, true>), grid, block, lds * 4, st, in,
+                           dst, is, ds, tw, 0u, 0u);
+      else
+        hipLaunchKernelGGL((k_ntt_tile<DIF, B, false, R, false, true>), grid, block, lds * 4, st, in,
+                           dst, is, ds, tw, 0u, 0u);
+      return;
+    }
+  }
   if constexpr (B == R16_TILE_LOG && BFZ_NTT_REPS == 1) {
     const uint32_t ntiles = grid.x * grid.y;
     if (tile_persist() && ntiles > 512) {  // 2 blocks per CU (LDS-bound) x 256 CUs
