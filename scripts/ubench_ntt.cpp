@@ -38,8 +38,12 @@ static int lde_mode(int L, int w, int reps) {
   float ms;
   CHK(hipEventElapsedTime(&ms, e0, e1));
   const double s = ms * 1e-3 / reps;
-  printf("coset LDE 2^%d x %d: %8.1f us  %7.0f GB/s (12 B/input elem)  %6.2f T elem-stages/s\n", L, w,
-         s * 1e6, 12.0 * words / s / 1e9, 3.0 * L * words / s / 1e12);
+  std::vector<uint32_t> o(2 * words);
+  CHK(hipMemcpy(o.data(), b, 2 * words * 4, hipMemcpyDeviceToHost));
+  uint64_t hsh = 1469598103934665603ull;
+  for (uint32_t v : o) hsh = (hsh ^ v) * 1099511628211ull;
+  printf("coset LDE 2^%d x %d: %8.1f us  %7.0f GB/s (12 B/input elem)  %6.2f T elem-stages/s  out %016llx\n",
+         L, w, s * 1e6, 12.0 * words / s / 1e9, 3.0 * L * words / s / 1e12, (unsigned long long)hsh);
   return 0;
 }
 
