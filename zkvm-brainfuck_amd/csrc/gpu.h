@@ -7,6 +7,7 @@
 // evaluation, FRI reduction and openings all stream columns with unit stride.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <cstdint>
 #include <cstdio>
@@ -147,6 +148,27 @@ Twiddles& twiddles();
 hipStream_t stream();
 // Every C entry point runs under one process-wide API lock (capi.cpp guarded()); proof code
 // that keeps process-global state (open_impl's pinned mailboxes) checks that it is held.
+// Profiler ranges named after the reference's tracing spans (crates/stark/src/prover.rs:63,281,
+// 333,355,410,460,575): roctx push / pop, recorded by `rocprofv3 --marker-trace` beside the kernel
+// trace.  They are host-side spans (launches plus the transcript's waits), as the reference's are
+// host spans around its CPU work; the kernels they enqueue run on the stream under them.
+struct Span {
+  bool open = false;
+  explicit Span(const char* name) { begin(name); }
+  ~Span() { end(); }
+  Span(const Span&) = delete;
+  Span& operator=(const Span&) = delete;
+  void begin(const char* name) {
+    end();
+    roctxRangePushA(name);
+    open = true;
+  }
+  void end() {
+    if (open) roctxRangePop();
+    open = false;
+  }
+};
+
 int& api_lock_depth();  // per thread
 struct ApiLockScope {
   ApiLockScope() { api_lock_depth()++; }

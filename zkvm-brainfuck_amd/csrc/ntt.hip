@@ -289,7 +289,12 @@ __device__ __forceinline__ constexpr int tile_off(int i) { return (i << G0) + ((
 // TWPF: each window's table twiddles are loaded one window ahead (into registers, double
 // buffered) instead of at the window's start, where every wave of the block would wait for the
 // L2 round trip at the same time (the waves run in lockstep between the LDS exchanges).
-template <bool DIF, int B, bool DIN = false, int R = 4, bool PERSIST = false, bool TWPF = false>
+// WS (B >= 13, R = 4): windows g0 = 0, 4, 6, B-4 (DIT; the DIF the reverse).  The threads of a
+// wave hold the same 1024 consecutive elements (bits [10, B) = the wave index) in every window
+// with g0 <= 6, so the exchanges between such windows go through the wave's own LDS region with
+// a wave-level fence instead of a block barrier: one block barrier per DIT tile instead of three.
+template <bool DIF, int B, bool DIN = false, int R = 4, bool PERSIST = false, bool TWPF = false,
+          bool WS = false>
 __global__ __launch_bounds__(1 << (B - R)) void k_ntt_tile(const uint32_t* __restrict__ src,
                                                            uint32_t* __restrict__ dst,
                                                            size_t src_stride, size_t dst_stride,
@@ -313,8 +318,13 @@ __global__ __launch_bounds__(1 << (B - R)) void k_ntt_tile(const uint32_t* __res
 #define BFZ_NTT_REPS 1
 #endif
   constexpr bool DIRECT = BFZ_NTT_REPS == 1;
+  // (The WS DIF's last window, 16 consecutive words per thread, stored straight to HBM as four
+  // 16-byte stores instead of through LDS: DIF pass 173-179 -> 192-199 us, profiles/r04/
+  // ab_tile_dout.txt.)
   static_assert(!DIN || (!DIF && BFZ_NTT_REPS == 1), "direct first window: DIT passes only");
+  constexpr bool DINL = DIN;
   static_assert(!PERSIST || BFZ_NTT_REPS == 1, "persistent tiles: production builds only");
+  static_assert(!WS || (R == 4 && B >= 13), "wave-local windows: 2^13 / 2^14 tiles");
   uint32_t tile = PERSIST ? blockIdx.x : 0;
   auto src_of = [&](uint32_t t) {
     const size_t col = PERSIST ? t / tiles_per_col : blockIdx.y;
@@ -331,7 +341,7 @@ __global__ __launch_bounds__(1 << (B - R)) void k_ntt_tile(const uint32_t* __res
   uint32_t pf[E];
   auto load = [&](uint32_t t) {
     const uint32_t* S = src_of(t);
-    if constexpr (DIN) {
+    if constexpr (DINL) {
       const uint4* s4 = reinterpret_cast<const uint4*>(S + (tid << R));
 #pragma unroll
       for (int q = 0; q < E / 4; q++) {
@@ -355,7 +365,7 @@ __global__ __launch_bounds__(1 << (B - R)) void k_ntt_tile(const uint32_t* __res
       twl = tw + z;
     }
     uint32_t x[E];
-    if constexpr (DIN) {
+    if constexpr (DINL) {
 #pragma unroll
       for (int i = 0; i < E; i++) x[i] = pf[i];
     } else {
@@ -366,6 +376,10 @@ __global__ __launch_bounds__(1 << (B - R)) void k_ntt_tile(const uint32_t* __res
     if (PERSIST && next < ntiles) load(next);  // in flight while this tile's windows run
     // window w: first stage g0(w) and its stage range [kk_lo, kk_hi) (compile-time after unrolling)
     auto win_g0 = [](int w) {
+      if (WS) {
+        constexpr int g[4] = {0, 4, 6, B - 4};
+        return DIF ? g[3 - w] : g[w];
+      }
       return DIF ? (B - R - R * w > 0 ? B - R - R * w : 0) : (R * w < B - R ? R * w : B - R);
     };
     auto win_range = [&](int w, int& lo, int& hi) {
@@ -400,8 +414,14 @@ __global__ __launch_bounds__(1 << (B - R)) void k_ntt_tile(const uint32_t* __res
       const uint32_t m_base = m_low | ((uint32_t)(tid >> g0) << (g0 + R));
       const uint32_t pb = m_base + (m_base >> R);
       const bool direct_out = DIRECT && !DIF && w == NW - 1;
-      if (!DIN || w > 0) {
-        __syncthreads();
+      if (!DINL || w > 0) {
+        if (WS && w > 0 && win_g0(w - 1) <= 6 && g0 <= 6) {  // the wave's own 1024 elements
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        } else {
+          __syncthreads();
+        }
 #pragma unroll
         for (int i = 0; i < E; i++) x[i] = lds[pb + (i << g0) + ((i << g0) >> R)];
       }
@@ -915,6 +935,14 @@ static void r16_attrs() {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ntt_tile<false, R16_TILE_LOG, true, 4, true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  const void* ws[] = {(const void*)&k_ntt_tile<true, R16_TILE_LOG, false, 4, false, false, true>,
+                      (const void*)&k_ntt_tile<true, R16_TILE_LOG, false, 4, false, true, true>,
+                      (const void*)&k_ntt_tile<false, R16_TILE_LOG, false, 4, false, false, true>,
+                      (const void*)&k_ntt_tile<false, R16_TILE_LOG, false, 4, false, true, true>,
+                      (const void*)&k_ntt_tile<false, R16_TILE_LOG, true, 4, false, false, true>,
+                      (const void*)&k_ntt_tile<false, R16_TILE_LOG, true, 4, false, true, true>};
+  for (const void* f : ws)
+    HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   done = true;
 }
 
@@ -936,6 +964,16 @@ static int tw_prefetch() {
   }();
   return mode;
 }
+// 2^14 tiles with wave-local LDS exchanges (k_ntt_tile WS): default since
+// profiles/r04/ab_tile_ws.txt (DIT pass 180 -> 167-172 us per 2^26 elements, DIF neutral, coset
+// LDE 2^22 x 8 471 -> 466 us, bit-exact); BFZ_TILE_WS=0 turns it off (A/B switch)
+static bool tile_ws() {
+  static const bool on = [] {
+    const char* e = std::getenv("BFZ_TILE_WS");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
 template <bool DIF, int B>
 static void tile_launch(dim3 grid, const uint32_t* in, size_t is, uint32_t* dst, size_t ds,
                         const uint32_t* tw, hipStream_t st) {
@@ -944,6 +982,24 @@ static void tile_launch(dim3 grid, const uint32_t* in, size_t is, uint32_t* dst,
   const dim3 block(1 << (B - R));
   const bool din = !DIF && BFZ_NTT_REPS == 1 && ((uintptr_t)in & 15) == 0 && (is & 3) == 0;
   if constexpr (B == R16_TILE_LOG && BFZ_NTT_REPS == 1) {
+    if (tile_ws()) {
+      const bool pf = tw_prefetch() == 1 || (DIF && tw_prefetch() == 2);
+      if (din) {
+        if (pf)
+          hipLaunchKernelGGL((k_ntt_tile<false, B, true, R, false, true, true>), grid, block, lds * 4,
+                             st, in, dst, is, ds, tw, 0u, 0u);
+        else
+          hipLaunchKernelGGL((k_ntt_tile<false, B, true, R, false, false, true>), grid, block, lds * 4,
+                             st, in, dst, is, ds, tw, 0u, 0u);
+      } else if (pf) {
+        hipLaunchKernelGGL((k_ntt_tile<DIF, B, false, R, false, true, true>), grid, block, lds * 4, st,
+                           in, dst, is, ds, tw, 0u, 0u);
+      } else {
+        hipLaunchKernelGGL((k_ntt_tile<DIF, B, false, R, false, false, true>), grid, block, lds * 4, st,
+                           in, dst, is, ds, tw, 0u, 0u);
+      }
+      return;
+    }
     if (tw_prefetch() == 1 || (DIF && tw_prefetch() == 2)) {
       if (din)
         hipLaunchKernelGGL((k_ntt_tile<false, B, true, R, false, true>), grid, block, lds * 4, st, in,

@@ -507,6 +507,7 @@ void commit_main_impl(MainData& md, ProofScope& ps, bool fetch_root = true) {
     md.hn[k] = dt.heights[md.order[k]];
   }
   hipEvent_t e0 = ps.ev.on ? ps.ev.begin(st) : nullptr;
+  Span span("commit to main traces");  // (no span of its own in the reference: commit_main)
   const Plan plan = make_plan();
   md.mainr = Round();
   md.mainr.mats.resize(nc);
@@ -634,6 +635,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   htrace().mark("perm challenges");
 
   hipEvent_t e1 = ev.on ? ev.begin(st) : nullptr;
+  Span span("generate permutation traces");  // prover.rs:281 (rows, then each chip's LDE)
   Round permr;
   permr.mats.resize(nc);
   // cums_d: the chips' cumulative sums, then (fetched together) the main, permutation and
@@ -659,13 +661,16 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
              tms ? &split : nullptr);
   }
   hipEvent_t bh = ev.on ? ev.begin(st) : nullptr;
+  span.begin("commit to permutation traces");  // prover.rs:333
   permr.commit(st, /*fetch_root=*/false);
+  span.end();
   if (ev.on) ev.end(bh, st, &tms->perm_hash);
   if (ev.on) ev.end(e1, st, &tms->perm);
   HIP_CHECK(hipMemcpyAsync(cums_d.p + nc + 2, permr.tree.layers.back().p, 32, hipMemcpyDeviceToDevice, st));
 
   // ---- quotient (prover.rs:344-412)
   hipEvent_t e2 = ev.on ? ev.begin(st) : nullptr;
+  span.begin("compute quotient values");  // prover.rs:355 (values, then the chunk LDEs)
   Round quotr;
   quotr.mats.resize(2 * nc);
   std::vector<DBuf<EF>> apows(nc);
@@ -771,7 +776,9 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     }
   }
   qv.clear();
+  span.begin("commit to quotient traces");  // prover.rs:410
   quotr.commit(st, /*fetch_root=*/false);
+  span.end();
   if (ev.on) ev.end(e2, st, &tms->quotient);
   HIP_CHECK(hipMemcpyAsync(cums_d.p + nc + 4, quotr.tree.layers.back().p, 32, hipMemcpyDeviceToDevice, st));
   // Single GPU: zeta is sampled on the device too (prover.rs:415), so the openings below are
@@ -814,6 +821,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
 
   // ---- PCS open: opened values (prover.rs:417-470)
   hipEvent_t e3 = ev.on ? ev.begin(st) : nullptr;
+  span.begin("open multi batches");  // prover.rs:460 (opened values, reduced openings, FRI, queries)
   const Round* rounds[4] = {&pk.prep, &mainr, &permr, &quotr};
   struct MatPts {
     int npts;
@@ -1396,6 +1404,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   if (after) *after = ch;  // the transcript is complete: MachineProver::open's &mut challenger
   const uint32_t* words = tbox + T_W;
   if (ev.on) ev.end(e4, st, &tms->fri);
+  span.end();
 
   // ---- serialize (BFZ1 normal form)
   Writer w;
@@ -1464,8 +1473,12 @@ std::vector<uint8_t> prove_events(const ProvingKey& pk, const DeviceEvents& ev,
     HIP_CHECK(hipEventRecord(a, st));
   }
   htrace().mark("proof start", true);
+  Span span("prove_shard");  // prover.rs:575
   DeviceTraces dt;
-  generate_traces_device(ev, dt, st);
+  {
+    Span gen("generate traces for shard");  // prover.rs:63
+    generate_traces_device(ev, dt, st);
+  }
   htrace().mark("traces launched");
   if (timing) HIP_CHECK(hipEventRecord(b, st));
   auto proof = prove_device(pk, dt, opt, times);
