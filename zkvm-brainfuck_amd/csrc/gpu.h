@@ -11,6 +11,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <unordered_map>
 #include <stdexcept>
@@ -202,18 +203,24 @@ struct KernelProbe {
     HIP_CHECK(hipEventRecord(e, st));
     return e;
   }
-  void end(hipEvent_t b, hipStream_t st, double nbytes) {
+  std::vector<const char*> ev_tag;
+  // BFZ_PROBE_DUMP=1: every timed launch on stderr ("probe <tag> <units> <ms>"), for per-kernel
+  // rates (e.g. permutations per second of k_compress against k_hash_leaves)
+  bool dump = std::getenv("BFZ_PROBE_DUMP") != nullptr;
+  void end(hipEvent_t b, hipStream_t st, double nbytes, const char* tag = "") {
     hipEvent_t e;
     HIP_CHECK(hipEventCreate(&e));
     HIP_CHECK(hipEventRecord(e, st));
     ev.push_back({b, e});
     ev_bytes.push_back(nbytes);
+    ev_tag.push_back(tag);
   }
   void collect() {
     for (size_t i = 0; i < ev.size(); i++) {
       HIP_CHECK(hipEventSynchronize(ev[i].second));
       float t = 0;
       HIP_CHECK(hipEventElapsedTime(&t, ev[i].first, ev[i].second));
+      if (dump) std::fprintf(stderr, "probe %s %.0f %.5f\n", ev_tag[i], ev_bytes[i], t);
       ms += t;
       bytes += ev_bytes[i];
       launches++;
@@ -222,6 +229,7 @@ struct KernelProbe {
     }
     ev.clear();
     ev_bytes.clear();
+    ev_tag.clear();
   }
   void reset() {
     collect();

@@ -286,7 +286,8 @@ static void launch_layer(MerkleTree& t, int L, size_t j0, size_t count,
     hipLaunchKernelGGL(k_compress, dim3(ceil_div(count, 256)), dim3(256), 0, st, prev, j0, count,
                        t.layers[L].p, cl);
     // one compression, plus the injected rows' sponge and one more compression if any
-    if (probe.on) probe.end(ev0, st, (double)count * (cl.n ? 2 + (cl.n + 7) / 8 : 1));
+    if (probe.on)
+      probe.end(ev0, st, (double)count * (cl.n ? 2 + (cl.n + 7) / 8 : 1), cl.n ? "k_compress+inject" : "k_compress");
   }
   KCHECK();
 }
@@ -401,7 +402,7 @@ void merkle_build(const std::vector<MatRef>& mats, MerkleTree& t, hipStream_t st
     hipLaunchKernelGGL(k_hash_leaves, dim3(ceil_div(count, 256)), dim3(256), 0, st, cl, r0,
                        count, t.layers[0].p);
     KCHECK();
-    if (probe.on) probe.end(ev0, st, (double)count * ((cl.n + 7) / 8));
+    if (probe.on) probe.end(ev0, st, (double)count * ((cl.n + 7) / 8), "k_hash_leaves");
   };
   if (shard_tree(h0)) {
     build_sharded(t, h0, sorted, next, leaves, st, fetch_root);
@@ -421,7 +422,7 @@ static void hash_rows8_range(const uint32_t* rows, size_t r0, size_t count, uint
     hipEvent_t ev0 = probe.on ? probe.begin(st) : nullptr;
     hipLaunchKernelGGL(k_hash_rows8, dim3(ceil_div(count, 256)), dim3(256), 0, st, rows, r0, count,
                        digests);
-    if (probe.on) probe.end(ev0, st, (double)count);
+    if (probe.on) probe.end(ev0, st, (double)count, "k_hash_rows8");
   }
   KCHECK();
 }
