@@ -62,15 +62,21 @@ def test_poseidon2_extreme_states_parity():
 
 
 def test_poseidon2_lane_mode_parity():
-    """16-lanes-per-state permutation (DPP cross-lane MDS) == oracle."""
+    """16-lanes-per-state permutation (DPP cross-lane MDS, signed lazy form) == oracle, with the
+    golden vector, the extreme states of the test above and 4096 random states."""
     rng = np.random.default_rng(3)
-    st = rng.integers(0, P, size=(100, 16), dtype=np.uint64).astype(np.uint32)
+    st = rng.integers(0, P, size=(4096 + 16, 16), dtype=np.uint64).astype(np.uint32)
     st[0] = GOLDEN["poseidon2"][0]["in"]
     dev = mont(st).reshape(-1).copy()
+    edge = [np.zeros(16), np.full(16, P - 1), np.ones(16), np.tile([P - 1, 0], 8),
+            np.tile([0, P - 1], 8), np.full(16, (P - 1) // 2), np.full(16, (P + 1) // 2),
+            np.arange(P - 16, P), np.tile([P - 1, 1], 8)]
+    dev.reshape(-1, 16)[1:1 + len(edge)] = np.array(edge, dtype=np.uint64).astype(np.uint32)
+    ref_in = unmont(dev).reshape(-1)
     _lib.check(_lib.lib().bfz_poseidon2_permute_small(dev.ctypes.data_as(P32), len(st)))
     got = unmont(dev).reshape(-1, 16)
     assert got[0].tolist() == GOLDEN["poseidon2"][0]["out"]
-    assert np.array_equal(got, O.poseidon2(st.reshape(-1)).reshape(-1, 16))
+    assert np.array_equal(got, O.poseidon2(ref_in).reshape(-1, 16))
 
 
 @pytest.mark.parametrize("logn,w", [(0, 3), (1, 2), (4, 31), (5, 1), (10, 45), (13, 7), (14, 5),

@@ -382,23 +382,107 @@ __device__ __forceinline__ uint32_t sum_lanes16(uint32_t v) {
   return madd(v, dpp<DPP_ROR8>(v));
 }
 
+// Signed lazy form in lane mode (BFZ_P2_LANE_SIGNED, default): the throughput permutation's
+// arithmetic (poseidon2_permute above: R^2-form 64-bit S-box outputs folded to < 2^55.1,
+// MDS-light in 64-bit adds, one signed reduction per element and round, round constants in front
+// of the MDS layer) with lane l holding element l and the cross-lane terms moved by DPP (both
+// halves of a 64-bit value): 619 VALU instructions per lane against 836 for the canonical form
+// below (three-instruction modular adds, five-instruction products).  Lane mode is latency-bound
+// (tree tops, the FRI tail, the device challenger): k_compress_top 18.0 -> 15.3 us and k_fri_tail
+// 107 -> 91 us per launch (profiles/r04/ab_lane_signed.txt); BFZ_P2_LANE_SIGNED=0 builds the old.
+#ifndef BFZ_P2_LANE_SIGNED
+#define BFZ_P2_LANE_SIGNED 1
+#endif
+// (mov_dpp: every lane of the row is a valid source for these controls, so no "old" value is
+// needed -- update_dpp(0, ...) would cost a v_mov of zero into every destination first)
+template <int CTRL>
+__device__ __forceinline__ int64_t dpp64(int64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(uint64_t)v, CTRL, 0xf, 0xf, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)((uint64_t)v >> 32), CTRL, 0xf, 0xf, false);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+// mds_light64 with one element per lane: M4 inside each quad, then the four blocks' sums.
+// (Plain 64-bit C++ adds instead of lshl_add64 compile to more instructions here: the compiler
+// rebuilds each DPP'd value as lo + (hi << 32), two 64-bit adds per use.)
+__device__ __forceinline__ int64_t mds_light64_lane(int64_t y) {
+  const int64_t a1 = dpp64<DPP_QROT1>(y), a2 = dpp64<DPP_QROT2>(y), a3 = dpp64<DPP_QROT3>(y);
+  const int64_t p1 = lshl_add64<1>(y, a1);                      // 2 y + a1
+  const int64_t m = lshl_add64<0>(p1, lshl_add64<0>(lshl_add64<1>(a1, a2), a3));  // + 2 a1 + a2 + a3
+  const int64_t t = lshl_add64<0>(m, dpp64<DPP_ROR8>(m));
+  return lshl_add64<0>(m, lshl_add64<0>(t, dpp64<DPP_ROR4>(t)));
+}
+__device__ __forceinline__ int64_t sum_lanes16_64(int64_t v) {
+  v = lshl_add64<0>(v, dpp64<DPP_ROR1>(v));
+  v = lshl_add64<0>(v, dpp64<DPP_ROR2>(v));
+  v = lshl_add64<0>(v, dpp64<DPP_ROR4>(v));
+  return lshl_add64<0>(v, dpp64<DPP_ROR8>(v));
+}
+
 // The lane's round constants, loaded once per kernel by callers that permute in a loop (the
 // loads are a memory round trip on a latency-bound chain).
 struct LaneConsts {
+#if BFZ_P2_LANE_SIGNED
+  int32_t kin[4], kte[3];  // P2PRE.init[r][lane], P2PRE.term[r][lane]
+  int32_t init0, d, rct;   // P2PRE.init0[lane], P2M.d[lane], P2S.rc_term[0][lane]
+#else
   uint32_t rce[8];
   uint32_t dg;
+#endif
 };
 __device__ __forceinline__ LaneConsts lane_consts(int lane) {
   LaneConsts k;
+#if BFZ_P2_LANE_SIGNED
+#pragma unroll
+  for (int r = 0; r < 4; r++) k.kin[r] = P2PRE.init[r][lane];
+#pragma unroll
+  for (int r = 0; r < 3; r++) k.kte[r] = P2PRE.term[r][lane];
+  k.init0 = P2PRE.init0[lane];
+  k.d = P2M.d[lane];
+  k.rct = P2S.rc_term[0][lane];
+#else
 #pragma unroll
   for (int r = 0; r < 4; r++) {
     k.rce[r] = P2.ext_init[r][lane];
     k.rce[4 + r] = P2.ext_term[r][lane];
   }
   k.dg = P2.diag[lane];
+#endif
   return k;
 }
 
+#if BFZ_P2_LANE_SIGNED
+// One external round per r (as external_rounds_pre): x -> x^3 R^2 + K[r] -> fold -> MDS-light.
+__device__ __forceinline__ int64_t external_rounds_lane(int32_t x, const int32_t* K, int nk) {
+  int64_t y = 0;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    if (r) x = mred_s(y);
+    const int64_t c3 = (int64_t)mred_s((int64_t)x * x) * x + (r < nk ? K[r] : 0);
+    y = mds_light64_lane(fold_s(c3));
+  }
+  return y;
+}
+__device__ __forceinline__ uint32_t poseidon2_permute_lane(uint32_t v, int lane,
+                                                           const LaneConsts& kc) {
+  // initial MDS-light on x R^2 + M^-1 rc_0 (x = v, Montgomery form, canonical)
+  int64_t y = mds_light64_lane((int64_t)((uint64_t)v * C32) + kc.init0);
+  y = external_rounds_lane(mred_s(y), kc.kin, 4);
+  int32_t t = mred_s(y);  // rc_int[0] already in lane 0's value
+#pragma unroll
+  for (int r = 0; r < 13; r++) {
+    // lane 0 carries the S-box element; every lane computes a cube, lane 0's is used
+    const int32_t c = mred_s(cube_s(t));
+    const int32_t u = lane == 0 ? c : t;
+    const int32_t sp = mred_s(sum_lanes16_64((int64_t)u));  // the plain sum of the state
+    const int64_t q = opaque64((int64_t)P2S.k * sp);
+    const int32_t add = r < 12 ? (lane == 0 ? P2S.rc_int[r + 1] : 0) : kc.rct;
+    t = mred_s((int64_t)kc.d * u + (q + add));
+  }
+  y = external_rounds_lane(t, kc.kte, 3);
+  const uint32_t r = (uint32_t)mred_s(y);
+  return umin(r, r + P);
+}
+#else
 __device__ __forceinline__ uint32_t poseidon2_permute_lane(uint32_t v, int lane,
                                                            const LaneConsts& kc) {
   const uint32_t* rce = kc.rce;
@@ -416,6 +500,7 @@ __device__ __forceinline__ uint32_t poseidon2_permute_lane(uint32_t v, int lane,
   for (int r = 0; r < 4; r++) v = mds_light_lane(cube(madd(v, rce[4 + r])));
   return v;
 }
+#endif
 __device__ __forceinline__ uint32_t poseidon2_permute_lane(uint32_t v, int lane) {
   return poseidon2_permute_lane(v, lane, lane_consts(lane));
 }
