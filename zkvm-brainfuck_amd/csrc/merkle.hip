@@ -153,7 +153,10 @@ constexpr int TOP_NODES = 64;   // fills a 1024-thread block in one lane-mode pa
 constexpr int TOP_LAYERS = 7;   // 64 nodes -> 1
 // Medium layers (TOP_NODES < nodes <= LANE_LAYER_MAX) go to lane mode: a single-lane launch
 // of this size is one permutation latency long (~12 us) while 16 lanes per node finish sooner.
-constexpr size_t LANE_LAYER_MAX = (size_t)1 << 14;
+#ifndef BFZ_LANE_LAYER_LOG
+#define BFZ_LANE_LAYER_LOG 14
+#endif
+constexpr size_t LANE_LAYER_MAX = (size_t)1 << BFZ_LANE_LAYER_LOG;
 constexpr int MAXTOP = TOP_LAYERS;
 struct TopLayers {
   uint32_t* out[MAXTOP];
