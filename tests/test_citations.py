@@ -60,3 +60,18 @@ def test_reference_citations_are_in_range():
                 bad.append(f"{src}:{line}: {path}:{span} (file has {longest} lines)")
     assert checked > 300, checked  # the scan found the citations
     assert not bad, "\n".join(bad)
+
+
+def test_profiler_ranges_use_the_reference_span_names():
+    """The roctx ranges of prover.hip (gpu.h Span) carry the names of the reference's tracing
+    spans (crates/stark/src/prover.rs), so a rocprofv3 --marker-trace of bfz lines up with a
+    tracing log of the reference; a range without a reference span says so in its comment."""
+    ref = os.path.join(REF, "crates/stark/src/prover.rs")
+    if not os.path.exists(ref):
+        pytest.skip("reference checkout absent")
+    spans = set(re.findall(r'_span!\((?:parent: &\w+, )?"([^"]+)"', open(ref).read()))
+    src = open(os.path.join(ROOT, "zkvm-brainfuck_amd/csrc/prover.hip")).read()
+    names = re.findall(r'(?:Span \w+\(|span\.begin\()"([^"]+)"\);(.*)', src)
+    assert len(names) >= 7
+    for name, comment in names:
+        assert name in spans or "no span of its own in the reference" in comment, name
