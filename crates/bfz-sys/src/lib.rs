@@ -266,6 +266,8 @@ extern "C" {
 
     pub fn bfz_set_num_queries(num_queries: c_int) -> c_int;
     pub fn bfz_set_pcs_variant(observe_openings: c_int) -> c_int;
+    /// Test-only fault injection (bit 0: perturb the device challenger); 0 = off.
+    pub fn bfz_set_fault_injection(mask: c_int) -> c_int;
 
     pub fn bfz_proof_to_bincode(proof: *const u8, len: usize, field_repr: c_int, out: *mut *mut u8,
                                 out_len: *mut usize) -> c_int;

@@ -350,6 +350,11 @@ int bfz_set_num_queries(int num_queries);
  * BFZ_OBSERVE_OPENINGS.  Applies to bfz_prove*, bfz_verify*, identically in the oracle. */
 int bfz_set_pcs_variant(int observe_openings);
 
+/* Test-only fault injection, no reference counterpart: bit 0 perturbs the device challenger's
+ * uploaded sponge state, so the host's replay of the device-sampled challenges must fail the
+ * proof with "device transcript diverged" (tests/test_gpu.py).  0 (default) = off. */
+int bfz_set_fault_injection(int mask);
+
 /* Proof wire format.  bfz_prove* return the BFZ1 normal form; bfz_proof_to_bincode turns it
  * into the reference's bytes: bincode::serialize(&MachineProof<KoalaBearPoseidon2>)
  * (crates/core/machine/src/utils/prove.rs:46), i.e. ShardProof (crates/stark/src/types.rs:66-73)

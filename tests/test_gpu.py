@@ -93,37 +93,6 @@ def test_coset_lde_parity(logn, w):
     assert np.array_equal(unmont(out), exp)
 
 
-_MFMA_LDE_CHECK = """
-import sys, ctypes, numpy as np
-sys.path[:0] = [sys.argv[1] + "/zkvm-brainfuck_amd", sys.argv[1] + "/tests"]
-import oracle_lib as O
-from bfz import _lib
-_lib.init(0)
-P = O.P
-for logn, w in ((14, 3), (18, 3), (22, 1)):
-    n = 1 << logn
-    m = np.random.default_rng(logn).integers(0, P, size=(n, w), dtype=np.uint64).astype(np.uint32)
-    src = ((m.astype(np.uint64) << np.uint64(32)) % np.uint64(P)).astype(np.uint32)
-    out = np.zeros((2 * n, w), dtype=np.uint32)
-    P32 = ctypes.POINTER(ctypes.c_uint32)
-    _lib.check(_lib.lib().bfz_coset_lde(src.ctypes.data_as(P32), n, w, (3 << 32) % P,
-                                        out.ctypes.data_as(P32)))
-    got = ((out.astype(np.uint64) * np.uint64(pow(2, -32, P))) % np.uint64(P)).astype(np.uint32)
-    assert np.array_equal(got, O.coset_lde(m, 3)), (logn, w)
-print("ok")
-"""
-
-
-def test_mfma_tiles_lde_parity():
-    """The matrix-core 2^14 tile passes (BFZ_NTT_MFMA=1, the A/B alternative to the VALU tiles,
-    read once per process: hence a child process) against the oracle's coset LDE."""
-    import subprocess
-    import sys
-    r = subprocess.run([sys.executable, "-c", _MFMA_LDE_CHECK, ROOT], capture_output=True,
-                       text=True, timeout=300, env=dict(os.environ, BFZ_NTT_MFMA="1"))
-    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
-
-
 def test_commit_root_parity():
     rng = np.random.default_rng(7)
     shapes = [(1 << 12, 31), (1 << 12, 41), (1 << 11, 7), (1 << 9, 45), (16, 5), (16, 12)]
@@ -584,10 +553,12 @@ def test_device_transcript_divergence_is_an_error(client, monkeypatch):
     must keep working afterwards."""
     prog, stdin = guests.FIBO, [17]
     pk, vk = client.setup(prog)
-    monkeypatch.setenv("BFZ_FAULT_DEVICE_CHALLENGER", "1")
-    with pytest.raises(_lib.BfzError, match="device transcript diverged"):
-        client.prove(pk, stdin).run()
-    monkeypatch.delenv("BFZ_FAULT_DEVICE_CHALLENGER")
+    _lib.check(_lib.lib().bfz_set_fault_injection(1))
+    try:
+        with pytest.raises(_lib.BfzError, match="device transcript diverged"):
+            client.prove(pk, stdin).run()
+    finally:
+        _lib.check(_lib.lib().bfz_set_fault_injection(0))
     pf = client.prove(pk, stdin).run()
     assert pf.proof == O.prove(prog, stdin)
 
@@ -612,7 +583,8 @@ def test_record_from_cycles_matches_oracle(client, name, prog, stdin):
 def test_record_from_cycles_refuses_cycles_no_record_holds(client):
     """Cycles a reference record cannot hold are refused before any trace kernel runs (pc past
     the program, an access on a memory step, a previous timestamp at or after the cycle's own,
-    a prev_value outside an Input, padding), and the library keeps working."""
+    a prev_value outside an Input, padding, a successor the executor would not step to), and the
+    library keeps working."""
     from bfz import events
     prog, stdin = guests.FIBO, [17]
     pk, vk = client.setup(prog)
@@ -629,6 +601,18 @@ def test_record_from_cycles_refuses_cycles_no_record_holds(client):
         bad[idx][field] = val
         with pytest.raises(_lib.BfzError, match="out of range"):
             events.record_from_cycles(pk, bad, rec.memory)
+    # a cycle's successor must be the executor's next step (executor.rs:107-176): pc + 1 after a
+    # non-jump, op_a or pc + 1 after a loop as mv chooses, mp unchanged off a memory step, and
+    # the last cycle must leave the program (a truncated record is refused)
+    jmp = int(np.flatnonzero((op == 0) | (op == 1))[2])
+    for idx, field, val in ((alu + 1, "pc", int(cyc[alu]["pc"])), (jmp, "mv", 1 - min(int(cyc[jmp]["mv"]), 1)),
+                            (alu + 1, "mp", int(cyc[alu]["mp"]) + 1)):
+        bad = cyc.copy()
+        bad[idx][field] = val
+        with pytest.raises(_lib.BfzError, match="out of range"):
+            events.record_from_cycles(pk, bad, rec.memory)
+    with pytest.raises(_lib.BfzError, match="out of range"):
+        events.record_from_cycles(pk, cyc[:-1].copy(), rec.memory)
     raw = cyc.view(np.uint8).reshape(len(cyc), 16).copy()
     raw[3, 15] = 1
     with pytest.raises(_lib.BfzError, match="out of range"):

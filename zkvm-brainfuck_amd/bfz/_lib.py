@@ -124,6 +124,7 @@ SIGNATURES = [
                                        c_size_t, POINTER(c_size_t)]),
     ("bfz_set_num_queries", c_int, [c_int]),
     ("bfz_set_pcs_variant", c_int, [c_int]),
+    ("bfz_set_fault_injection", c_int, [c_int]),
     ("bfz_proof_to_bincode", c_int, [POINTER(c_uint8), c_size_t, c_int, POINTER(POINTER(c_uint8)),
                                      POINTER(c_size_t)]),
     ("bfz_proof_from_bincode", c_int, [POINTER(c_uint8), c_size_t, c_int,

@@ -182,16 +182,6 @@ def cycles_from_record(rec: "ExecutionRecordArrays", pinned: bool = False) -> np
     out["prev_value"] = np.where(write, cpu["mv_access_prev_value"], 0)
     out.view(np.uint8).reshape(-1, 16)[:, 14:16] = 0  # padding
     return out
-    # word views: a CpuEvent is 12 words (pc = 1, mp = 3, mv = low byte of 5; mv_access: kind /
-    # prev_value = bytes 0 / 2 of word 6, prev_timestamp = word 8), a bfz_cycle 4 words
-    src = cpu.view(np.uint32).reshape(n, CPU.itemsize // 4)
-    dst = out.view(np.uint32).reshape(n, 4)
-
-    np.take(src, [1, 3, 8, 5], axis=1, out=dst)  # pc, mp, prev_timestamp, (mv, ...)
-    w6 = src[:, 6]
-    dst[:, 3] &= 0xFF
-    dst[:, 3] |= (((w6 >> 16) & 0xFF) * ((w6 & 0xFF) == 2)) << 8  # a Write's prev_value
-    return out
 
 
 class DeviceRecord:

@@ -50,6 +50,7 @@ std::unordered_map<void*, std::vector<uint8_t>*>& emitted() {
 }
 int g_num_queries = -1;
 int g_observe_openings = -1;  // -1: BFZ_OBSERVE_OPENINGS / default
+int g_fault = 0;              // bfz_set_fault_injection (tests only)
 
 int fail(const std::exception& e, int code = -1) {
   g_err = e.what();
@@ -59,6 +60,7 @@ bfz::ProveOptions opts() {
   bfz::ProveOptions o;
   o.num_queries = g_num_queries > 0 ? g_num_queries : bfz::num_queries_from_env();
   o.observe_openings = g_observe_openings >= 0 ? g_observe_openings != 0 : bfz::observe_openings_from_env();
+  o.fault_device_challenger = (g_fault & 1) != 0;
   return o;
 }
 template <class F>
@@ -68,8 +70,10 @@ int guarded(F&& f) {
   try {
     return f();
   } catch (const bfz::HipError& e) {
+    bfz::quiesce();  // nothing queued may still write a pinned mailbox after the error returns
     return fail(e, -2);
   } catch (const std::exception& e) {
+    bfz::quiesce();
     return fail(e, -1);
   }
 }
@@ -962,6 +966,14 @@ int bfz_set_pcs_variant(int observe_openings) {
     if (observe_openings < -1 || observe_openings > 1)
       throw std::runtime_error("observe_openings must be -1 (environment), 0 or 1");
     g_observe_openings = observe_openings;
+    return 0;
+  });
+}
+
+int bfz_set_fault_injection(int mask) {
+  return guarded([&] {
+    if (mask & ~1) throw std::runtime_error("fault mask: bit 0 (device challenger) only");
+    g_fault = mask;
     return 0;
   });
 }

@@ -66,17 +66,7 @@ __global__ __launch_bounds__(256) void k_inv_denoms(EF z, const EF* __restrict__
 }
 
 // ------------------------------------------------------------------ openings
-#ifndef BFZ_OPEN_R
-#define BFZ_OPEN_R 8
-#endif
-constexpr int OPEN_T = 256, OPEN_R = BFZ_OPEN_R, OPEN_CH = OPEN_T * OPEN_R;
-// BFZ_OPEN_WAVE=1: each wave adds up its own lanes' partials of a 4-column group through its own
-// LDS region (wave-level fence, no workgroup barrier) and writes its own partial: OPEN_PW
-// partials per block, summed by open_final with the others.
-#ifndef BFZ_OPEN_WAVE
-#define BFZ_OPEN_WAVE 0
-#endif
-constexpr int OPEN_PW = BFZ_OPEN_WAVE ? OPEN_T / 64 : 1;  // partials per block
+constexpr int OPEN_T = 256, OPEN_R = 8, OPEN_CH = OPEN_T * OPEN_R;  // (4 or 6 rows: neutral)
 
 __device__ __forceinline__ EF wave_sum(EF v) {
 #pragma unroll
@@ -135,54 +125,6 @@ __device__ __forceinline__ void open_tile(const uint32_t* __restrict__ mat, size
 #pragma unroll
   for (int j = 0; j < 4; j++)
     if (j < w) load(j, vr[j]);
-#if BFZ_OPEN_WAVE
-  constexpr int NSUM = NP * 16;          // (k, j, e) sums of a 4-column group
-  constexpr int RSW = NSUM + 4;          // a lane's row of NSUM words (16-byte aligned)
-  constexpr int LPS = 64 / NSUM, ROWS = 64 / LPS;  // lanes per sum, rows each of them adds
-  __shared__ __align__(16) uint32_t redw[OPEN_T / 64][64 * RSW];
-  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-  uint32_t* rw = redw[wv];
-  auto wave_sync = [] {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  };
-  for (int c = 0; c < w; c += 4) {
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      if (c + j < w) {
-#pragma unroll
-        for (int k = 0; k < NP; k++) {
-          LazyEF lz;
-          lz.init();
-#pragma unroll
-          for (int r = 0; r < OPEN_R; r++) lz.add(W[k][r], vr[j][r]);
-          const EF acc = lz.get();
-          *reinterpret_cast<uint4*>(rw + ln * RSW + (k * 4 + j) * 4) =
-              make_uint4(acc.c[0], acc.c[1], acc.c[2], acc.c[3]);
-        }
-        if (c + j + 4 < w) load(c + j + 4, vr[j]);
-      }
-    }
-    wave_sync();
-    {  // sum q is added up by the LPS lanes q, q + NSUM, ...: rows part * ROWS .. + ROWS - 1
-      const int q = ln % NSUM, part = ln / NSUM;
-      uint64_t a64 = 0;
-#pragma unroll 8
-      for (int i = 0; i < ROWS; i++) a64 += rw[(part * ROWS + i) * RSW + q];  // < 64 p
-      constexpr uint64_t C32 = (1u << 25) - 2;  // 2^32 mod p
-      a64 = (a64 >> 32) * C32 + (uint32_t)a64;
-      a64 = (a64 >> 32) * C32 + (uint32_t)a64;
-      uint32_t v = (uint32_t)(a64 >= 2ull * P ? a64 - 2ull * P : a64 >= P ? a64 - P : a64);
-#pragma unroll
-      for (int off = NSUM; off < 64; off <<= 1) v = madd(v, __shfl_xor(v, off, 64));
-      const int k = q / 16, j = (q / 4) % 4, e = q % 4;
-      if (part == 0 && c + j < w)
-        partial[(((size_t)chunk * OPEN_PW + wv) * w + c + j) * NP + k].c[e] = v;
-    }
-    wave_sync();  // the rows are read before the next group's writes
-  }
-#else
   constexpr int NSUM = NP * 16, PER = OPEN_T / NSUM;  // sums per group, threads per sum
   // row stride OPEN_T + PER: the PER-strided reads of the 32 / PER sums a half-wave adds up
   // land in distinct banks (stride OPEN_T put 32 / PER of them in each bank; kernel -1.6%)
@@ -223,7 +165,6 @@ __device__ __forceinline__ void open_tile(const uint32_t* __restrict__ mat, size
     }
     __syncthreads();
   }
-#endif
 }
 
 template <int NP, bool TAB = false>
@@ -297,15 +238,12 @@ __global__ __launch_bounds__(256) void k_open_final_batch(const OpenDesc* __rest
     sa = ef_mul_base(ef_sub(zn, ef_base(o.z3n)), o.zc);
     sb = ef_mul_base(sa, o.zb);
   }
-  open_final<NP>(partial + o.part_off, (int)o.nchunks * OPEN_PW, o.w, (int)(blockIdx.x - o.col0), sa, sb,
+  open_final<NP>(partial + o.part_off, (int)o.nchunks, o.w, (int)(blockIdx.x - o.col0), sa, sb,
                  o.out_a, o.out_b);
 }
 
 // ------------------------------------------------------------------ reduced openings
-#ifndef BFZ_RED_STEP
-#define BFZ_RED_STEP 16
-#endif
-constexpr int RED_STEP = BFZ_RED_STEP;
+constexpr int RED_STEP = 16;  // column loads per step (8: neutral)
 // Positions [t0, t1) (a shard's range; every pointer indexed by the global position).
 // invd_b == nullptr (has_b): the second point's denominators come from the zeta table at the
 // position of natural index i - 2 (see open_tile); the caller folds w_n^-1 into kb and yb.
@@ -657,19 +595,19 @@ void open_coefficients(const uint32_t* coef, size_t col_stride, int w, size_t co
                        const EF& scale_b, EF* out_b, hipStream_t st) {
   const int nchunks = (int)ceil_div(count, OPEN_CH);
   const int np = tab_b ? 2 : 1;
-  DBuf<EF> partial((size_t)nchunks * OPEN_PW * w * np);
+  DBuf<EF> partial((size_t)nchunks * w * np);
   if (np == 2) {
     hipLaunchKernelGGL((k_open_partial<2, true>), dim3(nchunks), dim3(OPEN_T), 0, st, coef,
                        col_stride, w, count, 0, tab_a, tab_b, nullptr, partial.p);
     KCHECK();
     hipLaunchKernelGGL(k_open_final<2>, dim3(w), dim3(256), 0, st, (const EF*)partial.p,
-                       nchunks * OPEN_PW, w, scale_a, scale_b, out_a, out_b);
+                       nchunks, w, scale_a, scale_b, out_a, out_b);
   } else {
     hipLaunchKernelGGL((k_open_partial<1, true>), dim3(nchunks), dim3(OPEN_T), 0, st, coef,
                        col_stride, w, count, 0, tab_a, tab_a, nullptr, partial.p);
     KCHECK();
     hipLaunchKernelGGL(k_open_final<1>, dim3(w), dim3(256), 0, st, (const EF*)partial.p,
-                       nchunks * OPEN_PW, w, scale_a, scale_a, out_a, out_a);
+                       nchunks, w, scale_a, scale_a, out_a, out_a);
   }
   KCHECK();
 }
@@ -685,7 +623,7 @@ void open_batch(std::vector<OpenDesc>& ds, int np, hipStream_t st) {
     o.part_off = part;
     chunks += o.nchunks;
     cols += (uint32_t)o.w;
-    part += (uint64_t)o.nchunks * OPEN_PW * o.w * np;
+    part += (uint64_t)o.nchunks * o.w * np;
   }
   DBuf<OpenDesc> dd(ds.size());
   upload_async(dd.p, ds.data(), ds.size() * sizeof(OpenDesc), st);
@@ -781,13 +719,12 @@ void reduce_prep(RedCol* cols, const RedColPrep* cp, RedMat* mats, const RedMatP
   KCHECK();
 }
 
-#ifndef BFZ_RED_GRID  // k_reduce's grid-stride cap in workgroups (A/B builds)
-#define BFZ_RED_GRID 32768
-#endif
+// k_reduce's grid-stride cap in workgroups (8k: 0.02-0.04 ms slower, profiles/r02/ab_reduce_grid.txt)
+constexpr unsigned RED_GRID = 32768;
 void reduce_range(const RedCol* cols, const RedMat* mats, int nmats, size_t height, size_t t0,
                   size_t count, const EF* invd_a, const EF* invd_b, const EF* yab,
                   bool has_b, EF* ro, hipStream_t st, int ncols) {
-  const unsigned grid = std::min<unsigned>(ceil_div(count, 256), BFZ_RED_GRID);
+  const unsigned grid = std::min<unsigned>(ceil_div(count, 256), RED_GRID);
   KernelProbe& probe = reduce_probe();
   hipEvent_t ev0 = probe.on ? probe.begin(st) : nullptr;
   hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(256), 0, st, cols, mats, nmats, t0, t0 + count,

@@ -7,7 +7,6 @@
 // evaluation, FRI reduction and openings all stream columns with unit stride.
 #pragma once
 #include <hip/hip_runtime.h>
-#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <cstdint>
 #include <cstdio>
@@ -147,6 +146,14 @@ struct Twiddles {
 Twiddles& twiddles();
 
 hipStream_t stream();
+// Waits for everything queued on stream() if the stream exists (errors ignored): the C ABI's
+// error path runs it so no copy into a process-global pinned buffer is still in flight when
+// a call returns with an error (the next call may reallocate those buffers).
+void quiesce() noexcept;
+// roctx range push / pop, bound lazily with dlopen: without the rocprofiler-sdk runtime they
+// are no-ops, so the prover does not depend on the profiler library.
+void roctx_push(const char* name) noexcept;
+void roctx_pop() noexcept;
 // Every C entry point runs under one process-wide API lock (capi.cpp guarded()); proof code
 // that keeps process-global state (open_impl's pinned mailboxes) checks that it is held.
 // Profiler ranges named after the reference's tracing spans (crates/stark/src/prover.rs:63,281,
@@ -161,11 +168,11 @@ struct Span {
   Span& operator=(const Span&) = delete;
   void begin(const char* name) {
     end();
-    roctxRangePushA(name);
+    roctx_push(name);
     open = true;
   }
   void end() {
-    if (open) roctxRangePop();
+    if (open) roctx_pop();
     open = false;
   }
 };

@@ -9,11 +9,8 @@
 #include "merkle.h"
 #include "poseidon2.h"
 
-// Throughput Poseidon2 kernels: optional occupancy floor for A/B builds
-// (e.g. -DBFZ_P2_KATTR='__attribute__((amdgpu_waves_per_eu(8, 8)))').
-#ifndef BFZ_P2_KATTR
-#define BFZ_P2_KATTR
-#endif
+// (Throughput Poseidon2 kernels at 7 or 8 waves per SIMD ran within noise of the compiler's
+// 5-6: profiles/r03/ab_p2_occupancy.txt.)
 
 namespace bfz {
 
@@ -45,7 +42,7 @@ __device__ __forceinline__ void sponge_cols(uint32_t st[16], const ColList& cl, 
 }
 
 // Rows [r0, r0 + count) (a shard's range; the whole matrix when unsharded).
-__global__ __launch_bounds__(256) BFZ_P2_KATTR void k_hash_leaves(ColList cl, size_t r0, size_t count,
+__global__ __launch_bounds__(256) void k_hash_leaves(ColList cl, size_t r0, size_t count,
                                                      uint32_t* __restrict__ out) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
@@ -108,7 +105,7 @@ __device__ __forceinline__ void store8(uint32_t* p, const uint32_t st[16]) {
 }
 
 // Nodes [j0, j0 + count) of a layer.
-__global__ __launch_bounds__(256) BFZ_P2_KATTR void k_compress(const uint32_t* __restrict__ prev, size_t j0,
+__global__ __launch_bounds__(256) void k_compress(const uint32_t* __restrict__ prev, size_t j0,
                                                   size_t count, uint32_t* __restrict__ out,
                                                   ColList inj) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -153,10 +150,8 @@ constexpr int TOP_NODES = 64;   // fills a 1024-thread block in one lane-mode pa
 constexpr int TOP_LAYERS = 7;   // 64 nodes -> 1
 // Medium layers (TOP_NODES < nodes <= LANE_LAYER_MAX) go to lane mode: a single-lane launch
 // of this size is one permutation latency long (~12 us) while 16 lanes per node finish sooner.
-#ifndef BFZ_LANE_LAYER_LOG
-#define BFZ_LANE_LAYER_LOG 14
-#endif
-constexpr size_t LANE_LAYER_MAX = (size_t)1 << BFZ_LANE_LAYER_LOG;
+// (2^12, 2^13, 2^15, 2^16: slower, profiles/r02/ab_merkle_top.txt, profiles/r04/ab_lane_layer_threshold.txt)
+constexpr size_t LANE_LAYER_MAX = (size_t)1 << 14;
 constexpr int MAXTOP = TOP_LAYERS;
 struct TopLayers {
   uint32_t* out[MAXTOP];
@@ -242,7 +237,7 @@ __global__ __launch_bounds__(256) void k_permute_batch(uint32_t* __restrict__ s,
   for (int k = 0; k < 16; k++) s[16 * i + k] = st[k];
 }
 
-__global__ __launch_bounds__(256) BFZ_P2_KATTR void k_hash_rows8(const uint32_t* __restrict__ rows, size_t r0,
+__global__ __launch_bounds__(256) void k_hash_rows8(const uint32_t* __restrict__ rows, size_t r0,
                                                     size_t count, uint32_t* __restrict__ out) {
   const size_t i = r0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= r0 + count) return;

@@ -367,32 +367,14 @@ __device__ __forceinline__ uint32_t dpp(uint32_t v) {
 constexpr int DPP_QROT1 = 0x39, DPP_QROT2 = 0x4E, DPP_QROT3 = 0x93;  // quad_perm x_{j+1,2,3}
 constexpr int DPP_ROR1 = 0x121, DPP_ROR2 = 0x122, DPP_ROR4 = 0x124, DPP_ROR8 = 0x128;
 
-__device__ __forceinline__ uint32_t mds_light_lane(uint32_t x) {
-  const uint32_t a1 = dpp<DPP_QROT1>(x), a2 = dpp<DPP_QROT2>(x), a3 = dpp<DPP_QROT3>(x);
-  const uint32_t s4 = madd(madd(x, a1), madd(a2, a3));
-  const uint32_t y = madd(madd(s4, x), mdbl(a1));  // 2x_j + 3x_{j+1} + x_{j+2} + x_{j+3}
-  const uint32_t t = madd(y, dpp<DPP_ROR8>(y));
-  return madd(y, madd(t, dpp<DPP_ROR4>(t)));      // + sum of the 4 blocks at this position
-}
-
-__device__ __forceinline__ uint32_t sum_lanes16(uint32_t v) {
-  v = madd(v, dpp<DPP_ROR1>(v));
-  v = madd(v, dpp<DPP_ROR2>(v));
-  v = madd(v, dpp<DPP_ROR4>(v));
-  return madd(v, dpp<DPP_ROR8>(v));
-}
-
-// Signed lazy form in lane mode (BFZ_P2_LANE_SIGNED, default): the throughput permutation's
+// Signed lazy form in lane mode: the throughput permutation's
 // arithmetic (poseidon2_permute above: R^2-form 64-bit S-box outputs folded to < 2^55.1,
 // MDS-light in 64-bit adds, one signed reduction per element and round, round constants in front
 // of the MDS layer) with lane l holding element l and the cross-lane terms moved by DPP (both
 // halves of a 64-bit value): 619 VALU instructions per lane against 836 for the canonical form
 // below (three-instruction modular adds, five-instruction products).  Lane mode is latency-bound
 // (tree tops, the FRI tail, the device challenger): k_compress_top 18.0 -> 15.3 us and k_fri_tail
-// 107 -> 91 us per launch (profiles/r04/ab_lane_signed.txt); BFZ_P2_LANE_SIGNED=0 builds the old.
-#ifndef BFZ_P2_LANE_SIGNED
-#define BFZ_P2_LANE_SIGNED 1
-#endif
+// 107 -> 91 us per launch (profiles/r04/ab_lane_signed.txt).
 // (mov_dpp: every lane of the row is a valid source for these controls, so no "old" value is
 // needed -- update_dpp(0, ...) would cost a v_mov of zero into every destination first)
 template <int CTRL>
@@ -421,17 +403,11 @@ __device__ __forceinline__ int64_t sum_lanes16_64(int64_t v) {
 // The lane's round constants, loaded once per kernel by callers that permute in a loop (the
 // loads are a memory round trip on a latency-bound chain).
 struct LaneConsts {
-#if BFZ_P2_LANE_SIGNED
   int32_t kin[4], kte[3];  // P2PRE.init[r][lane], P2PRE.term[r][lane]
   int32_t init0, d, rct;   // P2PRE.init0[lane], P2M.d[lane], P2S.rc_term[0][lane]
-#else
-  uint32_t rce[8];
-  uint32_t dg;
-#endif
 };
 __device__ __forceinline__ LaneConsts lane_consts(int lane) {
   LaneConsts k;
-#if BFZ_P2_LANE_SIGNED
 #pragma unroll
   for (int r = 0; r < 4; r++) k.kin[r] = P2PRE.init[r][lane];
 #pragma unroll
@@ -439,18 +415,9 @@ __device__ __forceinline__ LaneConsts lane_consts(int lane) {
   k.init0 = P2PRE.init0[lane];
   k.d = P2M.d[lane];
   k.rct = P2S.rc_term[0][lane];
-#else
-#pragma unroll
-  for (int r = 0; r < 4; r++) {
-    k.rce[r] = P2.ext_init[r][lane];
-    k.rce[4 + r] = P2.ext_term[r][lane];
-  }
-  k.dg = P2.diag[lane];
-#endif
   return k;
 }
 
-#if BFZ_P2_LANE_SIGNED
 // One external round per r (as external_rounds_pre): x -> x^3 R^2 + K[r] -> fold -> MDS-light.
 __device__ __forceinline__ int64_t external_rounds_lane(int32_t x, const int32_t* K, int nk) {
   int64_t y = 0;
@@ -482,25 +449,6 @@ __device__ __forceinline__ uint32_t poseidon2_permute_lane(uint32_t v, int lane,
   const uint32_t r = (uint32_t)mred_s(y);
   return umin(r, r + P);
 }
-#else
-__device__ __forceinline__ uint32_t poseidon2_permute_lane(uint32_t v, int lane,
-                                                           const LaneConsts& kc) {
-  const uint32_t* rce = kc.rce;
-  const uint32_t dg = kc.dg;
-  v = mds_light_lane(v);
-#pragma unroll
-  for (int r = 0; r < 4; r++) v = mds_light_lane(cube(madd(v, rce[r])));
-#pragma unroll
-  for (int r = 0; r < 13; r++) {
-    const uint32_t c = cube(madd(v, P2.internal[r]));
-    v = lane == 0 ? c : v;
-    v = madd(sum_lanes16(v), mmul(v, dg));
-  }
-#pragma unroll
-  for (int r = 0; r < 4; r++) v = mds_light_lane(cube(madd(v, rce[4 + r])));
-  return v;
-}
-#endif
 __device__ __forceinline__ uint32_t poseidon2_permute_lane(uint32_t v, int lane) {
   return poseidon2_permute_lane(v, lane, lane_consts(lane));
 }

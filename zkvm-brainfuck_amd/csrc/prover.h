@@ -104,6 +104,9 @@ struct ProveOptions {
   // Decision D1 ([p3-recalled]): TwoAdicFriPcs::open observes every opened
   // value before sampling the FRI batching challenge alpha (true), or samples alpha first (false)
   bool observe_openings = true;
+  // Test-only fault injection (bfz_set_fault_injection): perturb the device challenger's
+  // uploaded sponge so the host replay must report the divergence.
+  bool fault_device_challenger = false;
 };
 
 // Full core proof of (program, stdin) in the BFZ1 normal form.

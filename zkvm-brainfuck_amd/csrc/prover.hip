@@ -626,7 +626,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     dc.nout = ch.nout;
     // fault injection for tests/test_gpu.py: a device sponge that is not the host's must end in
     // an error at proving time, not in a proof the verifier rejects
-    if (const char* f = std::getenv("BFZ_FAULT_DEVICE_CHALLENGER"); f && *f == '1')
+    if (opt.fault_device_challenger)
       dc.st[15] = dc.st[15] ? dc.st[15] - 1 : 1;  // a capacity word (the rate is overwritten)
     upload_async(dc_d.p, &dc, sizeof(dc), st);
   }

@@ -1,4 +1,6 @@
 // Process-wide device state: allocator pool, stream, twiddle tables.
+#include <dlfcn.h>
+
 #include "gpu.h"
 
 #include <algorithm>
@@ -15,13 +17,46 @@ DevicePool& pool() {
   return *p;
 }
 
+namespace {
+hipStream_t g_stream = nullptr;
+}
 hipStream_t stream() {
   static hipStream_t s = [] {
     hipStream_t st;
     HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    g_stream = st;
     return st;
   }();
   return s;
+}
+
+void quiesce() noexcept {
+  if (g_stream) (void)hipStreamSynchronize(g_stream);
+}
+
+namespace {
+struct Roctx {
+  int (*push)(const char*) = nullptr;
+  int (*pop)() = nullptr;
+  Roctx() {
+    void* h = dlopen("librocprofiler-sdk-roctx.so", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librocprofiler-sdk-roctx.so", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return;
+    push = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxRangePushA"));
+    pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+    if (!push || !pop) push = nullptr, pop = nullptr;
+  }
+};
+const Roctx& roctx() {
+  static const Roctx r;
+  return r;
+}
+}  // namespace
+void roctx_push(const char* name) noexcept {
+  if (roctx().push) roctx().push(name);
+}
+void roctx_pop() noexcept {
+  if (roctx().pop) roctx().pop();
 }
 
 KernelProbe& ntt_probe() {
@@ -145,10 +180,7 @@ class CopyPool {
 void upload_bulk(void* dst, const void* src, size_t bytes, hipStream_t st) {
   if (!bytes) return;
   constexpr size_t CHUNK = (size_t)32 << 20;
-#ifndef BFZ_UPLOAD_THREADS
-#define BFZ_UPLOAD_THREADS 8
-#endif
-  constexpr int NTHR = BFZ_UPLOAD_THREADS;
+  constexpr int NTHR = 8;
   struct Bulk {
     uint8_t* buf[2] = {nullptr, nullptr};
     hipEvent_t done[2];

@@ -415,7 +415,8 @@ __device__ __forceinline__ int cat_of(int op) {
 }
 // A cycle the reference executor could have emitted (executor.rs:108-239): memory steps have
 // no access (mv = 0), only Input writes (prev_value), and an access's previous timestamp lies
-// before the cycle's first access at clk + 1.
+// before the cycle's first access at clk + 1.  k_cycles_count adds the step rules between a
+// cycle and its successor.
 __device__ __forceinline__ bool cycle_ok(const Cycle& c, uint32_t clk, int cat, int op) {
   if (c.pad[0] | c.pad[1]) return false;
   if (cat == CAT_MEM) return c.mv == 0 && c.prev_ts == 0 && c.prev_value == 0;
@@ -440,9 +441,22 @@ __global__ __launch_bounds__(XB) void k_cycles_count(const Cycle* __restrict__ c
     if (c.pc >= nprog) {
       bad = true;
     } else {
-      const int op = prog[c.pc].opcode;
+      const Instruction ins = prog[c.pc];
+      const int op = ins.opcode;
       cat = cat_of(op);
       bad = !cycle_ok(c, (uint32_t)(2 * i), cat, op);
+      // the successor the executor steps to (executor.rs:107-141,157-176): pc + 1, or a loop's
+      // op_a chosen by mv; mp moves only on a memory step; the last cycle leaves the program
+      uint32_t npc = c.pc + 1;
+      if (op == OP_LOOP_START && c.mv == 0) npc = ins.op_a;
+      if (op == OP_LOOP_END && c.mv != 0) npc = ins.op_a;
+      const uint32_t nmp = op == OP_MEM_FWD ? c.mp + 1 : op == OP_MEM_BWD ? c.mp - 1 : c.mp;
+      if (i + 1 < n) {
+        const Cycle nx = cyc[i + 1];
+        bad = bad || nx.pc != npc || nx.mp != nmp;
+      } else {
+        bad = bad || npc != nprog;
+      }
     }
   }
   const int wv = threadIdx.x >> 6;
