@@ -17,6 +17,10 @@ pub struct bfz_record {
 pub struct bfz_main_data {
     _opaque: [u8; 0],
 }
+#[repr(C)]
+pub struct bfz_cycle_upload {
+    _opaque: [u8; 0],
+}
 
 /// p3 `DuplexChallenger<KoalaBear, Poseidon2KoalaBear<16>, 16, 8>` as plain data.
 #[repr(C)]
@@ -249,6 +253,12 @@ extern "C" {
     pub fn bfz_record_from_cycles(pk: *const bfz_pk, cycles: *const bfz_cycle, n_cycles: usize,
                                   memory: *const bfz_memory_event, n_memory: usize,
                                   rec: *mut *mut bfz_record) -> c_int;
+    pub fn bfz_cycles_begin(pk: *const bfz_pk, n_cycles: usize, up: *mut *mut bfz_cycle_upload) -> c_int;
+    pub fn bfz_cycles_push(up: *mut bfz_cycle_upload, first: usize, cycles: *const bfz_cycle,
+                           n: usize) -> c_int;
+    pub fn bfz_cycles_finish(up: *mut bfz_cycle_upload, memory: *const bfz_memory_event,
+                             n_memory: usize, rec: *mut *mut bfz_record) -> c_int;
+    pub fn bfz_cycles_abort(up: *mut bfz_cycle_upload);
     pub fn bfz_host_alloc(bytes: usize, out: *mut *mut c_void) -> c_int;
     pub fn bfz_host_free(p: *mut c_void);
     pub fn bfz_record_prove_sharded(pk: *const bfz_pk, rec: *const bfz_record, rank: c_int,

@@ -278,7 +278,8 @@ int bfz_record_from_events(const bfz_pk* pk, const bfz_events* events, bfz_recor
  * (emit_events, executor.rs:196-239) -- so the device rebuilds them (tracegen.hip
  * expand_cycles) instead of receiving ~64 B per cycle.  Cycles that no reference record holds
  * (pc outside the program, an access on a memory step, prev_timestamp >= clk + 1, prev_value
- * outside an Input, nonzero padding) are refused before any trace kernel runs. */
+ * outside an Input, nonzero padding, a successor pc / mp the executor would not step to, a last
+ * cycle that does not leave the program) are refused before any trace kernel runs. */
 typedef struct {
   uint32_t pc;         /* CpuEvent::pc */
   uint32_t mp;         /* CpuEvent::mp */
@@ -290,11 +291,29 @@ typedef struct {
 int bfz_record_from_cycles(const bfz_pk* pk, const bfz_cycle* cycles, size_t n_cycles,
                            const bfz_memory_event* memory, size_t n_memory, bfz_record** rec);
 
+/* The same hand-over in chunks, so the host conversion of record.cpu_events overlaps the DMA:
+ * bfz_cycles_begin announces n_cycles; each bfz_cycles_push queues one converted chunk
+ * (cycles[first, first + n)) on a copy stream and returns at once -- from page-locked
+ * (bfz_host_alloc) memory the copy is a DMA that runs while the caller converts the next chunk,
+ * and the chunk must then stay unchanged until bfz_cycles_finish returns; chunks may come from
+ * several threads, in any order.  bfz_cycles_finish checks that every cycle was pushed exactly
+ * once, then validates and expands them exactly as bfz_record_from_cycles (same record, same
+ * proof) and consumes the handle, also on error; bfz_cycles_abort drops an unfinished one.
+ * Replaces the single-array call of HipProver::prove (crates/bf-hip-prover) with a pipelined
+ * CycleArrays::new; the reference hands the record over in memory (utils/prove.rs:44-46). */
+typedef struct bfz_cycle_upload bfz_cycle_upload;
+int bfz_cycles_begin(const bfz_pk* pk, size_t n_cycles, bfz_cycle_upload** up);
+int bfz_cycles_push(bfz_cycle_upload* up, size_t first, const bfz_cycle* cycles, size_t n);
+int bfz_cycles_finish(bfz_cycle_upload* up, const bfz_memory_event* memory, size_t n_memory,
+                      bfz_record** rec);
+void bfz_cycles_abort(bfz_cycle_upload* up);
+
 /* Page-locked host memory for the hand-over arrays (the Rust CycleArrays builds its bfz_cycle
  * vector in it): bfz_record_from_cycles / bfz_record_from_events then DMA straight from the
  * caller's array instead of staging it through the library's pinned chunks (PCIe-bound: ~60 GB/s
  * against ~35-40 GB/s staged).  Any host memory is still accepted; this only makes the upload
- * faster.  Pairs with bfz_host_free (not bfz_free).  Host-side replacement of the reference's
+ * faster.  Pairs with bfz_host_free (not bfz_free); freed blocks are kept page-locked for reuse
+ * (up to 8 GiB), so a per-proof allocation of the same size does not pin memory again.  Host-side replacement of the reference's
  * Vec allocation in ExecutionRecord hand-off (crates/core/machine/src/utils/prove.rs:44-46). */
 int bfz_host_alloc(size_t bytes, void** out);
 void bfz_host_free(void* p);

@@ -432,3 +432,21 @@ def test_batch_handover_failure_releases_emitted_proofs():
     from bfz import _lib
     assert _lib.lib().bfz_selftest(b"emit_rollback") == 0, _lib.lib().bfz_last_error()
     assert _lib.lib().bfz_selftest(b"no_such_test") != 0
+
+
+@pytest.mark.parametrize("name,prog,stdin", guests.REFERENCE_PROGRAMS[:4] + [("fibo17", guests.FIBO, [17])])
+def test_cycle_arrays_standin_matches_python_conversion(name, prog, stdin):
+    """The compiled stand-in of the Rust CycleArrays::new (crates/bf-hip-prover/standin, over
+    cpu_events laid out as rustc lays out CpuEvent) writes the same 16-byte cycles as the numpy
+    mirror cycles_from_record, on 1, 3 and 8 threads (no device needed)."""
+    import numpy as np
+    from bfz import events
+    rec = events.ExecutionRecordArrays.from_executor(prog, stdin)
+    want = events.cycles_from_record(rec)
+    rs = events.rust_cpu_events(rec)
+    sa = events.CycleArraysStandin()
+    for threads in (1, 3, 8):
+        got = np.zeros(len(want), dtype=events.CYCLE)
+        got.view(np.uint8)[:] = 0xAB  # every byte must be written
+        sa.convert(rs, got, threads)
+        assert got.tobytes() == want.tobytes(), (name, threads)

@@ -461,6 +461,10 @@ def _record_proof(pk, rec, cycles=False, pinned=False):
     from bfz import events
     drec = (events.record_from_cycles(pk, events.cycles_from_record(rec, pinned=pinned), rec.memory)
             if cycles else events.record_from_events(pk, rec))
+    return _prove_record(pk, drec)
+
+
+def _prove_record(pk, drec):
     ptr = ctypes.POINTER(ctypes.c_uint8)()
     n = ctypes.c_size_t()
     _lib.check(_lib.lib().bfz_record_prove(ctypes.c_void_p(pk.handle), ctypes.c_void_p(drec.handle),
@@ -578,6 +582,55 @@ def test_record_from_cycles_matches_oracle(client, name, prog, stdin):
     if len(rec.memory) > 1:
         rec.memory = np.ascontiguousarray(rec.memory[::-1])
         assert _record_proof(pk, rec, cycles=True) == want, name
+
+
+@pytest.mark.parametrize("name,prog,stdin", guests.REFERENCE_PROGRAMS[:5] + [("fibo255", guests.FIBO, [255])])
+def test_chunked_cycle_handover_matches_oracle(client, name, prog, stdin):
+    """bfz_cycles_begin / push / finish: the cycles pushed in chunks (any
+    order; chunk sizes 1 cycle, 7 cycles, a third of the run) give the oracle's proof, and so does
+    the compiled stand-in of CycleArrays::new pushing chunks from its worker threads."""
+    from bfz import events
+    pk, vk = client.setup(prog)
+    rec = events.ExecutionRecordArrays.from_executor(prog, stdin)
+    cyc = events.cycles_from_record(rec, pinned=True)
+    want = O.prove(prog, stdin)
+    chunks = [7, max(1, len(cyc) // 3)] + ([1] if len(cyc) < 5000 else [])
+    for ch in chunks:
+        drec = events.record_from_cycle_chunks(pk, cyc, rec.memory, ch)
+        assert _prove_record(pk, drec) == want, (name, ch)
+    sa = events.CycleArraysStandin()
+    out = events.pinned_empty(len(cyc), events.CYCLE)
+    drec, _ = sa.handover(pk, events.rust_cpu_events(rec), rec.memory, out, 4, 1000)
+    assert _prove_record(pk, drec) == want, name
+
+
+def test_chunked_cycle_handover_refuses_gaps_and_overlaps(client):
+    """A chunk outside the announced count, a missing cycle or one pushed twice is an error
+    (the handle is consumed), and the library keeps working."""
+    from bfz import events
+    prog, stdin = guests.FIBO, [17]
+    pk, vk = client.setup(prog)
+    rec = events.ExecutionRecordArrays.from_executor(prog, stdin)
+    cyc = events.cycles_from_record(rec)
+    L = _lib.lib()
+    n = len(cyc)
+    base = cyc.ctypes.data
+    for pushes, match in (([(0, n - 1)], "missing"), ([(0, n), (5, 3)], "twice"),
+                          ([(0, 10), (20, n - 20)], "missing")):
+        up = ctypes.c_void_p()
+        _lib.check(L.bfz_cycles_begin(ctypes.c_void_p(pk.handle), n, ctypes.byref(up)))
+        for a, k in pushes:
+            _lib.check(L.bfz_cycles_push(up, a, base + 16 * a, k))
+        out = ctypes.c_void_p()
+        with pytest.raises(_lib.BfzError, match=match):
+            _lib.check(L.bfz_cycles_finish(up, rec.memory.ctypes.data, len(rec.memory), ctypes.byref(out)))
+    up = ctypes.c_void_p()
+    _lib.check(L.bfz_cycles_begin(ctypes.c_void_p(pk.handle), n, ctypes.byref(up)))
+    with pytest.raises(_lib.BfzError, match="outside"):
+        _lib.check(L.bfz_cycles_push(up, n - 2, base, 3))
+    L.bfz_cycles_abort(up)
+    drec = events.record_from_cycle_chunks(pk, cyc, rec.memory, 100)
+    assert _prove_record(pk, drec) == O.prove(prog, stdin)
 
 
 def test_record_from_cycles_refuses_cycles_no_record_holds(client):

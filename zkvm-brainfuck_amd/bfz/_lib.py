@@ -115,6 +115,10 @@ SIGNATURES = [
     ("bfz_record_from_events", c_int, [c_void_p, POINTER(Events), POINTER(c_void_p)]),
     ("bfz_record_from_cycles", c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_size_t,
                                        POINTER(c_void_p)]),
+    ("bfz_cycles_begin", c_int, [c_void_p, c_size_t, POINTER(c_void_p)]),
+    ("bfz_cycles_push", c_int, [c_void_p, c_size_t, c_void_p, c_size_t]),
+    ("bfz_cycles_finish", c_int, [c_void_p, c_void_p, c_size_t, POINTER(c_void_p)]),
+    ("bfz_cycles_abort", None, [c_void_p]),
     ("bfz_record_prove_sharded", c_int, [c_void_p, c_void_p, c_int, c_int, ALLGATHER_FN,
                                          ALLREDUCE_FN, c_void_p, POINTER(POINTER(c_uint8)),
                                          POINTER(c_size_t), POINTER(Timings)]),

@@ -219,3 +219,91 @@ def record_from_cycles(pk, cycles: np.ndarray, memory: np.ndarray) -> DeviceReco
                                        memory.ctypes.data if len(memory) else None, len(memory),
                                        ctypes.byref(out)))
     return DeviceRecord(out.value)
+
+
+def record_from_cycle_chunks(pk, cycles: np.ndarray, memory: np.ndarray, chunk: int) -> DeviceRecord:
+    """The chunked hand-over (bfz_cycles_begin / push / finish) of the same cycles, `chunk`
+    cycles per push: the record (and proof) must equal bfz_record_from_cycles'."""
+    _lib.init()
+    assert cycles.dtype == CYCLE and cycles.flags["C_CONTIGUOUS"]
+    assert memory.dtype == MEMORY and memory.flags["C_CONTIGUOUS"]
+    L = lib()
+    up = ctypes.c_void_p()
+    check(L.bfz_cycles_begin(ctypes.c_void_p(pk.handle), len(cycles), ctypes.byref(up)))
+    try:
+        # pushed last chunk first: the library accepts any order
+        starts = list(range(0, len(cycles), chunk))[::-1]
+        for a in starts:
+            n = min(chunk, len(cycles) - a)
+            check(L.bfz_cycles_push(up, a, cycles.ctypes.data + a * CYCLE.itemsize, n))
+    except BaseException:
+        L.bfz_cycles_abort(up)
+        raise
+    out = ctypes.c_void_p()
+    check(L.bfz_cycles_finish(up, memory.ctypes.data if len(memory) else None, len(memory),
+                              ctypes.byref(out)))
+    return DeviceRecord(out.value)
+
+
+# Vec<CpuEvent> as rustc lays it out (repr(Rust): the u32 fields, the two 12-byte
+# Option<MemoryRecordEnum> -- tag 0 Read, 1 Write, 2 None in the niche -- then mv, next_mv):
+# the input of the compiled stand-in of CycleArrays::new (crates/bf-hip-prover/standin).
+_RS_ACCESS = [("tag", "u1", 0), ("value", "u1", 1), ("prev_value", "u1", 2),
+              ("timestamp", "<u4", 4), ("prev_timestamp", "<u4", 8)]
+RUST_CPU = _dt([("clk", "<u4", 0), ("pc", "<u4", 4), ("next_pc", "<u4", 8), ("mp", "<u4", 12),
+                ("next_mp", "<u4", 16)]
+               + [("mv_access_" + n, f, 20 + o) for n, f, o in _RS_ACCESS]
+               + [("next_mv_access_" + n, f, 32 + o) for n, f, o in _RS_ACCESS]
+               + [("mv", "u1", 44), ("next_mv", "u1", 45)], 48)
+
+
+def rust_cpu_events(rec: "ExecutionRecordArrays") -> np.ndarray:
+    """record.cpu_events in the Rust layout above (what HipProver::prove iterates)."""
+    cpu = rec.cpu
+    out = np.zeros(len(cpu), dtype=RUST_CPU)
+    for k in ("clk", "pc", "next_pc", "mp", "next_mp", "mv", "next_mv"):
+        out[k] = cpu[k]
+    tag = np.array([2, 0, 1], dtype=np.uint8)  # bfz kind None/Read/Write -> Rust tag
+    for a in ("mv_access_", "next_mv_access_"):
+        out[a + "tag"] = tag[cpu[a + "kind"]]
+        for k in ("value", "prev_value", "timestamp", "prev_timestamp"):
+            out[a + k] = cpu[a + k]
+    return out
+
+
+class CycleArraysStandin:
+    """ctypes view of crates/bf-hip-prover/standin/libcycle_arrays.so: the compiled stand-in of
+    the Rust CycleArrays::new (one parallel pass over cpu_events into page-locked memory) and its
+    pipelined form over bfz_cycles_* (conversion of chunk k+1 overlaps the DMA of chunk k)."""
+
+    def __init__(self):
+        import os
+        lib()  # libbfz first (the stand-in links it by its directory); no device needed to convert
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        path = os.path.join(root, "crates", "bf-hip-prover", "standin", "libcycle_arrays.so")
+        self.so = ctypes.CDLL(path)
+        self.so.ca_convert.restype = ctypes.c_int
+        self.so.ca_convert.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int]
+        self.so.ca_handover.restype = ctypes.c_int
+        self.so.ca_handover.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                        ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                        ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p),
+                                        ctypes.POINTER(ctypes.c_double)]
+
+    def convert(self, rust_cpu: np.ndarray, out: np.ndarray, threads: int) -> None:
+        assert rust_cpu.dtype == RUST_CPU and out.dtype == CYCLE and len(out) == len(rust_cpu)
+        if self.so.ca_convert(rust_cpu.ctypes.data, len(rust_cpu), out.ctypes.data, threads):
+            raise RuntimeError("ca_convert failed")
+
+    def handover(self, pk, rust_cpu: np.ndarray, memory: np.ndarray, out: np.ndarray,
+                 threads: int, chunk: int):
+        """(DeviceRecord, ms until the last chunk was pushed)."""
+        assert rust_cpu.dtype == RUST_CPU and out.dtype == CYCLE and len(out) == len(rust_cpu)
+        assert memory.dtype == MEMORY
+        rec = ctypes.c_void_p()
+        conv = ctypes.c_double()
+        check(self.so.ca_handover(ctypes.c_void_p(pk.handle), rust_cpu.ctypes.data, len(rust_cpu),
+                                  memory.ctypes.data if len(memory) else None, len(memory),
+                                  out.ctypes.data, threads, chunk, ctypes.byref(rec),
+                                  ctypes.byref(conv)))
+        return DeviceRecord(rec.value), conv.value

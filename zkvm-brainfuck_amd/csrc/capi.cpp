@@ -35,6 +35,16 @@ struct bfz_record {
   bfz::DeviceEvents ev;  // executor events resident in HBM
   uint64_t cycles = 0;
 };
+struct bfz_cycle_upload {  // a chunked hand-over in progress (bfz_cycles_begin .. finish)
+  const bfz_pk* pk = nullptr;
+  size_t n = 0;
+  bfz::DBuf<bfz::Cycle> d;
+  std::vector<std::pair<size_t, size_t>> ranges;  // pushed (first, count)
+  hipEvent_t copied = nullptr;
+  ~bfz_cycle_upload() {
+    if (copied) (void)hipEventDestroy(copied);
+  }
+};
 
 namespace {
 std::mutex g_mu;
@@ -731,6 +741,90 @@ static_assert(sizeof(bfz_cycle) == sizeof(bfz::Cycle) && offsetof(bfz_cycle, pre
                   offsetof(bfz_cycle, mv) == offsetof(bfz::Cycle, mv) &&
                   offsetof(bfz_cycle, prev_value) == offsetof(bfz::Cycle, prev_value),
               "bfz.h bfz_cycle must match machine.h Cycle");
+
+void check_cycle_counts(size_t n_cycles, size_t n_memory) {
+  if (n_cycles == 0) throw std::runtime_error("record_from_cycles: no cycles");
+  const size_t lim = (size_t)1 << 26;  // beyond any committable trace (2^23 rows)
+  if (n_cycles > lim || n_memory > 2 * lim)
+    throw std::runtime_error("record_from_cycles: event count out of range");
+}
+
+// bfz_host_alloc / bfz_host_free: page-locked blocks are kept for reuse (rounded up to 2 MiB,
+// up to 8 GiB held), because a caller such as HipProver allocates its hand-over array per proof
+// and pinning tens of MB costs milliseconds each time.
+class PinnedCache {
+ public:
+  void* take(size_t bytes) {
+    bytes = (bytes + GRAIN - 1) / GRAIN * GRAIN;
+    auto it = free_.find(bytes);
+    if (it != free_.end() && !it->second.empty()) {
+      void* p = it->second.back();
+      it->second.pop_back();
+      held_ -= bytes;
+      return p;
+    }
+    void* p = bfz::pinned_alloc(bytes);
+    if (p) size_of_[p] = bytes;
+    return p;
+  }
+  void give(void* p) {
+    if (!p) return;
+    auto it = size_of_.find(p);
+    if (it == size_of_.end()) return;  // not ours
+    if (held_ + it->second > CAP) {
+      bfz::pinned_free(p);
+      size_of_.erase(it);
+      return;
+    }
+    free_[it->second].push_back(p);
+    held_ += it->second;
+  }
+
+ private:
+  static constexpr size_t GRAIN = (size_t)2 << 20, CAP = (size_t)8 << 30;
+  std::unordered_map<size_t, std::vector<void*>> free_;
+  std::unordered_map<void*, size_t> size_of_;
+  size_t held_ = 0;
+};
+PinnedCache& pinned_cache() {
+  static auto* c = new PinnedCache();  // blocks stay pinned until the process exits
+  return *c;
+}
+
+// Copies of the chunked hand-over (bfz_cycles_push) run here, beside the prover stream.
+hipStream_t handover_stream() {
+  static hipStream_t s = [] {
+    hipStream_t st;
+    HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    return st;
+  }();
+  return s;
+}
+
+// The record from cycles already in HBM (ordered on the prover stream): program and memory
+// events uploaded, every cycle validated and expanded into the chip events (tracegen.hip).
+std::unique_ptr<bfz_record> record_from_device_cycles(const bfz_pk* pk, const bfz::DBuf<bfz::Cycle>& d,
+                                                      size_t n_cycles, const bfz_memory_event* memory,
+                                                      size_t n_memory) {
+  hipStream_t st = bfz::stream();
+  auto r = std::make_unique<bfz_record>();
+  bfz::DeviceEvents& ev = r->ev;
+  const bfz::Program& prog = put_program(ev, pk->pk->program, st);
+  ev.n[bfz::CHIP_PROGRAM] = prog.instructions.size();
+  const size_t nmem = put_memory_events(ev, memory, n_memory, st);
+  bfz::EventCounts n;
+  size_t bad = 0;
+  bfz::expand_cycles(d.p, n_cycles, ev, n, &bad, st);
+  if (bad)
+    throw std::runtime_error("record_from_cycles: " + std::to_string(bad) +
+                             " cycles out of range (pc outside the program, fields a reference "
+                             "record cannot hold, or a successor the executor would not step to)");
+  n.memory = nmem;
+  n.program = prog.instructions.size();
+  bfz::set_event_meta(ev, n, n_cycles);
+  r->cycles = n_cycles;
+  return r;
+}
 }  // namespace
 extern "C" {
 
@@ -781,7 +875,7 @@ int bfz_host_alloc(size_t bytes, void** out) {
     if (!out) throw std::runtime_error("host_alloc: null argument");
     *out = nullptr;
     if (bytes == 0 || bytes > ((size_t)1 << 38)) throw std::runtime_error("host_alloc: size out of range");
-    void* p = bfz::pinned_alloc(bytes);
+    void* p = pinned_cache().take(bytes);
     if (!p) throw std::runtime_error("host_alloc: hipHostMalloc failed");
     *out = p;
     return 0;
@@ -790,40 +884,84 @@ int bfz_host_alloc(size_t bytes, void** out) {
 
 void bfz_host_free(void* p) {
   std::lock_guard<std::mutex> lk(g_mu);
-  bfz::pinned_free(p);
+  pinned_cache().give(p);
 }
 
 int bfz_record_from_cycles(const bfz_pk* pk, const bfz_cycle* cycles, size_t n_cycles,
                            const bfz_memory_event* memory, size_t n_memory, bfz_record** rec) {
   return guarded([&] {
     if (!pk || !rec) throw std::runtime_error("null argument");
-    if (n_cycles == 0) throw std::runtime_error("record_from_cycles: no cycles");
+    check_cycle_counts(n_cycles, n_memory);
     if (!cycles) throw std::runtime_error("record_from_cycles: null cycle array");
-    const size_t lim = (size_t)1 << 26;  // beyond any committable trace (2^23 rows)
-    if (n_cycles > lim || n_memory > 2 * lim)
-      throw std::runtime_error("record_from_cycles: event count out of range");
     hipStream_t st = bfz::stream();
-    auto r = std::make_unique<bfz_record>();
-    bfz::DeviceEvents& ev = r->ev;
-    const bfz::Program& prog = put_program(ev, pk->pk->program, st);
-    ev.n[bfz::CHIP_PROGRAM] = prog.instructions.size();
     bfz::DBuf<bfz::Cycle> d(n_cycles);
     bfz::upload_bulk(d.p, cycles, n_cycles * sizeof(bfz::Cycle), st);
-    const size_t nmem = put_memory_events(ev, memory, n_memory, st);
-    bfz::EventCounts n;
-    size_t bad = 0;
-    bfz::expand_cycles(d.p, n_cycles, ev, n, &bad, st);
-    if (bad)
-      throw std::runtime_error("record_from_cycles: " + std::to_string(bad) +
-                               " cycles out of range (pc outside the program, or fields a "
-                               "reference record cannot hold)");
-    n.memory = nmem;
-    n.program = prog.instructions.size();
-    bfz::set_event_meta(ev, n, n_cycles);
-    r->cycles = n_cycles;
-    *rec = r.release();
+    *rec = record_from_device_cycles(pk, d, n_cycles, memory, n_memory).release();
     return 0;
   });
+}
+
+int bfz_cycles_begin(const bfz_pk* pk, size_t n_cycles, bfz_cycle_upload** up) {
+  return guarded([&] {
+    if (!pk || !up) throw std::runtime_error("null argument");
+    check_cycle_counts(n_cycles, 0);
+    auto u = std::make_unique<bfz_cycle_upload>();
+    u->pk = pk;
+    u->n = n_cycles;
+    u->d.reset(n_cycles);
+    // the pooled buffer may still be read by work queued on the prover stream (the pool is
+    // ordered on that stream only): the copy stream starts after everything queued there
+    HIP_CHECK(hipEventCreateWithFlags(&u->copied, hipEventDisableTiming));
+    HIP_CHECK(hipEventRecord(u->copied, bfz::stream()));
+    HIP_CHECK(hipStreamWaitEvent(handover_stream(), u->copied, 0));
+    *up = u.release();
+    return 0;
+  });
+}
+
+int bfz_cycles_push(bfz_cycle_upload* up, size_t first, const bfz_cycle* cycles, size_t n) {
+  return guarded([&] {
+    if (!up || !cycles) throw std::runtime_error("null argument");
+    if (n == 0 || first > up->n || n > up->n - first)
+      throw std::runtime_error("cycles_push: chunk [" + std::to_string(first) + ", +" +
+                               std::to_string(n) + ") outside the " + std::to_string(up->n) +
+                               " announced cycles");
+    up->ranges.push_back({first, n});
+    HIP_CHECK(hipMemcpyAsync(up->d.p + first, cycles, n * sizeof(bfz::Cycle), hipMemcpyHostToDevice,
+                             handover_stream()));
+    return 0;
+  });
+}
+
+int bfz_cycles_finish(bfz_cycle_upload* up, const bfz_memory_event* memory, size_t n_memory,
+                      bfz_record** rec) {
+  std::unique_ptr<bfz_cycle_upload> u(up);  // consumed whatever happens
+  return guarded([&] {
+    if (!u || !rec) throw std::runtime_error("null argument");
+    // the prover stream waits for the last copy on the device (no host synchronisation); done
+    // first, so the buffer goes back to the stream-ordered pool after the copies on any path
+    HIP_CHECK(hipEventRecord(u->copied, handover_stream()));
+    HIP_CHECK(hipStreamWaitEvent(bfz::stream(), u->copied, 0));
+    check_cycle_counts(u->n, n_memory);
+    std::sort(u->ranges.begin(), u->ranges.end());
+    size_t next = 0;
+    for (const auto& r : u->ranges) {
+      if (r.first != next)
+        throw std::runtime_error(r.first < next ? "cycles_finish: a cycle was pushed twice"
+                                                : "cycles_finish: cycles missing at " + std::to_string(next));
+      next = r.first + r.second;
+    }
+    if (next != u->n) throw std::runtime_error("cycles_finish: cycles missing at " + std::to_string(next));
+    *rec = record_from_device_cycles(u->pk, u->d, u->n, memory, n_memory).release();
+    return 0;
+  });
+}
+
+void bfz_cycles_abort(bfz_cycle_upload* up) {
+  if (!up) return;
+  std::lock_guard<std::mutex> lk(g_mu);
+  (void)hipStreamSynchronize(handover_stream());  // no copy may still write the buffer
+  delete up;
 }
 
 namespace {
