@@ -347,7 +347,7 @@ def host_threads():
     return min(avail, int(os.environ.get("OMP_NUM_THREADS") or avail)), avail
 
 
-def compiled_handover(pk, rec, prove, best, ref_proof, chunk=1 << 18):
+def compiled_handover(pk, rec, prove, best, ref_proof, chunk=1 << 15):
     """The Rust HipProver::prove path with its host conversion in compiled code (VERDICT r4 item
     2): crates/bf-hip-prover/standin/libcycle_arrays.so converts record.cpu_events -- laid out as
     rustc lays out Vec<CpuEvent>, 48 B each -- on the job's threads straight into page-locked
@@ -438,6 +438,60 @@ def sharded_latency(dist, pk, rec, rank, world, device, ref_proof, steps=3):
         return {"error": f"{type(e).__name__}: {e}"}
 
 
+# Collective-time model of the N-GPU sharded proof.  Inputs, stated as
+# assumptions because this pool has no multi-GPU box to measure RCCL on:
+#  - xGMI: 7 links per MI355X, ~153 GB/s each (the build brief's figure, taken as bidirectional),
+#    so 76.8 GB/s per direction per link; every pair of GPUs of the node has its own link;
+#  - RCCL reaches XGMI_EFF of a link's rate on large messages and costs XGMI_ALPHA_US per
+#    collective (launch + synchronisation) on small ones.
+XGMI_LINK_GBS = 153.6 / 2
+XGMI_EFF = 0.7
+XGMI_ALPHA_US = 20.0
+
+
+def collective_ms(kind, nbytes, world):
+    """One collective on a fully connected node: an all-gather of `nbytes` per rank sends it to
+    each of the N-1 peers over their own links in parallel; a sum all-reduce of an `nbytes`
+    vector is a reduce-scatter plus an all-gather of nbytes/N per peer link."""
+    bw = XGMI_LINK_GBS * XGMI_EFF * 1e9
+    if kind == 0:
+        return (XGMI_ALPHA_US * 1e-6 + nbytes / bw) * 1e3
+    return (2 * XGMI_ALPHA_US * 1e-6 + 2 * (nbytes / world) / bw) * 1e3
+
+
+def collective_model(exchanges, world):
+    """Per-rank bytes and modeled time of the logged collectives of one rank's share."""
+    ms = sum(collective_ms(k, b, world) for k, b in exchanges)
+    recv = sum((world - 1) * b if k == 0 else 2 * (world - 1) * b / world for k, b in exchanges)
+    big = sorted(((b, k) for k, b in exchanges), reverse=True)[:4]
+    return {"collectives": len(exchanges),
+            "allgathers": sum(1 for k, _ in exchanges if k == 0),
+            "allreduces": sum(1 for k, _ in exchanges if k == 1),
+            "recv_bytes_per_rank": int(recv),
+            "largest": [{"kind": "all-gather" if k == 0 else "all-reduce", "bytes_per_rank": int(b),
+                         "ms": round(collective_ms(k, b, world), 3)} for b, k in big],
+            "modeled_ms": round(ms, 3)}
+
+
+def replication_tradeoff(stages, cells_main, cells_perm, world):
+    """The work every rank repeats at N GPUs (main + permutation iDFTs, LogUp rows: measured on
+    the slowest rank's share) against the column-sharded alternative: each rank runs the iDFT and
+    the full coset LDE of 1/N of the columns, then one all-to-all turns column shards into the
+    row shards the Merkle subtrees need (each rank sends (N-1)/N of its 2n x w/N LDE words, over
+    N-1 links in parallel); the LogUp rows need whole rows of the main trace, so sharding them
+    would add an all-gather of the main trace (modeled the same way)."""
+    replicated = stages.get("main_idft_ms", 0) + stages.get("perm_idft_ms", 0) + stages.get("perm_rows_ms", 0)
+    lde_words = 2 * (cells_main + cells_perm)
+    a2a_bytes_per_link = 4 * lde_words / world / world
+    a2a = collective_ms(0, a2a_bytes_per_link, world)
+    gather_main = collective_ms(0, 4 * cells_main / world, world)
+    alt = ((stages.get("main_idft_ms", 0) + stages.get("perm_idft_ms", 0)) / world
+           + stages.get("perm_rows_ms", 0) / world + a2a + gather_main)
+    return {"replicated_ms": round(replicated, 3), "column_sharded_ms": round(alt, 3),
+            "all_to_all_ms": round(a2a, 3), "main_trace_allgather_ms": round(gather_main, 3),
+            "choice": "replicate" if replicated <= alt else "column-shard"}
+
+
 def shard_solo(pk, rec, world, steps=3):
     """Per-rank work of a `world`-GPU sharded proof measured on ONE GPU (VERDICT r2 Next 6):
     bfz_record_prove_shard_solo runs rank k's share -- the same kernels and sizes as
@@ -447,6 +501,7 @@ def shard_solo(pk, rec, world, steps=3):
     from bfz import _lib as _l
     L = _l.lib()
     ranks = []
+    exchanges = None
     for k in range(world):
         best = None
         for _ in range(steps):
@@ -455,11 +510,22 @@ def shard_solo(pk, rec, world, steps=3):
                                                    ctypes.byref(tm)))
             if best is None or tm.total_ms < best.total_ms:
                 best = tm
+        if exchanges is None:  # every rank takes part in the same collectives
+            n = ctypes.c_size_t()
+            _l.check(L.bfz_shard_solo_exchanges(None, None, 0, ctypes.byref(n)))
+            kinds = (ctypes.c_int * max(n.value, 1))()
+            sizes = (ctypes.c_uint64 * max(n.value, 1))()
+            _l.check(L.bfz_shard_solo_exchanges(kinds, sizes, n.value, ctypes.byref(n)))
+            exchanges = [(kinds[i], sizes[i]) for i in range(n.value)]
+            cells = (best.main_cells, best.perm_cells)
         ranks.append({"rank": k, "total_ms": round(best.total_ms, 3),
                       "stages_ms": {n: round(v, 3) for n, v in best.as_dict().items()
                                     if n.endswith("_ms") and n not in ("total_ms", "lde_ms", "ntt_kernel_ms", "p2_kernel_ms")}})
     worst = max(r["total_ms"] for r in ranks)
+    slow = max(ranks, key=lambda r: r["total_ms"])
     return {"world": world, "max_rank_ms": worst, "ranks": ranks,
+            "collectives": collective_model(exchanges, world),
+            "replication": replication_tradeoff(slow["stages_ms"], cells[0], cells[1], world),
             "what": f"each rank's share of a {world}-GPU sharded proof run alone on one GPU with "
                     "no-op exchanges (bfz_record_prove_shard_solo); excludes collective time"}
 
@@ -730,9 +796,25 @@ def main():
             runs = {n: shard_solo(pk, rec, n) for n in solo}
             curve = {"1": round(ms, 3)}
             curve.update({str(n): runs[n]["max_rank_ms"] for n in solo})
+            modeled = {str(n): runs[n]["collectives"]["modeled_ms"] for n in solo}
+            with_coll = {"1": round(ms, 3)}
+            with_coll.update({str(n): round(runs[n]["max_rank_ms"] + runs[n]["collectives"]["modeled_ms"], 3)
+                              for n in solo})
             line["shard_solo_curve"] = {
                 "ms_per_proof_by_gpus": curve,
                 "speedup_by_gpus": {k: round(ms / v, 2) for k, v in curve.items()},
+                "modeled_collective_ms": modeled,
+                "ms_per_proof_with_collectives": with_coll,
+                "speedup_with_collectives": {k: round(ms / v, 2) for k, v in with_coll.items()},
+                "collectives_by_gpus": {str(n): runs[n]["collectives"] for n in solo},
+                "replication_by_gpus": {str(n): runs[n]["replication"] for n in solo},
+                "collective_model": {
+                    "xgmi_link_gbs_per_direction": XGMI_LINK_GBS, "efficiency": XGMI_EFF,
+                    "latency_us_per_collective": XGMI_ALPHA_US,
+                    "source": "build brief: 7 xGMI links x ~153 GB/s per MI355X (bidirectional "
+                              "assumed); efficiency and latency assumed, not measured (no "
+                              "multi-GPU box on this pool); collectives are synchronous on the "
+                              "prover stream (no overlap)"},
                 "what": "one proof split over N GPUs, predicted: N = 1 is the timed single-GPU "
                         "proof; N > 1 is the slowest rank's share run alone on this GPU with "
                         "no-op exchanges (bfz_record_prove_shard_solo), before collective time",

@@ -340,38 +340,84 @@ struct CycleArrays {
     memory: Vec<sys::bfz_memory_event>,
 }
 
+fn cycle_of(e: &bf_core_executor::events::CpuEvent) -> sys::bfz_cycle {
+    let (prev_ts, prev_value) = match e.mv_access {
+        None => (0, 0),
+        Some(MemoryRecordEnum::Read(a)) => (a.prev_timestamp, 0),
+        Some(MemoryRecordEnum::Write(a)) => (a.prev_timestamp, a.prev_value),
+    };
+    sys::bfz_cycle { pc: e.pc, mp: e.mp, prev_ts, mv: e.mv, prev_value, _pad: [0; 2] }
+}
+
+fn memory_events(r: &ExecutionRecord) -> Vec<sys::bfz_memory_event> {
+    // HashMap-drain order (executor.rs:74); libbfz sorts it into the normal form
+    r.cpu_memory_access
+        .iter()
+        .map(|e| sys::bfz_memory_event {
+            addr: e.addr,
+            initial_timestamp: e.initial_mem_access.timestamp,
+            final_timestamp: e.final_mem_access.timestamp,
+            initial_value: e.initial_mem_access.value,
+            final_value: e.final_mem_access.value,
+            _pad: [0; 2],
+        })
+        .collect()
+}
+
+/// Cycles per bfz_cycles_push: small enough that the DMA of the first chunks starts while the
+/// rest are converted (crates/bf-hip-prover/standin/cycle_arrays.cpp times the same loop).
+const HANDOVER_CHUNK: usize = 1 << 15;
+
 impl CycleArrays {
+    #[allow(dead_code)] // the one-shot hand-over (bfz_record_from_cycles); prove uses hand_over
     fn new(r: &ExecutionRecord) -> Self {
-        let cycle = |e: &bf_core_executor::events::CpuEvent| {
-            let (prev_ts, prev_value) = match e.mv_access {
-                None => (0, 0),
-                Some(MemoryRecordEnum::Read(a)) => (a.prev_timestamp, 0),
-                Some(MemoryRecordEnum::Write(a)) => (a.prev_timestamp, a.prev_value),
-            };
-            sys::bfz_cycle { pc: e.pc, mp: e.mp, prev_ts, mv: e.mv, prev_value, _pad: [0; 2] }
-        };
         let mut cycles = PinnedVec::new(r.cpu_events.len());
         cycles
             .as_mut_slice()
             .par_iter_mut()
             .zip(r.cpu_events.par_iter())
-            .for_each(|(o, e)| *o = cycle(e));
-        Self {
-            cycles,
-            // HashMap-drain order (executor.rs:74); libbfz sorts it into the normal form
-            memory: r
-                .cpu_memory_access
-                .iter()
-                .map(|e| sys::bfz_memory_event {
-                    addr: e.addr,
-                    initial_timestamp: e.initial_mem_access.timestamp,
-                    final_timestamp: e.final_mem_access.timestamp,
-                    initial_value: e.initial_mem_access.value,
-                    final_value: e.final_mem_access.value,
-                    _pad: [0; 2],
-                })
-                .collect(),
+            .for_each(|(o, e)| *o = cycle_of(e));
+        Self { cycles, memory: memory_events(r) }
+    }
+
+    /// The pipelined hand-over: rayon converts record.cpu_events chunk by chunk into page-locked
+    /// memory and each chunk is pushed (bfz_cycles_push) as soon as it is written, so its DMA runs
+    /// while the next chunks are converted; bfz_cycles_finish validates, expands and returns the
+    /// device record (the same record as bfz_record_from_cycles over CycleArrays::new).
+    fn hand_over(pk: *const sys::bfz_pk, r: &ExecutionRecord) -> *mut sys::bfz_record {
+        let n = r.cpu_events.len();
+        let mut cycles = PinnedVec::<sys::bfz_cycle>::new(n);
+        let mut up = core::ptr::null_mut();
+        sys::check(unsafe { sys::bfz_cycles_begin(pk, n, &mut up) });
+        let up_addr = up as usize; // the handle is only passed back to libbfz (thread-safe calls)
+        let failed = core::sync::atomic::AtomicI32::new(0);
+        cycles
+            .as_mut_slice()
+            .par_chunks_mut(HANDOVER_CHUNK)
+            .zip(r.cpu_events.par_chunks(HANDOVER_CHUNK))
+            .enumerate()
+            .for_each(|(k, (o, e))| {
+                for (oi, ei) in o.iter_mut().zip(e) {
+                    *oi = cycle_of(ei);
+                }
+                let rc = unsafe {
+                    sys::bfz_cycles_push(up_addr as *mut sys::bfz_cycle_upload, k * HANDOVER_CHUNK,
+                                         o.as_ptr(), o.len())
+                };
+                if rc != 0 {
+                    failed.store(rc, core::sync::atomic::Ordering::Relaxed);
+                }
+            });
+        if failed.load(core::sync::atomic::Ordering::Relaxed) != 0 {
+            unsafe { sys::bfz_cycles_abort(up) };
+            sys::check(failed.into_inner());
         }
+        let memory = memory_events(r);
+        let mut rec = core::ptr::null_mut();
+        // finish returns after every copy has landed: the pinned chunks may be freed afterwards
+        sys::check(unsafe { sys::bfz_cycles_finish(up, memory.as_ptr(), memory.len(), &mut rec) });
+        drop(cycles);
+        rec
     }
 }
 
@@ -489,22 +535,10 @@ impl MachineProver<SC, A> for HipProver {
         #[cfg(feature = "debug")]
         self.machine().generate_dependencies(record, None);
         pk.observe_into(challenger); // prover.rs:572
-        // the compact hand-over (16 B per cycle); EventArrays + bfz_record_from_events remains
-        // for callers that hold the full event vectors
-        let events = CycleArrays::new(record);
-        let mut rec = core::ptr::null_mut();
-        sys::check(unsafe {
-            sys::bfz_record_from_cycles(
-                pk.dev,
-                events.cycles.as_ptr(),
-                events.cycles.len(),
-                events.memory.as_ptr(),
-                events.memory.len(),
-                &mut rec,
-            )
-        });
-        let rec = HipRecord(rec);
-        drop(events); // the events are in HBM now
+        // the compact hand-over (16 B per cycle), pipelined with its DMA; CycleArrays::new +
+        // bfz_record_from_cycles and EventArrays + bfz_record_from_events remain for callers that
+        // hold the cycles or the full event vectors
+        let rec = HipRecord(CycleArrays::hand_over(pk.dev, record));
         let mut data = core::ptr::null_mut();
         let mut root = [0u32; 8];
         sys::check(unsafe {

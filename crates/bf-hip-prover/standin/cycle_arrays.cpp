@@ -15,6 +15,8 @@
 //   ca_handover  the pipelined form: the events are converted in chunks and each chunk is handed
 //                to bfz_cycles_push as soon as it is written, so the DMA of chunk k runs while
 //                chunk k+1 is converted; bfz_cycles_finish returns the record
+#include <immintrin.h>
+
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -104,8 +106,17 @@ Pool& pool(int threads) {
   return *p;
 }
 
+// Streaming (non-temporal) 16-byte stores: the output is written once and read only by the DMA
+// engine, so it need not be read into the cache first; the fence orders the stores before the
+// copy that follows.
 void convert_range(const RsCpuEvent* ev, bfz_cycle* out, size_t a, size_t b) {
-  for (size_t i = a; i < b; i++) out[i] = cycle_of(ev[i]);
+  for (size_t i = a; i < b; i++) {
+    const bfz_cycle c = cycle_of(ev[i]);
+    __m128i v;
+    __builtin_memcpy(&v, &c, 16);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(out + i), v);
+  }
+  _mm_sfence();
 }
 
 }  // namespace

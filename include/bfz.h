@@ -81,6 +81,11 @@ typedef struct {
    * 0 unsharded), fold + forward DFT (this rank's residue and its next-residue shards when
    * sharded; the whole coset LDE unsharded), Merkle hashing (split). */
   double perm_rows_ms, perm_idft_ms, perm_dft_ms, perm_hash_ms;
+  /* The main commit (main_commit_ms, prover.rs:209-236) in the same parts: iDFT of the main
+   * columns (replicated when sharded; 0 unsharded), fold + forward DFT, Merkle hashing. */
+  double main_idft_ms, main_dft_ms, main_hash_ms;
+  /* Base-field cells (sum of height x width) of the main and permutation traces. */
+  double main_cells, perm_cells;
 } bfz_timings;
 
 int bfz_init(int device);
@@ -342,6 +347,13 @@ int bfz_record_prove_sharded(const bfz_pk* pk, const bfz_record* rec, int rank, 
  * Predicts the per-rank critical path of an N-GPU proof without N GPUs. */
 int bfz_record_prove_shard_solo(const bfz_pk* pk, const bfz_record* rec, int rank, int world,
                                 bfz_timings* timings);
+
+/* The collectives of the last bfz_record_prove_shard_solo run, in call order: kinds[i] = 0 for an
+ * all-gather (bytes[i] = this rank's contribution; it receives world - 1 times that), 1 for a sum
+ * all-reduce of u32 words (bytes[i] = the vector's size).  *n = the number of collectives; at most
+ * cap entries are written.  Feeds bench.py's collective-time model of the N-GPU curve; the
+ * reference has no multi-GPU prover. */
+int bfz_shard_solo_exchanges(int* kinds, uint64_t* bytes, size_t cap, size_t* n);
 
 /* Column-sharded PCS commit + FRI commit phase of a synthetic trace (BASELINE.json configs 4
  * and 5).  Replaces, for one n x (world * w_local) trace, TwoAdicFriPcs::commit

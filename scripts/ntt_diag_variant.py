@@ -30,11 +30,11 @@ DIAG_TW = ("__device__ __forceinline__ uint32_t diag_tw(int l) {\n"
 PATCHES = {
     "twconst": [
         ("ntt_dev.h", "constexpr uint32_t G24 = cpow(3, 127);", DIAG_TW + "constexpr uint32_t G24 = cpow(3, 127);"),
-        ("ntt_dev.h", "if (l < (1 << kk)) tws[l] = tt[(size_t)l << (g0 + s0)];",
-         "if (l < (1 << kk)) tws[l] = diag_tw(l); (void)tt;"),
+        ("ntt_dev.h", "tws[l] = ld_b(rt, off, ((1u << (s0 + g0 + kk)) + ((uint32_t)l << (g0 + s0))) * 4u);",
+         "tws[l] = diag_tw(l); (void)rt; (void)off;"),
         ("ntt_dev.h", "const uint32_t wb = tw[(1u << (s0 + t)) + (m_low << s0) + lo_g];",
          "const uint32_t wb = diag_tw(t);"),
-        ("ntt_dev.h", "pre[(1 << kk) - 1 + l] = tw[(1u << (g0 + kk)) + m_low + ((uint32_t)l << g0)];",
+        ("ntt_dev.h", "pre[(1 << kk) - 1 + l] = ld_b(rsrc_of(tw), m_low * 4u, ((1u << (g0 + kk)) + ((uint32_t)l << g0)) * 4u);",
          "pre[(1 << kk) - 1 + l] = diag_tw(l);"),
     ],
     "noexch": [

@@ -31,6 +31,8 @@ class Timings(ctypes.Structure):
         ("reduce_kernel_launches", c_int),
         ("perm_rows_ms", c_double), ("perm_idft_ms", c_double), ("perm_dft_ms", c_double),
         ("perm_hash_ms", c_double),
+        ("main_idft_ms", c_double), ("main_dft_ms", c_double), ("main_hash_ms", c_double),
+        ("main_cells", c_double), ("perm_cells", c_double),
     ]
 
     def as_dict(self) -> dict:
@@ -119,6 +121,8 @@ SIGNATURES = [
     ("bfz_cycles_push", c_int, [c_void_p, c_size_t, c_void_p, c_size_t]),
     ("bfz_cycles_finish", c_int, [c_void_p, c_void_p, c_size_t, POINTER(c_void_p)]),
     ("bfz_cycles_abort", None, [c_void_p]),
+    ("bfz_shard_solo_exchanges", c_int, [POINTER(c_int), POINTER(ctypes.c_uint64), c_size_t,
+                                         POINTER(c_size_t)]),
     ("bfz_record_prove_sharded", c_int, [c_void_p, c_void_p, c_int, c_int, ALLGATHER_FN,
                                          ALLREDUCE_FN, c_void_p, POINTER(POINTER(c_uint8)),
                                          POINTER(c_size_t), POINTER(Timings)]),

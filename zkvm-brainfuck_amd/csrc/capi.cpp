@@ -791,6 +791,13 @@ PinnedCache& pinned_cache() {
   return *c;
 }
 
+// The collectives of the last bfz_record_prove_shard_solo run: (0 all-gather | 1 sum all-reduce,
+// this rank's bytes).
+std::vector<std::pair<int, uint64_t>>& solo_exchange_log() {
+  static auto* v = new std::vector<std::pair<int, uint64_t>>();
+  return *v;
+}
+
 // Copies of the chunked hand-over (bfz_cycles_push) run here, beside the prover stream.
 hipStream_t handover_stream() {
   static hipStream_t s = [] {
@@ -994,6 +1001,11 @@ void fill_timings(const bfz::StageTimes& st, bfz_timings* t) {
   t->perm_idft_ms = st.perm_idft;
   t->perm_dft_ms = st.perm_dft;
   t->perm_hash_ms = st.perm_hash;
+  t->main_idft_ms = st.main_idft;
+  t->main_dft_ms = st.main_dft;
+  t->main_hash_ms = st.main_hash;
+  t->main_cells = st.main_cells;
+  t->perm_cells = st.perm_cells;
 }
 struct ShardScope {  // installs the shard context for one proof
   explicit ShardScope(bfz::ShardCtx* c) { bfz::shard_ctx() = c; }
@@ -1042,6 +1054,19 @@ int bfz_record_prove_sharded(const bfz_pk* pk, const bfz_record* rec, int rank, 
   });
 }
 
+int bfz_shard_solo_exchanges(int* kinds, uint64_t* bytes, size_t cap, size_t* n) {
+  return guarded([&] {
+    if (!n) throw std::runtime_error("null argument");
+    const auto& log = solo_exchange_log();
+    *n = log.size();
+    for (size_t i = 0; i < log.size() && i < cap; i++) {
+      if (kinds) kinds[i] = log[i].first;
+      if (bytes) bytes[i] = log[i].second;
+    }
+    return 0;
+  });
+}
+
 int bfz_record_prove_shard_solo(const bfz_pk* pk, const bfz_record* rec, int rank, int world,
                                 bfz_timings* t) {
   return guarded([&] {
@@ -1052,8 +1077,12 @@ int bfz_record_prove_shard_solo(const bfz_pk* pk, const bfz_record* rec, int ran
     c.rank = rank;
     c.world = world;
     c.solo = true;
-    c.allgather = [](const void*, size_t, void*) {};  // receive buffers keep what they hold
-    c.allreduce_sum_u32 = [](uint32_t*, size_t) {};
+    // the exchanges are no-ops (receive buffers keep what they hold), logged for the bench's
+    // collective-time model (bfz_shard_solo_exchanges)
+    auto& log = solo_exchange_log();
+    log.clear();
+    c.allgather = [&log](const void*, size_t bytes, void*) { log.push_back({0, bytes}); };
+    c.allreduce_sum_u32 = [&log](uint32_t*, size_t n) { log.push_back({1, n * 4}); };
     ShardScope scope(&c);
     bfz::ProveOptions o = opts();
     o.timing = true;

@@ -197,8 +197,9 @@ __global__ __launch_bounds__(1 << (B - 4)) void k_ntt_tile(const uint32_t* __res
       x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
     }
   } else {
+    const __amdgpu_buffer_rsrc_t rs = rsrc_of(S);
 #pragma unroll
-    for (int i = 0; i < E; i++) lds[i * (T + T / E) + tpad] = S[i * T + tid];
+    for (int i = 0; i < E; i++) lds[i * (T + T / E) + tpad] = ld_b(rs, tid * 4u, (uint32_t)(i * T) * 4u);
   }
   // window w: first stage g0(w) and its stage range [kk_lo, kk_hi) (compile-time after unrolling)
   auto win_g0 = [](int w) {
@@ -266,8 +267,9 @@ __global__ __launch_bounds__(1 << (B - 4)) void k_ntt_tile(const uint32_t* __res
     else
       r16_window<DIF, false, true, R>(x, g0, kk_lo, kk_hi, 0, m_low, 0, tw);
     if (direct_out) {
+      const __amdgpu_buffer_rsrc_t rd = rsrc_of(D);
 #pragma unroll
-      for (int i = 0; i < E; i++) D[i * T + tid] = x[i];
+      for (int i = 0; i < E; i++) st_b(rd, tid * 4u, (uint32_t)(i * T) * 4u, x[i]);
     } else {
 #pragma unroll
       for (int i = 0; i < E; i++) lds[pb + (i << g0) + ((i << g0) >> R)] = x[i];
@@ -275,8 +277,9 @@ __global__ __launch_bounds__(1 << (B - 4)) void k_ntt_tile(const uint32_t* __res
   }
   if constexpr (DIF) {
     __syncthreads();
+    const __amdgpu_buffer_rsrc_t rd = rsrc_of(D);
 #pragma unroll
-    for (int i = 0; i < E; i++) D[i * T + tid] = lds[i * (T + T / E) + tpad];
+    for (int i = 0; i < E; i++) st_b(rd, tid * 4u, (uint32_t)(i * T) * 4u, lds[i * (T + T / E) + tpad]);
   }
 }
 
@@ -329,8 +332,10 @@ __global__ __launch_bounds__(1 << (MidPlan<L>::b2 + MidPlan<L>::c2 - 4)) void k_
     const uint32_t m_low = rest & ((1 << g0) - 1);
     const uint32_t m_base = m_low | ((uint32_t)(rest >> g0) << (g0 + 4));
     if (w == 0) {
+      const __amdgpu_buffer_rsrc_t rs = rsrc_of(S);
+      const uint32_t off = ((m_base << s0) + lo) * 4u;  // i's part of the index is uniform
 #pragma unroll
-      for (int i = 0; i < 16; i++) x[i] = S[(uint32_t)((m_base | ((uint32_t)i << g0)) << s0) + lo];
+      for (int i = 0; i < 16; i++) x[i] = ld_b(rs, off, ((uint32_t)i << (g0 + s0)) * 4u);
     } else {
       __syncthreads();
 #pragma unroll
@@ -379,8 +384,10 @@ __global__ __launch_bounds__(1 << (MidPlan<L>::b2 + MidPlan<L>::c2 - 4)) void k_
         done_hi = gg;
         r16_window<true, false, true>(x, gg, 0, kk_hi, s0, m_low, lo_g, tw_fwd);
         if (w == nwin - 1) {
+          const __amdgpu_buffer_rsrc_t rd = rsrc_of(Dh);
+          const uint32_t off = ((mb << s0) + lo) * 4u;
 #pragma unroll
-          for (int i = 0; i < 16; i++) Dh[(uint32_t)((mb | ((uint32_t)i << gg)) << s0) + lo] = x[i];
+          for (int i = 0; i < 16; i++) st_b(rd, off, ((uint32_t)i << (gg + s0)) * 4u, x[i]);
         } else {
 #pragma unroll
           for (int i = 0; i < 16; i++)

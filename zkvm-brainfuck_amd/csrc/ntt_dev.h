@@ -15,6 +15,21 @@ using namespace kb;
 // through LDS.  The first window loads straight from HBM and the last stores straight
 // back, so a pass is one read + one write of the data.
 
+// Buffer loads / stores through a descriptor built from a wave-uniform base: the per-thread
+// part of an address is the 32-bit voffset and the compile-time part (stage, l, i) the scalar
+// soffset, so a twiddle or data access costs no VALU address arithmetic (a flat global access
+// with an offset beyond the 12-bit immediate costs two half-rate 64-bit adds per load).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), /*stride*/ 0, /*bytes*/ 0x7fffffff,
+                                           0x00020000);
+}
+__device__ __forceinline__ uint32_t ld_b(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0);
+}
+__device__ __forceinline__ void st_b(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, uint32_t v) {
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)voff, (int)soff, 0);
+}
+
 constexpr uint32_t G24 = cpow(3, 127);
 constexpr uint32_t root_pow2(int k) {  // w_(2^k), canonical
   uint32_t g = G24;
@@ -73,10 +88,12 @@ __device__ __forceinline__ void r16_window(uint32_t (&x)[1 << R], int g0, int kk
       for (int l = 0; l < H; l++)
         if (l < (1 << kk)) tws[l] = pre[(1 << kk) - 1 + l];
     } else if (TW_LOAD) {  // one table load per twiddle instead of a load and a multiply
-      const uint32_t* tt = tw + (1u << (s0 + g0 + kk)) + ((size_t)m_low << s0) + lo_g;
+      const __amdgpu_buffer_rsrc_t rt = rsrc_of(tw);
+      const uint32_t off = ((m_low << s0) + lo_g) * 4u;  // the per-thread part of the index
 #pragma unroll
       for (int l = 0; l < H; l++)
-        if (l < (1 << kk)) tws[l] = tt[(size_t)l << (g0 + s0)];
+        if (l < (1 << kk))
+          tws[l] = ld_b(rt, off, ((1u << (s0 + g0 + kk)) + ((uint32_t)l << (g0 + s0))) * 4u);
     } else {
       const int t = g0 + kk;
       const uint32_t wb = tw[(1u << (s0 + t)) + (m_low << s0) + lo_g];
@@ -118,7 +135,7 @@ __device__ __forceinline__ void load_window_tw(uint32_t (&pre)[(1 << R) - 1], in
     if (kk < kk_lo || kk >= kk_hi) continue;
 #pragma unroll
     for (int l = 0; l < (1 << kk); l++)
-      pre[(1 << kk) - 1 + l] = tw[(1u << (g0 + kk)) + m_low + ((uint32_t)l << g0)];
+      pre[(1 << kk) - 1 + l] = ld_b(rsrc_of(tw), m_low * 4u, ((1u << (g0 + kk)) + ((uint32_t)l << g0)) * 4u);
   }
 }
 

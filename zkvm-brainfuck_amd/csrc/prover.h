@@ -90,6 +90,10 @@ struct StageTimes {          // milliseconds, measured with HIP events on the pr
   int reduce_kernel_launches = 0;
   // the LogUp stage in parts (bfz.h bfz_timings)
   double perm_rows = 0, perm_idft = 0, perm_dft = 0, perm_hash = 0;
+  // the main commit in parts: iDFT of the main columns, fold + forward DFT, Merkle hashing
+  double main_idft = 0, main_dft = 0, main_hash = 0;
+  // base-field cells (sum of n x w) of the main and permutation traces
+  double main_cells = 0, perm_cells = 0;
 };
 
 std::unique_ptr<ProvingKey> setup(const std::string& program_src);

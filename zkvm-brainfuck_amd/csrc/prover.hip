@@ -511,10 +511,15 @@ void commit_main_impl(MainData& md, ProofScope& ps, bool fetch_root = true) {
   const Plan plan = make_plan();
   md.mainr = Round();
   md.mainr.mats.resize(nc);
-  for (int k = 0; k < nc; k++)
+  LdeSplit split{ps.tms ? &ps.tms->main_idft : nullptr, ps.tms ? &ps.tms->main_dft : nullptr};
+  for (int k = 0; k < nc; k++) {
     lde_into(md.mainr.mats[k], dt.evals[md.order[k]].p, md.hn[k], CHIP_INFO[md.chip[k]].main_w, ONE,
-             st, &ps.ev, ps.tms, &plan, &chip_next_cols(md.chip[k]).main);
+             st, &ps.ev, ps.tms, &plan, &chip_next_cols(md.chip[k]).main, ps.tms ? &split : nullptr);
+    if (ps.tms) ps.tms->main_cells += (double)md.hn[k] * CHIP_INFO[md.chip[k]].main_w;
+  }
+  hipEvent_t eh = ps.ev.on ? ps.ev.begin(st) : nullptr;
   md.mainr.commit(st, fetch_root);
+  if (ps.ev.on) ps.ev.end(eh, st, &ps.tms->main_hash);
   md.root_on_host = fetch_root;
   if (ps.ev.on) ps.ev.end(e0, st, &ps.tms->main_commit);
 }
@@ -657,6 +662,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     if (ev.on) ev.end(br, st, &tms->perm_rows);
     if (k == 0) htrace().mark("perm_rows launched");
     LdeSplit split{tms ? &tms->perm_idft : nullptr, tms ? &tms->perm_dft : nullptr};
+    if (tms) tms->perm_cells += (double)hn[k] * 4 * pw;
     lde_into(permr.mats[k], pe.p, hn[k], 4 * pw, ONE, st, &ev, tms, &plan, &chip_next_cols(c).perm,
              tms ? &split : nullptr);
   }
