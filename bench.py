@@ -546,6 +546,32 @@ def sustained(step, seconds, sync):
             "what": "back-to-back proofs of the same record after the timed steps (one rank)"}
 
 
+def sustained_lanes(pk, rec, ms_one, seconds, ref_proof):
+    """The same steady state through bfz_record_prove_repeat with 1 and 2 proofs in flight
+    (VERDICT r4 item 5): two lanes (streams, pools, pinned mailboxes, one host thread each) let
+    one proof's latency-bound launches run beside the other's bulk kernels.  Every proof is
+    compared with the first inside the library; the first is checked here."""
+    import ctypes
+    from bfz import _lib as _l
+    L = _l.lib()
+    out = {}
+    count = max(4, int(seconds * 1e3 / max(ms_one, 1.0)))
+    for inflight in (1, 2):
+        ptr = ctypes.POINTER(ctypes.c_uint8)()
+        n = ctypes.c_size_t()
+        wall = ctypes.c_double()
+        _l.check(L.bfz_record_prove_repeat(ctypes.c_void_p(pk.handle), rec, count, inflight,
+                                           ctypes.byref(ptr), ctypes.byref(n), ctypes.byref(wall)))
+        if _l.take_bytes(ptr, n.value) != ref_proof:
+            raise SystemExit("bench: bfz_record_prove_repeat proof differs from the verified proof")
+        out[str(inflight)] = round(wall.value / count, 3)
+    return {"proofs": count, "ms_per_proof_by_inflight": out,
+            "what": "bfz_record_prove_repeat: `proofs` proofs of the record back to back with 1 or 2 "
+                    "in flight (one lane = stream + buffer pool + pinned mailboxes + host thread); "
+                    "all byte-identical, the first checked against the verified proof; the "
+                    "headline `value` stays the single-proof latency"}
+
+
 def timed_steps(step, steps, dist=None, sync=lambda: None):
     """Runs `step` exactly `steps` times between barrier + device synchronize on both sides
     and returns ms per step, the max over ranks (every rank proves its own replica; the
@@ -742,6 +768,7 @@ def main():
         if last["proof"] != proof:
             raise SystemExit("bench: the last sustained proof differs from the verified proof")
         extra["sustained"]["last_proof_checked"] = True
+        extra["sustained"]["lanes"] = sustained_lanes(pk, rec, ms, args.sustain_s, proof)
     hung = False
     if world > 1 and not sharded and not args.no_extra:  # every rank takes part
         # RCCL has no run on this pool's one-GPU boxes: a hang in it must not cost the replica

@@ -266,6 +266,9 @@ extern "C" {
     pub fn bfz_cycles_abort(up: *mut bfz_cycle_upload);
     pub fn bfz_host_alloc(bytes: usize, out: *mut *mut c_void) -> c_int;
     pub fn bfz_host_free(p: *mut c_void);
+    pub fn bfz_record_prove_repeat(pk: *const bfz_pk, rec: *const bfz_record, count: c_int,
+                                   inflight: c_int, proof: *mut *mut u8, len: *mut usize,
+                                   wall_ms: *mut f64) -> c_int;
     pub fn bfz_record_prove_sharded(pk: *const bfz_pk, rec: *const bfz_record, rank: c_int,
                                     world: c_int, allgather: bfz_allgather_fn,
                                     allreduce_sum: bfz_allreduce_u32_fn, ctx: *mut c_void,

@@ -336,6 +336,16 @@ void bfz_host_free(void* p);
  * place when the callback returns): ncclAllGather / ncclAllReduce run on them directly. */
 typedef int (*bfz_allgather_fn)(void* ctx, const void* send, size_t bytes, void* recv);
 typedef int (*bfz_allreduce_u32_fn)(void* ctx, uint32_t* data, size_t n);
+/* `count` proofs of one record back to back with `inflight` (1 or 2) of them in flight, each on
+ * its own stream, pool and pinned mailboxes ("lane", one host thread each): one proof's
+ * latency-bound launches (Merkle tree tops, the FRI tail, the transcript steps) then run beside
+ * the other's bulk hashing.  Every proof must be byte-identical to the first (an error
+ * otherwise); *proof receives the first; wall_ms (optional) the whole run.  The steady-state
+ * throughput of the bfz_record_prove loop; the reference proves one shard at a time
+ * (utils/prove.rs:38-66). */
+int bfz_record_prove_repeat(const bfz_pk* pk, const bfz_record* rec, int count, int inflight,
+                            uint8_t** proof, size_t* len, double* wall_ms);
+
 int bfz_record_prove_sharded(const bfz_pk* pk, const bfz_record* rec, int rank, int world,
                              bfz_allgather_fn allgather, bfz_allreduce_u32_fn allreduce_sum,
                              void* ctx, uint8_t** proof, size_t* proof_len, bfz_timings* timings);

@@ -20,9 +20,16 @@ step ab
 for rep in 1 2; do
   for v in "$@"; do ab $v $rep || { echo "ab $v failed"; exit 1; }; done
 done
-step tests && timeout -k 10 600 python -u -m pytest tests/test_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread \
-  -k "coset_lde or chunked or record_from_cycles or fibo_x4 or commit_root" > $O/pytest.log 2>&1 && \
-step bench && timeout -k 10 600 python bench.py --no-cpu-baseline > $O/bench.json 2> $O/bench.err && \
+if [ -z "$SKIP_TESTS" ]; then
+  if [ -n "$FULL_TESTS" ]; then
+    step tests && timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread \
+      > $O/pytest.log 2>&1 || exit 1
+  else
+    step tests && timeout -k 10 600 python -u -m pytest tests/test_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread \
+      -k "coset_lde or chunked or record_from_cycles or fibo_x4 or commit_root or repeat or batch" > $O/pytest.log 2>&1 || exit 1
+  fi
+fi
+step bench && timeout -k 10 600 python bench.py --no-cpu-baseline $BENCH_ARGS > $O/bench.json 2> $O/bench.err && \
 step done
 rc=$?
 echo "exit $rc"; cat $O/status; tail -2 $O/pytest.log

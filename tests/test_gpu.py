@@ -234,6 +234,32 @@ def test_prove_batch_pipelined_matches_single(client):
     assert client.prove_batch(pk, []) == []
 
 
+def test_record_prove_repeat_two_lanes_matches_oracle(client):
+    """bfz_record_prove_repeat: proofs of one record back to back with one or
+    two in flight, each on its own stream / pool / mailboxes; every proof is checked against the
+    first inside the library and the first is the oracle's.  Then the default lane still proves."""
+    from bfz import events
+    prog, stdin = guests.FIBO, [255]
+    pk, vk = client.setup(prog)
+    rec = events.ExecutionRecordArrays.from_executor(prog, stdin)
+    drec = events.record_from_events(pk, rec)
+    want = O.prove(prog, stdin)
+    L = _lib.lib()
+    for inflight, count in ((1, 3), (2, 7)):
+        ptr = ctypes.POINTER(ctypes.c_uint8)()
+        n = ctypes.c_size_t()
+        wall = ctypes.c_double()
+        _lib.check(L.bfz_record_prove_repeat(ctypes.c_void_p(pk.handle), ctypes.c_void_p(drec.handle),
+                                             count, inflight, ctypes.byref(ptr), ctypes.byref(n),
+                                             ctypes.byref(wall)))
+        assert _lib.take_bytes(ptr, n.value) == want, inflight
+        assert wall.value > 0
+    with pytest.raises(_lib.BfzError, match="inflight"):
+        _lib.check(L.bfz_record_prove_repeat(ctypes.c_void_p(pk.handle), ctypes.c_void_p(drec.handle),
+                                             2, 3, ctypes.byref(ptr), ctypes.byref(n), None))
+    assert _prove_record(pk, drec) == want
+
+
 def test_prove_batch_error_does_not_hang(client):
     """An executor failure (missing input) in the middle of a batch is reported, the other
     threads stop, and the library stays usable."""

@@ -121,6 +121,8 @@ SIGNATURES = [
     ("bfz_cycles_push", c_int, [c_void_p, c_size_t, c_void_p, c_size_t]),
     ("bfz_cycles_finish", c_int, [c_void_p, c_void_p, c_size_t, POINTER(c_void_p)]),
     ("bfz_cycles_abort", None, [c_void_p]),
+    ("bfz_record_prove_repeat", c_int, [c_void_p, c_void_p, c_int, c_int, POINTER(POINTER(c_uint8)),
+                                        POINTER(c_size_t), POINTER(ctypes.c_double)]),
     ("bfz_shard_solo_exchanges", c_int, [POINTER(c_int), POINTER(ctypes.c_uint64), c_size_t,
                                          POINTER(c_size_t)]),
     ("bfz_record_prove_sharded", c_int, [c_void_p, c_void_p, c_int, c_int, ALLGATHER_FN,

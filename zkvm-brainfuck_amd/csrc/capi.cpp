@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstddef>
 #include <cstdlib>
 #include <cstring>
@@ -643,7 +645,11 @@ int bfz_prove_batch(const bfz_pk* pk, const uint8_t* const* stdins, const size_t
     }
     if (E < 1 || E > 64) throw std::runtime_error("exec_threads must be in 1..64");
     bfz::BatchStats bs;
-    auto v = bfz::prove_batch(*pk->pk, jobs, opts(), E, &bs);
+    static const int inflight = [] {  // proofs in flight (lanes); BFZ_INFLIGHT = 1 for one
+      const char* e = std::getenv("BFZ_INFLIGHT");
+      return e && *e == '1' ? 1 : bfz::MAX_LANES;
+    }();
+    auto v = bfz::prove_batch(*pk->pk, jobs, opts(), E, inflight, &bs);
     emit_all(v, proofs, proof_lens, (size_t)-1);
     if (stats) {
       stats->wall_ms = bs.wall_ms;
@@ -1024,6 +1030,38 @@ int bfz_record_prove(const bfz_pk* pk, const bfz_record* rec, uint8_t** proof, s
     const int r = emit(std::move(v), proof, len);
     bfz::host_mark("emitted");
     return r;
+  });
+}
+
+int bfz_record_prove_repeat(const bfz_pk* pk, const bfz_record* rec, int count, int inflight,
+                            uint8_t** proof, size_t* len, double* wall_ms) {
+  return guarded([&] {
+    if (!pk || !rec || !proof || !len) throw std::runtime_error("null argument");
+    if (count < 1 || inflight < 1 || inflight > bfz::MAX_LANES)
+      throw std::runtime_error("prove_repeat: count >= 1, inflight 1.." + std::to_string(bfz::MAX_LANES));
+    HIP_CHECK(hipStreamSynchronize(bfz::stream()));  // the record is complete for every lane
+    const bfz::ProveOptions o = opts();
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<uint8_t> first;
+    std::mutex mu;
+    std::atomic<int> next{0};
+    std::atomic<bool> differ{false};
+    bfz::run_lanes(inflight, [&](int) {
+      for (int k; (k = next.fetch_add(1)) < count;) {
+        auto v = bfz::prove_events(*pk->pk, rec->ev, o, nullptr);
+        std::lock_guard<std::mutex> lk(mu);
+        if (first.empty()) {
+          first = std::move(v);
+        } else {
+          if (v != first) differ = true;
+          bfz::release_proof_buffer(std::move(v));
+        }
+      }
+    });
+    if (wall_ms)
+      *wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (differ) throw std::runtime_error("prove_repeat: proofs of one record differ");
+    return emit(std::move(first), proof, len);
   });
 }
 

@@ -11,6 +11,8 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <functional>
+#include <atomic>
 #include <map>
 #include <unordered_map>
 #include <stdexcept>
@@ -89,6 +91,42 @@ class DevicePool {
   std::unordered_map<void*, size_t> size_of_;
 };
 
+// A proof lane: the device context one proof runs in -- its stream, the stream-ordered buffer
+// pool of that stream, the pinned staging arena of its in-proof uploads and its transcript
+// mailboxes.  The process has a default lane; bfz_prove_batch and bfz_record_prove_repeat keep
+// two proofs in flight on two lanes (one host thread each), so the latency-bound launches of one
+// proof (tree tops, the FRI tail, transcript steps) run beside the other's bulk kernels.
+constexpr int MAX_LANES = 2;
+struct Lane {
+  int id = 0;
+  hipStream_t stream = nullptr;
+  DevicePool pool;
+  uint8_t* stage = nullptr;  // pinned arena of upload_async, rewound by staging_reset
+  size_t stage_cap = 0, stage_off = 0;
+  uint8_t* box = nullptr;  // pinned mailbox of fetch
+  size_t box_cap = 0;
+  hipEvent_t spin = nullptr;  // spin_sync's event
+  // open_impl's pinned buffers (prover.hip): the opened-value groups and the proof's tail
+  static constexpr int NGEV = 4;
+  hipEvent_t gev[NGEV] = {};
+  void* gbox = nullptr;
+  size_t gcap = 0;
+  uint32_t* tbox = nullptr;
+  size_t tcap = 0;
+};
+Lane& lane();           // this thread's lane (the default lane unless a LaneScope is active)
+Lane* lane_at(int i);   // lane i (0 = the default lane), created on first use; lives for the process
+struct LaneScope {      // runs this thread's device work on another lane while in scope
+  Lane* prev;
+  explicit LaneScope(Lane* l);
+  ~LaneScope();
+};
+
+// body(i) on lane i for i < n, concurrently: lane 0 on the calling thread, the others on
+// threads of their own; each thread counts as holding the API lock (the caller holds it for
+// the whole call).  Waits for every lane's stream; rethrows the first exception.
+void run_lanes(int n, const std::function<void(int)>& body);
+
 DevicePool& pool();
 
 template <class T>
@@ -96,13 +134,14 @@ struct DBuf {  // RAII device buffer from the pool (or a borrowed view of memory
   T* p = nullptr;
   size_t n = 0;
   bool owned = true;
+  DevicePool* from = nullptr;  // the pool it returns to (the lane it was allocated in)
   DBuf() = default;
   explicit DBuf(size_t count) { reset(count); }
   DBuf(const DBuf&) = delete;
   DBuf& operator=(const DBuf&) = delete;
-  DBuf(DBuf&& o) noexcept : p(o.p), n(o.n), owned(o.owned) { o.p = nullptr; o.n = 0; }
+  DBuf(DBuf&& o) noexcept : p(o.p), n(o.n), owned(o.owned), from(o.from) { o.p = nullptr; o.n = 0; }
   DBuf& operator=(DBuf&& o) noexcept {
-    if (this != &o) { free(); p = o.p; n = o.n; owned = o.owned; o.p = nullptr; o.n = 0; }
+    if (this != &o) { free(); p = o.p; n = o.n; owned = o.owned; from = o.from; o.p = nullptr; o.n = 0; }
     return *this;
   }
   static DBuf borrow(T* ptr, size_t count) {  // not released on destruction
@@ -116,10 +155,11 @@ struct DBuf {  // RAII device buffer from the pool (or a borrowed view of memory
     free();
     n = count;
     owned = true;
-    p = (T*)pool().alloc(count * sizeof(T));
+    from = &pool();
+    p = (T*)from->alloc(count * sizeof(T));
   }
   void free() {
-    if (p && owned) pool().release(p);
+    if (p && owned) from->release(p);
     p = nullptr;
     n = 0;
     owned = true;
@@ -138,7 +178,7 @@ struct DevMatrix {
 // Twiddle tables: T[h + j] = w_{2h}^j for h = 2^k (k < LOGMAX), j < h   (forward)
 //                 and w_{2h}^-j                                          (inverse)
 struct Twiddles {
-  int logmax = 0;
+  std::atomic<int> logmax{0};
   DBuf<uint32_t> fwd, inv;
   std::vector<uint32_t> host_fwd, host_inv;
   void ensure(int log_n);

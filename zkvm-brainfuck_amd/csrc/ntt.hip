@@ -14,7 +14,15 @@
 #include "ntt_dev.h"
 
 #include <cstdlib>
+#include <mutex>
 #include <cstring>
+
+#ifndef BFZ_DIF_DIN
+#define BFZ_DIF_DIN 0
+#endif
+#ifndef BFZ_MID_PF
+#define BFZ_MID_PF 0
+#endif
 
 namespace bfz {
 
@@ -165,8 +173,9 @@ __global__ __launch_bounds__(1024) void k_ntt_r16(const uint32_t* __restrict__ s
 // TWPF: each window's table twiddles are loaded one window ahead (into registers, double
 // buffered) instead of at the window's start, where every wave of the block would wait for the
 // L2 round trip at the same time (the waves run in lockstep between the LDS exchanges).  Shipped
-// for the 2^14 DIF tile (profiles/r04/ab_twiddle_prefetch.txt: DIF pass 198 -> 185 us per 2^26
-// elements, DIT neutral).
+// for the 2^14 tiles: DIF pass 198 -> 185 us per 2^26 elements (profiles/r04/
+// ab_twiddle_prefetch.txt); the DIT pass, neutral with flat loads, 86.5 -> 79 us per 2^25 once the
+// loads were buffer loads with scalar offsets (profiles/r05/ab_ntt_variants.txt).
 // WS (B = 14): windows g0 = 0, 4, 6, 10 (DIT; the DIF the reverse).  The threads of a wave hold
 // the same 1024 consecutive elements (bits [10, 14) = the wave index) in every window with
 // g0 <= 6, so the exchanges between such windows go through the wave's own LDS region with a
@@ -183,6 +192,8 @@ __global__ __launch_bounds__(1 << (B - 4)) void k_ntt_tile(const uint32_t* __res
   static_assert(!DIN || !DIF, "direct first window: DIT passes only");
   static_assert(!WS || B >= 13, "wave-local windows: 2^13 / 2^14 tiles");
   constexpr int R = 4, E = 1 << R, T = 1 << (B - R), NW = (B + R - 1) / R;
+  // WS DIF: the first window (g0 = B - 4) holds elements tid + i T, a coalesced HBM order
+  constexpr bool DIFIN = DIF && WS && BFZ_DIF_DIN;
   extern __shared__ uint32_t lds[];
   const int tid = threadIdx.x;
   const int tpad = tid + (tid >> R);
@@ -196,6 +207,10 @@ __global__ __launch_bounds__(1 << (B - 4)) void k_ntt_tile(const uint32_t* __res
       const uint4 v = s4[q];
       x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
     }
+  } else if constexpr (DIFIN) {
+    const __amdgpu_buffer_rsrc_t rs = rsrc_of(S);
+#pragma unroll
+    for (int i = 0; i < E; i++) x[i] = ld_b(rs, tid * 4u, (uint32_t)(i * T) * 4u);
   } else {
     const __amdgpu_buffer_rsrc_t rs = rsrc_of(S);
 #pragma unroll
@@ -239,7 +254,7 @@ __global__ __launch_bounds__(1 << (B - 4)) void k_ntt_tile(const uint32_t* __res
     const uint32_t m_base = m_low | ((uint32_t)(tid >> g0) << (g0 + R));
     const uint32_t pb = m_base + (m_base >> R);
     const bool direct_out = !DIF && w == NW - 1;
-    if (!DIN || w > 0) {
+    if (!(DIN || DIFIN) || w > 0) {
       if (WS && w > 0 && win_g0(w - 1) <= 6 && g0 <= 6) {  // the wave's own 1024 elements
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -315,11 +330,12 @@ __global__ __launch_bounds__(1 << (MidPlan<L>::b2 + MidPlan<L>::c2 - 4)) void k_
   extern __shared__ uint32_t lds[];
   const int tid = threadIdx.x;
   const int nlo_log = s0 - c;
-  const size_t lo_blk = blockIdx.x & ((1u << nlo_log) - 1);
-  const size_t hi = (size_t)blockIdx.x >> nlo_log;
+  const uint32_t bx = blockIdx.x, by = blockIdx.y;
+  const size_t lo_blk = bx & ((1u << nlo_log) - 1);
+  const size_t hi = (size_t)bx >> nlo_log;
   const size_t base = (hi << (s0 + b)) + (lo_blk << c);
-  const uint32_t* S = src + (size_t)blockIdx.y * src_stride + base;
-  uint32_t* D = lde + (size_t)blockIdx.y * 2 * n + base;
+  const uint32_t* S = src + (size_t)by * src_stride + base;
+  uint32_t* D = lde + (size_t)by * 2 * n + base;
   const int lo = tid & ((1 << c) - 1);
   const uint32_t lo_g = (uint32_t)(lo_blk << c) + lo;
   const int rest = tid >> c;
@@ -369,6 +385,11 @@ __global__ __launch_bounds__(1 << (MidPlan<L>::b2 + MidPlan<L>::c2 - 4)) void k_
       if (half && nwin > 1) __syncthreads();  // the lo half's last LDS reads are done
       uint32_t* Dh = D + (size_t)half * n;
       int done_hi = b;
+#if BFZ_MID_PF
+      uint32_t pre[2][15];
+      load_window_tw_s<4>(pre[0], max(b - 4, 0), 0, min(4, b - max(b - 4, 0)), s0,
+                          rest & ((1 << max(b - 4, 0)) - 1), lo_g, tw_fwd);
+#endif
 #pragma unroll
       for (int w = 0; w < nwin; w++) {  // DFT of this half
         const int gg = max(b - 4 - 4 * w, 0);
@@ -382,7 +403,16 @@ __global__ __launch_bounds__(1 << (MidPlan<L>::b2 + MidPlan<L>::c2 - 4)) void k_
         }
         const int kk_hi = min(4, done_hi - gg);
         done_hi = gg;
+#if BFZ_MID_PF
+        if (w + 1 < nwin) {
+          const int g1 = max(b - 8 - 4 * w, 0);
+          load_window_tw_s<4>(pre[(w + 1) & 1], g1, 0, min(4, gg - g1), s0, rest & ((1 << g1) - 1),
+                              lo_g, tw_fwd);
+        }
+        r16_window<true, false, true, 4, true>(x, gg, 0, kk_hi, s0, m_low, lo_g, tw_fwd, pre[w & 1]);
+#else
         r16_window<true, false, true>(x, gg, 0, kk_hi, s0, m_low, lo_g, tw_fwd);
+#endif
         if (w == nwin - 1) {
           const __amdgpu_buffer_rsrc_t rd = rsrc_of(Dh);
           const uint32_t off = ((mb << s0) + lo) * 4u;
@@ -482,8 +512,8 @@ static std::vector<R16Pass> r16_plan(int L) {
 
 // The 2^14 tiles and the middle passes use more than the default 64 KiB of dynamic LDS.
 static void r16_attrs() {
-  static bool done = false;
-  if (done) return;
+  static std::once_flag once;
+  std::call_once(once, [] {
   const int bytes = ((1 << R16_TILE_LOG) + (1 << (R16_TILE_LOG - 4))) * 4;
   const void* fs[] = {(const void*)&k_ntt_r16<true>, (const void*)&k_ntt_r16<false>,
                       (const void*)&k_lde_mid<14>, (const void*)&k_lde_mid<15>,
@@ -492,16 +522,16 @@ static void r16_attrs() {
                       (const void*)&k_lde_mid<20>, (const void*)&k_lde_mid<21>,
                       (const void*)&k_lde_mid<22>, (const void*)&k_lde_mid<23>,
                       (const void*)&k_ntt_tile<true, R16_TILE_LOG, false, true, true>,
-                      (const void*)&k_ntt_tile<false, R16_TILE_LOG, true, false, true>,
-                      (const void*)&k_ntt_tile<false, R16_TILE_LOG, false, false, true>};
+                      (const void*)&k_ntt_tile<false, R16_TILE_LOG, true, true, true>,
+                      (const void*)&k_ntt_tile<false, R16_TILE_LOG, false, true, true>};
   for (const void* f : fs)
     HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-  done = true;
+  });
 }
 
-// One contiguous tile pass: the 2^14 tiles run wave-local (WS), the DIF with its twiddles one
-// window ahead (TWPF); a DIT reads its first window straight from HBM when the rows are
-// 16-byte aligned (DIN).
+// One contiguous tile pass: the 2^14 tiles run wave-local (WS) with their twiddles one window
+// ahead (TWPF); a DIT reads its first window straight from HBM when the rows are 16-byte aligned
+// (DIN).
 template <bool DIF, int B>
 static void tile_launch(dim3 grid, const uint32_t* in, size_t is, uint32_t* dst, size_t ds,
                         const uint32_t* tw, hipStream_t st) {
@@ -513,10 +543,10 @@ static void tile_launch(dim3 grid, const uint32_t* in, size_t is, uint32_t* dst,
     hipLaunchKernelGGL((k_ntt_tile<true, B, false, WS, WS>), grid, block, lds * 4, st, in, dst, is,
                        ds, tw);
   else if (din)
-    hipLaunchKernelGGL((k_ntt_tile<false, B, true, false, WS>), grid, block, lds * 4, st, in, dst,
+    hipLaunchKernelGGL((k_ntt_tile<false, B, true, WS, WS>), grid, block, lds * 4, st, in, dst,
                        is, ds, tw);
   else
-    hipLaunchKernelGGL((k_ntt_tile<false, B, false, false, WS>), grid, block, lds * 4, st, in, dst,
+    hipLaunchKernelGGL((k_ntt_tile<false, B, false, WS, WS>), grid, block, lds * 4, st, in, dst,
                        is, ds, tw);
 }
 
@@ -606,7 +636,12 @@ std::map<PowKey, DBuf<uint32_t>>& pow_cache() {
   static auto* m = new std::map<PowKey, DBuf<uint32_t>>();
   return *m;
 }
+std::mutex& cache_mu() {  // the device table caches below are shared by the proof lanes
+  static std::mutex m;
+  return m;
+}
 const uint32_t* scale_tables(uint32_t shift, int L, int B) {
+  std::lock_guard<std::mutex> lk(cache_mu());
   auto& cache = pow_cache();
   auto it = cache.find({shift, L});
   if (it != cache.end()) return it->second.p;
@@ -730,6 +765,7 @@ __global__ __launch_bounds__(256) void k_fold_residue(const uint32_t* __restrict
 
 // Two-level power table of a (with 1/2^L folded into the high half), cached per (a, L).
 static const uint32_t* residue_powers(uint32_t a, int L, int B) {
+  std::lock_guard<std::mutex> lk(cache_mu());
   static auto* cache = new std::map<std::pair<uint32_t, int>, DBuf<uint32_t>>();
   auto it = cache->find({a, L});
   if (it != cache->end()) return it->second.p;

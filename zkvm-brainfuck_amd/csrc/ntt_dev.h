@@ -139,4 +139,20 @@ __device__ __forceinline__ void load_window_tw(uint32_t (&pre)[(1 << R) - 1], in
   }
 }
 
+// The same for a strided window (stage s0 + g0 + kk, positions (m_low + l 2^g0) << s0 + lo_g).
+template <int R>
+__device__ __forceinline__ void load_window_tw_s(uint32_t (&pre)[(1 << R) - 1], int g0, int kk_lo,
+                                                 int kk_hi, int s0, uint32_t m_low, uint32_t lo_g,
+                                                 const uint32_t* __restrict__ tw) {
+  const __amdgpu_buffer_rsrc_t rt = rsrc_of(tw);
+  const uint32_t off = ((m_low << s0) + lo_g) * 4u;
+#pragma unroll
+  for (int kk = 0; kk < R; kk++) {
+    if (kk < kk_lo || kk >= kk_hi) continue;
+#pragma unroll
+    for (int l = 0; l < (1 << kk); l++)
+      pre[(1 << kk) - 1 + l] = ld_b(rt, off, ((1u << (s0 + g0 + kk)) + ((uint32_t)l << (g0 + s0))) * 4u);
+  }
+}
+
 }  // namespace bfz

@@ -20,9 +20,10 @@ struct BatchStats {
 };
 
 // Proofs of `jobs` (stdins of pk.program), in order; byte-identical to prove() per job.
+// inflight: proofs on the GPU at once (1 or 2 lanes, gpu.h Lane).
 std::vector<std::vector<uint8_t>> prove_batch(const ProvingKey& pk, const std::vector<Job>& jobs,
                                               const ProveOptions& opt, int exec_threads,
-                                              BatchStats* stats);
+                                              int inflight, BatchStats* stats);
 
 // Process-wide pinned HostEvents for single proofs (bfz_prove, bfz_record_new); callers hold the
 // C ABI lock.

@@ -38,7 +38,9 @@ hipStream_t copy_stream() {
 }
 
 // Device event arrays of one pipeline slot: plain hipMalloc memory (not the stream-ordered
-// pool, which is ordered on the prover stream only), grown on demand and kept for the process.
+// pools, which are ordered on the lanes' streams only), grown on demand and kept for the process.
+// Job j uses slot j % NSLOT: with two proofs in flight, a third slot takes the next upload.
+constexpr int NSLOT = MAX_LANES + 1;
 struct EventSlot {
   static constexpr int N = 6;  // cpu, alu, jump, meminstr, io, memory
   void* p[N] = {};
@@ -54,8 +56,8 @@ struct EventSlot {
 };
 EventSlot* slots() {
   static EventSlot* s = [] {
-    auto* x = new EventSlot[2];
-    for (int i = 0; i < 2; i++) {
+    auto* x = new EventSlot[NSLOT];
+    for (int i = 0; i < NSLOT; i++) {
       HIP_CHECK(hipEventCreateWithFlags(&x[i].uploaded, hipEventDisableTiming));
       HIP_CHECK(hipEventCreateWithFlags(&x[i].consumed, hipEventDisableTiming));
       HIP_CHECK(hipEventRecord(x[i].consumed, stream()));  // "never read yet"
@@ -95,13 +97,14 @@ HostEvents& scratch_events() {
 
 std::vector<std::vector<uint8_t>> prove_batch(const ProvingKey& pk, const std::vector<Job>& jobs,
                                               const ProveOptions& opt, int exec_threads,
-                                              BatchStats* stats) {
+                                              int inflight, BatchStats* stats) {
   const size_t n = jobs.size();
   std::vector<std::vector<uint8_t>> proofs(n);
   if (n == 0) return proofs;
   const auto t_start = std::chrono::steady_clock::now();
   const int E = std::max(1, std::min<int>(exec_threads, (int)n));
-  const size_t H = (size_t)E + 2;  // pinned host buffers: E executing + 2 waiting / uploading
+  const int F = std::max(1, std::min(inflight, MAX_LANES));  // proofs in flight (lanes)
+  const size_t H = (size_t)E + F + 1;  // pinned host buffers: E executing + the rest waiting
   auto& hp = host_pool();
   while (hp.size() < H) {
     auto* h = new HostEvents();
@@ -115,14 +118,14 @@ std::vector<std::vector<uint8_t>> prove_batch(const ProvingKey& pk, const std::v
   HIP_CHECK(hipMemcpyAsync(prog_d.p, pk.program.instructions.data(),
                            pk.program.instructions.size() * sizeof(Instruction),
                            hipMemcpyHostToDevice, stream()));
+  HIP_CHECK(hipStreamSynchronize(stream()));  // read by every lane
 
   std::mutex mu;
   std::condition_variable cv;
   std::vector<HostEvents*> free_h(hp.begin(), hp.begin() + H);
   std::vector<HostEvents*> executed(n, nullptr);
-  std::vector<char> uploaded(n, 0);
-  long consumed_upto = -1;  // jobs whose slot-consumed event has been recorded
-  size_t next_job = 0;
+  std::vector<char> uploaded(n, 0), consumed(n, 0);  // consumed: the slot's event is recorded
+  size_t next_job = 0, next_prove = 0;
   bool abort = false;
   std::exception_ptr err;
   std::vector<double> exec_ms(n, 0.0), up_ms(n, 0.0);
@@ -167,13 +170,13 @@ std::vector<std::vector<uint8_t>> prove_batch(const ProvingKey& pk, const std::v
         {
           std::unique_lock<std::mutex> lk(mu);
           cv.wait(lk, [&] {
-            return abort || (executed[j] && consumed_upto >= (long)j - 2);
+            return abort || (executed[j] && (j < NSLOT || consumed[j - NSLOT]));
           });
           if (abort) return;
           h = executed[j];
         }
-        EventSlot& s = sl[j & 1];
-        HIP_CHECK(hipEventSynchronize(s.consumed));  // job j-2 has read this slot
+        EventSlot& s = sl[j % NSLOT];
+        HIP_CHECK(hipEventSynchronize(s.consumed));  // job j - NSLOT has read this slot
         const auto t0 = std::chrono::steady_clock::now();
         copy_arr(s, 0, h->cpu, cs);
         copy_arr(s, 1, h->alu, cs);
@@ -197,17 +200,22 @@ std::vector<std::vector<uint8_t>> prove_batch(const ProvingKey& pk, const std::v
   for (int e = 0; e < E; e++) threads.emplace_back(executor);
   threads.emplace_back(uploader);
   double prove_ms = 0;
-  try {
-    for (size_t j = 0; j < n; j++) {
+  // F lanes prove jobs in order of arrival (job j on whichever lane takes it), each on its own
+  // stream and pool: one proof's latency-bound launches run beside another's bulk kernels
+  auto prover = [&](int) {
+    for (;;) {
+      size_t j;
       HostEvents* h = nullptr;
       {
         std::unique_lock<std::mutex> lk(mu);
+        if (abort || next_prove >= n) return;
+        j = next_prove++;
         cv.wait(lk, [&] { return abort || uploaded[j]; });
-        if (abort) break;
+        if (abort) return;
         h = executed[j];
       }
       const auto t0 = std::chrono::steady_clock::now();
-      EventSlot& s = sl[j & 1];
+      EventSlot& s = sl[j % NSLOT];
       DeviceEvents ev;
       ev.cpu = view<CpuEvent>(s, 0, h->cpu.n);
       ev.alu = view<AluEvent>(s, 1, h->alu.n);
@@ -228,12 +236,24 @@ std::vector<std::vector<uint8_t>> prove_batch(const ProvingKey& pk, const std::v
       HIP_CHECK(hipEventRecord(s.consumed, stream()));
       {
         std::lock_guard<std::mutex> lk(mu);
-        consumed_upto = (long)j;
+        consumed[j] = 1;
         cv.notify_all();
       }
-      proofs[j] = prove_device(pk, dt, opt, nullptr);
-      prove_ms += ms_since(t0);
+      auto pf = prove_device(pk, dt, opt, nullptr);
+      const double ms = ms_since(t0);
+      std::lock_guard<std::mutex> lk(mu);
+      proofs[j] = std::move(pf);
+      prove_ms += ms;
     }
+  };
+  try {
+    run_lanes(F, [&](int i) {
+      try {
+        prover(i);
+      } catch (...) {
+        fail(std::current_exception());
+      }
+    });
   } catch (...) {
     fail(std::current_exception());
   }

@@ -794,7 +794,8 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   const bool dev_zeta = !plan.on();
   EF* const zeta_d = cums_d.p + nc + 9;
   if (dev_zeta) challenge_zeta(dc_d.p, quotr.tree.layers.back().p, zeta_d, st);
-  static Mailbox roots_box;  // process-global: the API lock is held (see open_impl's gbox)
+  static Mailbox roots_boxes[MAX_LANES];  // per lane: the API lock is held (see open_impl's gbox)
+  Mailbox& roots_box = roots_boxes[lane().id];
   roots_box.post(cums_d.p, (nc + 10) * sizeof(EF), st);
   EF zeta = ef_zero();
   std::vector<EF> cums(nc + 10);  // [0, nc): the chips' cumulative sums (written into the proof)
@@ -988,22 +989,24 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
                                                           rounds[r]->mats.back().lde.width);
     }
   std::vector<EF> opened(nvals);
-  // gev / gbox (and tbox below) are process-global and reallocated on the assumption that no
-  // copy into them is pending: safe only because every caller holds the API lock and every
-  // proof synchronizes before it returns.  A caller outside the lock is a bug.
+  // gev / gbox (and tbox below) belong to this proof's lane and are reallocated on the
+  // assumption that no copy into them is pending: safe only because every caller holds the API
+  // lock (one proof per lane at a time) and every proof synchronizes before it returns.  A
+  // caller outside the lock is a bug.
   if (api_lock_depth() == 0) throw std::logic_error("open_impl called outside the bfz API lock");
-  static hipEvent_t gev[NGROUP] = {};
-  static EF* gbox = nullptr;  // pinned: the groups' opened values
-  static size_t gcap = 0;
+  static_assert(NGROUP <= Lane::NGEV, "lane events");
+  Lane& ln = lane();
+  hipEvent_t* gev = ln.gev;
   if (grouped) {
     if (!gev[0])
-      for (hipEvent_t& e : gev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    if (nvals > gcap) {  // no copy into it is pending: every proof waits for its groups
-      if (gbox) HIP_CHECK(hipHostFree(gbox));
-      gcap = std::max(nvals, (size_t)1024);
-      HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&gbox), gcap * sizeof(EF), hipHostMallocDefault));
+      for (int g = 0; g < NGROUP; g++) HIP_CHECK(hipEventCreateWithFlags(&gev[g], hipEventDisableTiming));
+    if (nvals > ln.gcap) {  // no copy into it is pending: every proof waits for its groups
+      if (ln.gbox) HIP_CHECK(hipHostFree(ln.gbox));
+      ln.gcap = std::max(nvals, (size_t)1024);
+      HIP_CHECK(hipHostMalloc(&ln.gbox, ln.gcap * sizeof(EF), hipHostMallocDefault));
     }
   }
+  EF* gbox = static_cast<EF*>(ln.gbox);
   for (int g = 0; g < (grouped ? NGROUP : 1); g++) {
     open_batch(open2g[g], 2, st);  // barycentric openings: two partial + two final launches
     open_batch(open1g[g], 1, st);
@@ -1370,13 +1373,13 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   fri_transcript_tail(dch, nt ? dstate.p : nullptr, layers.back().v.p, POW_BITS, nq, Lmax,
                       tailbuf.p + T_Q, tailbuf.p + T_RES, st);
   gather_queries(segs, tailbuf.p + T_Q, nq, tailbuf.p + T_W, shard, st);
-  static uint32_t* tbox = nullptr;  // pinned: the tail of the proof
-  static size_t tcap = 0;
-  if (tail_n > tcap) {  // no copy into it is pending: every proof waits for its tail
-    if (tbox) HIP_CHECK(hipHostFree(tbox));
-    tcap = tail_n + tail_n / 4;
-    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&tbox), tcap * 4, hipHostMallocDefault));
+  Lane& tl = lane();  // pinned: the tail of the proof (per lane)
+  if (tail_n > tl.tcap) {  // no copy into it is pending: every proof waits for its tail
+    if (tl.tbox) HIP_CHECK(hipHostFree(tl.tbox));
+    tl.tcap = tail_n + tail_n / 4;
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&tl.tbox), tl.tcap * 4, hipHostMallocDefault));
   }
+  uint32_t* tbox = tl.tbox;
   HIP_CHECK(hipMemcpyAsync(tbox, tailbuf.p, tail_n * 4, hipMemcpyDeviceToHost, st));
   spin_sync(st);
   htrace().mark("queries gathered");

@@ -12,6 +12,8 @@
 // 3 w_2n^k H_n (split_evals / split_domains), ready for the chunk LDE.
 #include "quotient.h"
 
+#include <mutex>
+
 #include <array>
 #include <map>
 
@@ -165,6 +167,8 @@ static void launch_q(const QuotRows& in, int logN, const QuotParams* qp_dev, con
 // The selector-denominator table of 3 H_N (k_sel_inv), built on first use per log N.  It is
 // written on the prover stream, so every later reader on that stream sees it complete.
 static const uint32_t* sel_inv_table(int logN, const QuotParams& qp, hipStream_t st) {
+  static std::mutex mu;  // shared by the proof lanes
+  std::lock_guard<std::mutex> lk(mu);
   static auto* cache = new std::map<int, DBuf<uint32_t>>();
   auto it = cache->find(logN);
   if (it != cache->end()) return it->second.p;
@@ -173,6 +177,7 @@ static const uint32_t* sel_inv_table(int logN, const QuotParams& qp, hipStream_t
   hipLaunchKernelGGL(k_sel_inv, dim3(ceil_div(N, 256)), dim3(256), 0, st, logN, qp.shift,
                      qp.wn_inv, (const uint32_t*)twiddles().fwd.p, d.p);
   KCHECK();
+  HIP_CHECK(hipStreamSynchronize(st));  // complete before another lane's stream reads it
   const uint32_t* p = d.p;
   cache->emplace(logN, std::move(d));
   return p;

@@ -12,26 +12,59 @@
 
 namespace bfz {
 
-DevicePool& pool() {
-  static DevicePool* p = new DevicePool();  // intentionally leaked: freed by process exit
-  return *p;
-}
-
 namespace {
-hipStream_t g_stream = nullptr;
+std::mutex g_lanes_mu;
+Lane* g_lanes[MAX_LANES] = {};  // intentionally leaked: they live for the process
+thread_local Lane* tl_lane = nullptr;
+Lane* make_lane(int id) {
+  auto* l = new Lane();
+  l->id = id;
+  HIP_CHECK(hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking));
+  return l;
 }
-hipStream_t stream() {
-  static hipStream_t s = [] {
-    hipStream_t st;
-    HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    g_stream = st;
-    return st;
-  }();
-  return s;
+}  // namespace
+
+Lane* lane_at(int i) {
+  if (i < 0 || i >= MAX_LANES) throw std::runtime_error("lane index out of range");
+  std::lock_guard<std::mutex> lk(g_lanes_mu);
+  if (!g_lanes[i]) g_lanes[i] = make_lane(i);
+  return g_lanes[i];
 }
+Lane& lane() {
+  if (tl_lane) return *tl_lane;
+  static Lane* d = lane_at(0);
+  return *d;
+}
+LaneScope::LaneScope(Lane* l) : prev(tl_lane) { tl_lane = l; }
+LaneScope::~LaneScope() { tl_lane = prev; }
+
+DevicePool& pool() { return lane().pool; }
+
+void run_lanes(int n, const std::function<void(int)>& body) {
+  std::exception_ptr err;
+  std::mutex mu;
+  auto one = [&](int i) {
+    try {
+      ApiLockScope held;  // the caller holds the API lock for the whole call
+      LaneScope ls(lane_at(i));
+      body(i);
+      HIP_CHECK(hipStreamSynchronize(stream()));
+    } catch (...) {
+      std::lock_guard<std::mutex> lk(mu);
+      if (!err) err = std::current_exception();
+    }
+  };
+  std::vector<std::thread> th;
+  for (int i = 1; i < n; i++) th.emplace_back(one, i);
+  one(0);
+  for (auto& t : th) t.join();
+  if (err) std::rethrow_exception(err);
+}
+hipStream_t stream() { return lane().stream; }
 
 void quiesce() noexcept {
-  if (g_stream) (void)hipStreamSynchronize(g_stream);
+  for (Lane* l : g_lanes)
+    if (l && l->stream) (void)hipStreamSynchronize(l->stream);
 }
 
 namespace {
@@ -84,35 +117,23 @@ KernelProbe& reduce_probe() {
 // up; from pinned memory it is a plain stream-ordered DMA.  The arena is rewound when a proof
 // ends (after its stream synchronize), so a slot is never rewritten while its copy may still
 // be pending.
-namespace {
-struct Staging {
-  uint8_t* base = nullptr;
-  size_t cap = 0, off = 0;
-};
-Staging& staging() {
-  static Staging* s = [] {
-    auto* st = new Staging();
-    st->cap = (size_t)8 << 20;
-    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&st->base), st->cap, hipHostMallocDefault));
-    return st;
-  }();
-  return *s;
-}
-}  // namespace
-
-void staging_reset() { staging().off = 0; }
+void staging_reset() { lane().stage_off = 0; }
 
 void upload_async(void* dst, const void* src, size_t bytes, hipStream_t st) {
   if (!bytes) return;
-  Staging& s = staging();
+  Lane& s = lane();
+  if (!s.stage) {
+    s.stage_cap = (size_t)8 << 20;
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&s.stage), s.stage_cap, hipHostMallocDefault));
+  }
   const size_t need = (bytes + 255) & ~(size_t)255;
-  if (s.off + need > s.cap) {  // arena full: a synchronous copy is always safe
+  if (s.stage_off + need > s.stage_cap) {  // arena full: a synchronous copy is always safe
     HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st));
     HIP_CHECK(hipStreamSynchronize(st));
     return;
   }
-  uint8_t* slot = s.base + s.off;
-  s.off += need;
+  uint8_t* slot = s.stage + s.stage_off;
+  s.stage_off += need;
   std::memcpy(slot, src, bytes);
   HIP_CHECK(hipMemcpyAsync(dst, slot, bytes, hipMemcpyHostToDevice, st));
 }
@@ -233,11 +254,9 @@ void upload_bulk(void* dst, const void* src, size_t bytes, hipStream_t st) {
 // goes to a pinned mailbox (a pageable destination makes the runtime stage it), and the host
 // spins on an event instead of a stream synchronize that may put the thread to sleep.
 void spin_sync(hipStream_t st) {
-  static hipEvent_t ev = [] {
-    hipEvent_t e;
-    HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    return e;
-  }();
+  Lane& l = lane();
+  if (!l.spin) HIP_CHECK(hipEventCreateWithFlags(&l.spin, hipEventDisableTiming));
+  const hipEvent_t ev = l.spin;
   HIP_CHECK(hipEventRecord(ev, st));
   for (;;) {
     const hipError_t e = hipEventQuery(ev);
@@ -248,16 +267,15 @@ void spin_sync(hipStream_t st) {
 
 void fetch(void* dst, const void* src, size_t bytes, hipStream_t st) {
   if (!bytes) return;
-  static uint8_t* box = nullptr;
-  static size_t cap = 0;
-  if (bytes > cap) {  // no copy into it is pending: every fetch waits for its copy
-    if (box) HIP_CHECK(hipHostFree(box));
-    cap = std::max(bytes, (size_t)1 << 16);
-    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&box), cap, hipHostMallocDefault));
+  Lane& l = lane();
+  if (bytes > l.box_cap) {  // no copy into it is pending: every fetch waits for its copy
+    if (l.box) HIP_CHECK(hipHostFree(l.box));
+    l.box_cap = std::max(bytes, (size_t)1 << 16);
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&l.box), l.box_cap, hipHostMallocDefault));
   }
-  HIP_CHECK(hipMemcpyAsync(box, src, bytes, hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipMemcpyAsync(l.box, src, bytes, hipMemcpyDeviceToHost, st));
   spin_sync(st);
-  std::memcpy(dst, box, bytes);
+  std::memcpy(dst, l.box, bytes);
 }
 
 Twiddles& twiddles() {
@@ -272,6 +290,14 @@ int& api_lock_depth() {
 
 void Twiddles::ensure(int log_n) {
   if (log_n <= logmax) return;
+  static std::mutex mu;  // lanes may ask at once; an outgrown table stays allocated (another
+  std::lock_guard<std::mutex> lk(mu);  // lane's kernels may still read it)
+  if (log_n <= logmax) return;
+  if (fwd.p) {
+    static auto* old = new std::vector<DBuf<uint32_t>>();
+    old->push_back(std::move(fwd));
+    old->push_back(std::move(inv));
+  }
   size_t N = (size_t)1 << log_n;
   host_fwd.assign(N, 0);
   host_inv.assign(N, 0);
