@@ -10,6 +10,7 @@
 //  * FRI commit-phase fold: (1/2 + beta/2 g^-rev(i)) lo + (1/2 - beta/2 g^-rev(i)) hi
 //  * proof-of-work grind over the challenger state (smallest witness = normal form)
 #include "fri.h"
+#include "ntt_dev.h"
 
 #include "poseidon2.h"
 
@@ -87,14 +88,17 @@ __device__ __forceinline__ EF wave_sum(EF v) {
 // TAB = false: barycentric weights W_k,t = -x_t invd_k[t] over the low coset (mat = the LDE).
 // TAB = true: W_k,t = invd_k[t] read as a weight table (coefficient form: mat = a range of
 // coefficients, the table = powers of the point), logH/twf unused.
-template <int NP, bool TAB>
-__device__ __forceinline__ void open_tile(const uint32_t* __restrict__ mat, size_t height, int w,
-                                          size_t n, int logH, const EF* __restrict__ invd_a,
-                                          const EF* __restrict__ invd_b,
-                                          const uint32_t* __restrict__ twf,
-                                          EF* __restrict__ partial, unsigned chunk) {
+// FULL: every thread of the chunk has all OPEN_R rows (every chunk of a matrix of >= OPEN_CH
+// low-coset rows): no per-row bounds selects.  Column words come through a buffer descriptor per
+// column with the row step in the scalar offset (no 64-bit VALU address arithmetic per load).
+template <int NP, bool TAB, bool FULL>
+__device__ __forceinline__ void open_tile_body(const uint32_t* __restrict__ mat, size_t height, int w,
+                                               size_t n, int logH, const EF* __restrict__ invd_a,
+                                               const EF* __restrict__ invd_b,
+                                               const uint32_t* __restrict__ twf,
+                                               EF* __restrict__ partial, unsigned chunk) {
   const size_t c0 = (size_t)chunk * OPEN_CH + threadIdx.x;
-  const int nr = c0 >= n ? 0 : (int)min((size_t)OPEN_R, (n - c0 + OPEN_T - 1) / OPEN_T);
+  const int nr = FULL ? OPEN_R : c0 >= n ? 0 : (int)min((size_t)OPEN_R, (n - c0 + OPEN_T - 1) / OPEN_T);
   EF W[NP][OPEN_R];
 #pragma unroll
   for (int r = 0; r < OPEN_R; r++) {
@@ -116,9 +120,15 @@ __device__ __forceinline__ void open_tile(const uint32_t* __restrict__ mat, size
     }
   }
   auto load = [&](int c, uint32_t (&v)[OPEN_R]) {
-    const uint32_t* col = mat + (size_t)c * height + c0;
+    if constexpr (FULL) {
+      const __amdgpu_buffer_rsrc_t rc = rsrc_of(mat + (size_t)c * height + (size_t)chunk * OPEN_CH);
 #pragma unroll
-    for (int r = 0; r < OPEN_R; r++) v[r] = r < nr ? ld_global(col, (size_t)r * OPEN_T) : 0u;
+      for (int r = 0; r < OPEN_R; r++) v[r] = ld_b(rc, threadIdx.x * 4u, (uint32_t)(r * OPEN_T) * 4u);
+    } else {
+      const uint32_t* col = mat + (size_t)c * height + c0;
+#pragma unroll
+      for (int r = 0; r < OPEN_R; r++) v[r] = r < nr ? ld_global(col, (size_t)r * OPEN_T) : 0u;
+    }
   };
   // four column buffers in a ring: three columns stay in flight while one is consumed
   uint32_t vr[4][OPEN_R];
@@ -165,6 +175,18 @@ __device__ __forceinline__ void open_tile(const uint32_t* __restrict__ mat, size
     }
     __syncthreads();
   }
+}
+
+template <int NP, bool TAB>
+__device__ __forceinline__ void open_tile(const uint32_t* __restrict__ mat, size_t height, int w,
+                                          size_t n, int logH, const EF* __restrict__ invd_a,
+                                          const EF* __restrict__ invd_b,
+                                          const uint32_t* __restrict__ twf,
+                                          EF* __restrict__ partial, unsigned chunk) {
+  if ((size_t)(chunk + 1) * OPEN_CH <= n)  // uniform across the block
+    open_tile_body<NP, TAB, true>(mat, height, w, n, logH, invd_a, invd_b, twf, partial, chunk);
+  else
+    open_tile_body<NP, TAB, false>(mat, height, w, n, logH, invd_a, invd_b, twf, partial, chunk);
 }
 
 template <int NP, bool TAB = false>

@@ -17,12 +17,6 @@
 #include <mutex>
 #include <cstring>
 
-#ifndef BFZ_DIF_DIN
-#define BFZ_DIF_DIN 0
-#endif
-#ifndef BFZ_MID_PF
-#define BFZ_MID_PF 0
-#endif
 
 namespace bfz {
 
@@ -192,8 +186,12 @@ __global__ __launch_bounds__(1 << (B - 4)) void k_ntt_tile(const uint32_t* __res
   static_assert(!DIN || !DIF, "direct first window: DIT passes only");
   static_assert(!WS || B >= 13, "wave-local windows: 2^13 / 2^14 tiles");
   constexpr int R = 4, E = 1 << R, T = 1 << (B - R), NW = (B + R - 1) / R;
-  // WS DIF: the first window (g0 = B - 4) holds elements tid + i T, a coalesced HBM order
-  constexpr bool DIFIN = DIF && WS && BFZ_DIF_DIN;
+  // WS DIF: the first window (g0 = B - 4) holds elements tid + i T, a coalesced HBM order, so
+  // it is read straight from HBM (no LDS staging, one block barrier fewer), and the last window
+  // leaves each wave its own 1024 consecutive outputs, which the wave stores itself: one block
+  // barrier per DIF tile (DIF pass 162 -> 153-156 us per 2^26 elements, profiles/r05/
+  // ab_ntt_variants.txt; in round 2, before the wave-local windows, direct reads measured +4.5%)
+  constexpr bool DIFIN = DIF && WS;
   extern __shared__ uint32_t lds[];
   const int tid = threadIdx.x;
   const int tpad = tid + (tid >> R);
@@ -290,7 +288,20 @@ __global__ __launch_bounds__(1 << (B - 4)) void k_ntt_tile(const uint32_t* __res
       for (int i = 0; i < E; i++) lds[pb + (i << g0) + ((i << g0) >> R)] = x[i];
     }
   }
-  if constexpr (DIF) {
+  if constexpr (DIFIN) {
+    // the last window (g0 = 0) left each wave's own 1024 consecutive elements in its own LDS
+    // region: the wave stores them itself, 64 consecutive words per instruction (no block barrier)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const __amdgpu_buffer_rsrc_t rd = rsrc_of(D);
+    const uint32_t e0 = (uint32_t)(tid >> 6) * 1024u + (tid & 63);
+#pragma unroll
+    for (int j = 0; j < E; j++) {
+      const uint32_t e = e0 + 64u * j;
+      st_b(rd, e0 * 4u, 256u * j, lds[e + (e >> R)]);
+    }
+  } else if constexpr (DIF) {
     __syncthreads();
     const __amdgpu_buffer_rsrc_t rd = rsrc_of(D);
 #pragma unroll
@@ -385,11 +396,6 @@ __global__ __launch_bounds__(1 << (MidPlan<L>::b2 + MidPlan<L>::c2 - 4)) void k_
       if (half && nwin > 1) __syncthreads();  // the lo half's last LDS reads are done
       uint32_t* Dh = D + (size_t)half * n;
       int done_hi = b;
-#if BFZ_MID_PF
-      uint32_t pre[2][15];
-      load_window_tw_s<4>(pre[0], max(b - 4, 0), 0, min(4, b - max(b - 4, 0)), s0,
-                          rest & ((1 << max(b - 4, 0)) - 1), lo_g, tw_fwd);
-#endif
 #pragma unroll
       for (int w = 0; w < nwin; w++) {  // DFT of this half
         const int gg = max(b - 4 - 4 * w, 0);
@@ -403,16 +409,7 @@ __global__ __launch_bounds__(1 << (MidPlan<L>::b2 + MidPlan<L>::c2 - 4)) void k_
         }
         const int kk_hi = min(4, done_hi - gg);
         done_hi = gg;
-#if BFZ_MID_PF
-        if (w + 1 < nwin) {
-          const int g1 = max(b - 8 - 4 * w, 0);
-          load_window_tw_s<4>(pre[(w + 1) & 1], g1, 0, min(4, gg - g1), s0, rest & ((1 << g1) - 1),
-                              lo_g, tw_fwd);
-        }
-        r16_window<true, false, true, 4, true>(x, gg, 0, kk_hi, s0, m_low, lo_g, tw_fwd, pre[w & 1]);
-#else
         r16_window<true, false, true>(x, gg, 0, kk_hi, s0, m_low, lo_g, tw_fwd);
-#endif
         if (w == nwin - 1) {
           const __amdgpu_buffer_rsrc_t rd = rsrc_of(Dh);
           const uint32_t off = ((mb << s0) + lo) * 4u;
