@@ -16,13 +16,18 @@
 //                to bfz_cycles_push as soon as it is written, so the DMA of chunk k runs while
 //                chunk k+1 is converted; bfz_cycles_finish returns the record
 #include <immintrin.h>
+#include <pthread.h>
+#include <sched.h>
 
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstddef>
 #include <cstdint>
+#include <fstream>
 #include <functional>
+#include <sstream>
+#include <string>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -54,11 +59,52 @@ inline bfz_cycle cycle_of(const RsCpuEvent& e) {  // lib.rs CycleArrays::new's c
   return c;
 }
 
-// A fixed pool of workers (the caller's thread is worker 0), like rayon's global pool.
+// The CPUs of the caller's NUMA node that this process may run on (empty if unknown): the
+// events were written by the executor's thread, so they sit in that node's memory, and on a
+// two-socket host a worker on the other socket reads them at a fraction of the local rate.
+std::vector<int> node_cpus() {
+  cpu_set_t aff;
+  if (sched_getaffinity(0, sizeof aff, &aff)) return {};
+  const int me = sched_getcpu();
+  for (int node = 0; node < 64; node++) {
+    std::ifstream f("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");
+    if (!f) continue;
+    std::string list;
+    std::getline(f, list);
+    std::vector<int> cpus;
+    std::stringstream ss(list);
+    std::string part;
+    bool mine = false;
+    while (std::getline(ss, part, ',')) {
+      const size_t dash = part.find('-');
+      const int a = std::stoi(part.substr(0, dash));
+      const int b = dash == std::string::npos ? a : std::stoi(part.substr(dash + 1));
+      for (int c = a; c <= b; c++) {
+        if (c == me) mine = true;
+        if (c < CPU_SETSIZE && CPU_ISSET(c, &aff)) cpus.push_back(c);
+      }
+    }
+    if (mine) return cpus;
+  }
+  return {};
+}
+
+// A fixed pool of workers (the caller's thread is worker 0), like rayon's global pool; the
+// workers are pinned to CPUs of the caller's NUMA node when the host tells us which those are
+// (rayon: ThreadPoolBuilder::spawn_handler can do the same).
 class Pool {
  public:
   explicit Pool(int n) : n_(n) {
-    for (int i = 1; i < n; i++) th_.emplace_back([this, i] { loop(i); });
+    const std::vector<int> cpus = node_cpus();
+    for (int i = 1; i < n; i++) {
+      th_.emplace_back([this, i] { loop(i); });
+      if ((int)cpus.size() >= n) {
+        cpu_set_t one;
+        CPU_ZERO(&one);
+        CPU_SET(cpus[(size_t)i % cpus.size()], &one);
+        (void)pthread_setaffinity_np(th_.back().native_handle(), sizeof one, &one);
+      }
+    }
   }
   int size() const { return n_; }
   void run(const std::function<void(int)>& f) {

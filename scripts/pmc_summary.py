@@ -37,10 +37,23 @@ def per_kernel(rows):
     return agg
 
 
+def durations(root):
+    """{kernel: (launches, mean us, max us)} from the kernel traces the --pmc passes wrote beside
+    their counters (outliers must show up in review, not be averaged away)."""
+    d = collections.defaultdict(list)
+    for f in glob.glob(os.path.join(root, "pmc_*", "**", "*kernel_trace*.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            key = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
+            d[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    return {k: (len(v), sum(v) / len(v), max(v)) for k, v in d.items()}
+
+
 def main(root):
     fetch = per_kernel(load(root, "FETCH_SIZE"))
     write = per_kernel(load(root, "WRITE_SIZE"))
-    out = {"unit": "kB per launch (rocprofv3 FETCH_SIZE / WRITE_SIZE)", "kernels": {}}
+    dur = durations(root)
+    out = {"unit": "kB per launch (rocprofv3 FETCH_SIZE / WRITE_SIZE); durations in us from the same "
+                   "passes' kernel traces (counter passes run slower than plain runs)", "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
         f, w = fetch.get(k), write.get(k)
         n = max((f or w)["launches"], 1)
@@ -53,6 +66,9 @@ def main(root):
             e["algorithmic_kB"] = round(per_elem * elems / 1024, 1)
             e["traffic_kB_fetch_x2_plus_write"] = round(2 * e["fetch_kB"] + e["write_kB"], 1)
             e["traffic_kB_raw"] = round(e["fetch_kB"] + e["write_kB"], 1)
+        if k in dur:
+            e["duration_us_mean"] = round(dur[k][1], 2)
+            e["duration_us_max"] = round(dur[k][2], 2)
         out["kernels"][k] = e
     print(json.dumps(out, indent=1))
 
