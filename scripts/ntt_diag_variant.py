@@ -8,6 +8,9 @@ wrong by construction: they exist to time one ingredient of the NTT kernels.
   noexch   the 2^14 / small tile passes skip the LDS exchanges between windows (every window
            works on the registers the previous one left): compute + HBM only
   reps0    the tile passes do no butterflies at all: HBM -> (LDS) -> HBM data movement only
+  syncmalloc  the device pool waits for the GPU to go idle before every hipMalloc: tests whether
+           the first proof's long launches (kernel_outliers.py) are stalls caused by the pool
+           growing while kernels run
 
 usage: python3 scripts/ntt_diag_variant.py <name> [<name> ...]
 Then run a program against it with LD_LIBRARY_PATH=zkvm-brainfuck_amd/variants/<name>
@@ -42,6 +45,10 @@ PATCHES = {
          "    if (!DIN && w == 0) {\n      if (WS && w > 0"),
         ("ntt.hip", "    } else {\n#pragma unroll\n      for (int i = 0; i < E; i++) lds[pb + (i << g0) + ((i << g0) >> R)] = x[i];",
          "    } else if (w == NW - 1) {\n#pragma unroll\n      for (int i = 0; i < E; i++) lds[pb + (i << g0) + ((i << g0) >> R)] = x[i];"),
+    ],
+    "syncmalloc": [
+        ("gpu.h", "    void* p = nullptr;\n    HIP_CHECK(hipMalloc(&p, bytes));",
+         "    void* p = nullptr;\n    HIP_CHECK(hipDeviceSynchronize());\n    HIP_CHECK(hipMalloc(&p, bytes));"),
     ],
     "reps0": [
         ("ntt.hip", "    if (g0 == 0)\n      r16_window<DIF, true, false, R>",
