@@ -336,7 +336,7 @@ void bfz_host_free(void* p);
  * place when the callback returns): ncclAllGather / ncclAllReduce run on them directly. */
 typedef int (*bfz_allgather_fn)(void* ctx, const void* send, size_t bytes, void* recv);
 typedef int (*bfz_allreduce_u32_fn)(void* ctx, uint32_t* data, size_t n);
-/* `count` proofs of one record back to back with `inflight` (1 or 2) of them in flight, each on
+/* `count` proofs of one record back to back with `inflight` (1..4) of them in flight, each on
  * its own stream, pool and pinned mailboxes ("lane", one host thread each): one proof's
  * latency-bound launches (Merkle tree tops, the FRI tail, the transcript steps) then run beside
  * the other's bulk hashing.  Every proof must be byte-identical to the first (an error

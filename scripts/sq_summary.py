@@ -25,7 +25,7 @@ def main(root):
     print("# wait_any = parked at s_waitcnt/barrier; wait_inst = ready but not issued; "
           "active = issuing; valu = issuing VALU")
     print(f"{'kernel':60s} {'wait_any':>8s} {'wait_inst':>9s} {'active':>7s} {'valu':>6s}")
-    for name, c in rows[:16]:
+    for name, c in rows[:28]:
         w = c["SQ_WAVE_CYCLES"] or 1.0
         print(f"{name[:60]:60s} {c['SQ_WAIT_ANY'] / w:8.2f} {c['SQ_WAIT_INST_ANY'] / w:9.2f} "
               f"{c['SQ_ACTIVE_INST_ANY'] / w:7.2f} {c['SQ_ACTIVE_INST_VALU'] / w:6.2f}")

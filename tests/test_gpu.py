@@ -245,7 +245,7 @@ def test_record_prove_repeat_two_lanes_matches_oracle(client):
     drec = events.record_from_events(pk, rec)
     want = O.prove(prog, stdin)
     L = _lib.lib()
-    for inflight, count in ((1, 3), (2, 7)):
+    for inflight, count in ((1, 3), (2, 7), (4, 9)):
         ptr = ctypes.POINTER(ctypes.c_uint8)()
         n = ctypes.c_size_t()
         wall = ctypes.c_double()
@@ -256,7 +256,7 @@ def test_record_prove_repeat_two_lanes_matches_oracle(client):
         assert wall.value > 0
     with pytest.raises(_lib.BfzError, match="inflight"):
         _lib.check(L.bfz_record_prove_repeat(ctypes.c_void_p(pk.handle), ctypes.c_void_p(drec.handle),
-                                             2, 3, ctypes.byref(ptr), ctypes.byref(n), None))
+                                             2, 5, ctypes.byref(ptr), ctypes.byref(n), None))
     assert _prove_record(pk, drec) == want
 
 

@@ -645,9 +645,9 @@ int bfz_prove_batch(const bfz_pk* pk, const uint8_t* const* stdins, const size_t
     }
     if (E < 1 || E > 64) throw std::runtime_error("exec_threads must be in 1..64");
     bfz::BatchStats bs;
-    static const int inflight = [] {  // proofs in flight (lanes); BFZ_INFLIGHT = 1 for one
+    static const int inflight = [] {  // proofs in flight (lanes); BFZ_INFLIGHT = 1..MAX_LANES
       const char* e = std::getenv("BFZ_INFLIGHT");
-      return e && *e == '1' ? 1 : bfz::MAX_LANES;
+      return e && *e >= '1' && *e <= '0' + bfz::MAX_LANES ? *e - '0' : bfz::DEFAULT_INFLIGHT;
     }();
     auto v = bfz::prove_batch(*pk->pk, jobs, opts(), E, inflight, &bs);
     emit_all(v, proofs, proof_lens, (size_t)-1);

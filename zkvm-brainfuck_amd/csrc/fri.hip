@@ -78,7 +78,8 @@ __device__ __forceinline__ EF wave_sum(EF v) {
 }
 
 // Barycentric opening of one matrix at one or two points (NP):
-// partial[(chunk * w + c) * NP + k] = sum_{t in chunk} W_k,t col_c[t],  W_k,t = -x_t invd_k[t].
+// partial[(chunk * w + c) * NP + k] = sum_{t in chunk} W_k,t col_c[t],  W_k,t = x_t invd_k[t]
+// (the barycentric weight is -x_t invd_k[t]: k_open_final_batch negates the scale instead).
 // A thread owns OPEN_R rows and keeps their weights for both points in registers, so every
 // matrix element is read once for both points.  Four column buffers form a ring (three columns
 // in flight while one is consumed).  Each thread's reduced partial of a column goes to LDS and
@@ -116,7 +117,8 @@ __device__ __forceinline__ void open_tile_body(const uint32_t* __restrict__ mat,
       // w_n^-1 into scale_b), so the zeta table serves both points
       const size_t tk = k && !invd_b ? prev2_pos(t, logH) : t;
       const EF* tab = k && invd_b ? invd_b : invd_a;
-      W[k][r] = r < nr ? ef_neg(ef_mul_base(ld_global(tab, tk), x)) : ef_zero();
+      // + x_t invd: the minus sign of W is applied once per column, to the scale (k_open_final_batch)
+      W[k][r] = r < nr ? ef_mul_base(ld_global(tab, tk), x) : ef_zero();
     }
   }
   auto load = [&](int c, uint32_t (&v)[OPEN_R]) {
@@ -260,8 +262,9 @@ __global__ __launch_bounds__(256) void k_open_final_batch(const OpenDesc* __rest
     sa = ef_mul_base(ef_sub(zn, ef_base(o.z3n)), o.zc);
     sb = ef_mul_base(sa, o.zb);
   }
-  open_final<NP>(partial + o.part_off, (int)o.nchunks, o.w, (int)(blockIdx.x - o.col0), sa, sb,
-                 o.out_a, o.out_b);
+  // the partial sums are of x_t invd_k[t] col[t]: the weight's sign goes into the scale
+  open_final<NP>(partial + o.part_off, (int)o.nchunks, o.w, (int)(blockIdx.x - o.col0), ef_neg(sa),
+                 ef_neg(sb), o.out_a, o.out_b);
 }
 
 // ------------------------------------------------------------------ reduced openings

@@ -96,7 +96,8 @@ class DevicePool {
 // mailboxes.  The process has a default lane; bfz_prove_batch and bfz_record_prove_repeat keep
 // two proofs in flight on two lanes (one host thread each), so the latency-bound launches of one
 // proof (tree tops, the FRI tail, transcript steps) run beside the other's bulk kernels.
-constexpr int MAX_LANES = 2;
+constexpr int MAX_LANES = 4;
+constexpr int DEFAULT_INFLIGHT = 2;  // proofs in flight in bfz_prove_batch (profiles/r05)
 struct Lane {
   int id = 0;
   hipStream_t stream = nullptr;
