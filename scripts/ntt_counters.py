@@ -31,9 +31,9 @@ def kernel_key(name):
 
 
 def family(key):
-    if key.startswith("k_ntt_tile<false,14") or key.startswith("k_tile14_mfma<false"):
+    if key.startswith("k_ntt_tile<false,14"):
         return "dit_tile", 14.0 * N * W, 8.0 * N * W
-    if key.startswith("k_ntt_tile<true,14") or key.startswith("k_tile14_mfma<true"):
+    if key.startswith("k_ntt_tile<true,14"):
         return "dif_tile", 28.0 * N * W, 16.0 * N * W
     if key.startswith(f"k_lde_mid<{L}>"):
         return "lde_mid", 3.0 * (L - 14) * N * W, 12.0 * N * W

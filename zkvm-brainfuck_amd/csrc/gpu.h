@@ -14,6 +14,7 @@
 #include <functional>
 #include <atomic>
 #include <map>
+#include <mutex>
 #include <unordered_map>
 #include <stdexcept>
 #include <string>
@@ -54,7 +55,9 @@ __device__ __forceinline__ uint32_t dbitrev(uint32_t x, int bits) {
 // proof no hipMalloc/hipFree happens inside the timed region.
 class DevicePool {
  public:
+  // (locked: a buffer may be released from another lane's thread than the one that allocated it)
   void* alloc(size_t bytes) {
+    std::lock_guard<std::mutex> lk(mu_);
     bytes = (bytes + 255) & ~(size_t)255;
     if (bytes == 0) bytes = 256;
     auto it = free_.find(bytes);
@@ -70,11 +73,13 @@ class DevicePool {
   }
   void release(void* p) {
     if (!p) return;
+    std::lock_guard<std::mutex> lk(mu_);
     auto it = size_of_.find(p);
     if (it == size_of_.end()) return;
     free_[it->second].push_back(p);
   }
   void trim() {
+    std::lock_guard<std::mutex> lk(mu_);
     for (auto& kv : free_)
       for (void* p : kv.second) {
         (void)hipFree(p);
@@ -89,6 +94,7 @@ class DevicePool {
   // end of a proof sit between the last kernel of one proof and the first of the next
   std::unordered_map<size_t, std::vector<void*>> free_;
   std::unordered_map<void*, size_t> size_of_;
+  std::mutex mu_;
 };
 
 // A proof lane: the device context one proof runs in -- its stream, the stream-ordered buffer
