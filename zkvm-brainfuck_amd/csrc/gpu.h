@@ -187,7 +187,6 @@ struct DevMatrix {
 struct Twiddles {
   std::atomic<int> logmax{0};
   DBuf<uint32_t> fwd, inv;
-  std::vector<uint32_t> host_fwd, host_inv;
   void ensure(int log_n);
 };
 Twiddles& twiddles();

@@ -259,4 +259,20 @@ __device__ __forceinline__ EF ld_global(const EF* p, size_t i) {
   return EF{{u.x, u.y, u.z, u.w}};
 }
 
+// Buffer loads / stores through a descriptor built from a wave-uniform base: the per-thread
+// part of an address is the 32-bit voffset and the uniform part (column, stage, element index)
+// the scalar soffset, so an access costs no VALU address arithmetic and no VGPR pair (a flat
+// global access with an offset beyond the 12-bit immediate costs two half-rate 64-bit adds per
+// load).  Offsets stay below 2 GiB of the base.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), /*stride*/ 0, /*bytes*/ 0x7fffffff,
+                                           0x00020000);
+}
+__device__ __forceinline__ uint32_t ld_b(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0);
+}
+__device__ __forceinline__ void st_b(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, uint32_t v) {
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)voff, (int)soff, 0);
+}
+
 }  // namespace kb

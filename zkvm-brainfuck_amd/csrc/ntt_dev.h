@@ -15,20 +15,6 @@ using namespace kb;
 // through LDS.  The first window loads straight from HBM and the last stores straight
 // back, so a pass is one read + one write of the data.
 
-// Buffer loads / stores through a descriptor built from a wave-uniform base: the per-thread
-// part of an address is the 32-bit voffset and the compile-time part (stage, l, i) the scalar
-// soffset, so a twiddle or data access costs no VALU address arithmetic (a flat global access
-// with an offset beyond the 12-bit immediate costs two half-rate 64-bit adds per load).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), /*stride*/ 0, /*bytes*/ 0x7fffffff,
-                                           0x00020000);
-}
-__device__ __forceinline__ uint32_t ld_b(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0);
-}
-__device__ __forceinline__ void st_b(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, uint32_t v) {
-  __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)voff, (int)soff, 0);
-}
 
 constexpr uint32_t G24 = cpow(3, 127);
 constexpr uint32_t root_pow2(int k) {  // w_(2^k), canonical

@@ -11,6 +11,8 @@
 // A device slot is refilled only after the proof that read it has finished generating its
 // traces (an event recorded on the prover stream right after tracegen).
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <condition_variable>
 #include <cstring>
 #include <exception>
@@ -23,6 +25,18 @@
 namespace bfz {
 
 namespace {
+
+// BFZ_HOST_TRACE=live: every step of every job on stderr as it happens (where a stalled batch
+// stands: executor, uploader or a proof lane).
+void btrace(const char* what, size_t j) {
+  static const bool on = [] {
+    const char* e = std::getenv("BFZ_HOST_TRACE");
+    return e && std::strcmp(e, "live") == 0;
+  }();
+  if (!on) return;
+  std::fprintf(stderr, "batch job %zu: %s (lane %d)\n", j, what, lane().id);
+  std::fflush(stderr);
+}
 
 double ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -151,8 +165,10 @@ std::vector<std::vector<uint8_t>> prove_batch(const ProvingKey& pk, const std::v
           h = free_h.back();
           free_h.pop_back();
         }
+        btrace("execute", j);
         const auto t0 = std::chrono::steady_clock::now();
         execute_into(pk.program, jobs[j].stdin_data, jobs[j].nin, *h);
+        btrace("executed", j);
         exec_ms[j] = ms_since(t0);
         std::lock_guard<std::mutex> lk(mu);
         executed[j] = h;
@@ -176,7 +192,9 @@ std::vector<std::vector<uint8_t>> prove_batch(const ProvingKey& pk, const std::v
           h = executed[j];
         }
         EventSlot& s = sl[j % NSLOT];
+        btrace("upload: slot free?", j);
         HIP_CHECK(hipEventSynchronize(s.consumed));  // job j - NSLOT has read this slot
+        btrace("upload", j);
         const auto t0 = std::chrono::steady_clock::now();
         copy_arr(s, 0, h->cpu, cs);
         copy_arr(s, 1, h->alu, cs);
@@ -187,6 +205,7 @@ std::vector<std::vector<uint8_t>> prove_batch(const ProvingKey& pk, const std::v
         HIP_CHECK(hipEventRecord(s.uploaded, cs));
         HIP_CHECK(hipEventSynchronize(s.uploaded));
         up_ms[j] = ms_since(t0);
+        btrace("uploaded", j);
         std::lock_guard<std::mutex> lk(mu);
         uploaded[j] = 1;
         cv.notify_all();
@@ -214,6 +233,7 @@ std::vector<std::vector<uint8_t>> prove_batch(const ProvingKey& pk, const std::v
         if (abort) return;
         h = executed[j];
       }
+      btrace("prove", j);
       const auto t0 = std::chrono::steady_clock::now();
       EventSlot& s = sl[j % NSLOT];
       DeviceEvents ev;
@@ -234,6 +254,7 @@ std::vector<std::vector<uint8_t>> prove_batch(const ProvingKey& pk, const std::v
       DeviceTraces dt;
       generate_traces_device(ev, dt, stream());
       HIP_CHECK(hipEventRecord(s.consumed, stream()));
+      btrace("traces queued", j);
       {
         std::lock_guard<std::mutex> lk(mu);
         consumed[j] = 1;
@@ -241,6 +262,7 @@ std::vector<std::vector<uint8_t>> prove_batch(const ProvingKey& pk, const std::v
       }
       auto pf = prove_device(pk, dt, opt, nullptr);
       const double ms = ms_since(t0);
+      btrace("proved", j);
       std::lock_guard<std::mutex> lk(mu);
       proofs[j] = std::move(pf);
       prove_ms += ms;

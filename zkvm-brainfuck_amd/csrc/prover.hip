@@ -109,19 +109,30 @@ namespace {
 // proof, printed on stderr at exit -- splits the GPU's idle gaps into host work and launch
 // latency (scripts/hostgap.py).  The marks are kept in memory: an fprintf per mark cost tens
 // of microseconds on the GPU boxes and doubled the idle time it was measuring.
+// BFZ_HOST_TRACE=live: each mark is printed at once with its lane (where a stalled proof lane
+// stands).
 struct HostTrace {
   bool on = std::getenv("BFZ_HOST_TRACE") != nullptr;
+  bool live = on && std::string(std::getenv("BFZ_HOST_TRACE")) == "live";
   struct Mark {
     std::chrono::steady_clock::time_point t;
     const char* what;  // string literals only
     bool reset;
   };
   std::vector<Mark> marks;
+  std::mutex mu;  // the proof lanes mark concurrently
   HostTrace() {
     if (on) marks.reserve(1 << 16);
   }
   void mark(const char* what, bool reset = false) {
-    if (!on || marks.size() >= (1u << 20)) return;
+    if (!on) return;
+    std::lock_guard<std::mutex> lk(mu);
+    if (live) {
+      std::fprintf(stderr, "host lane %d: %s\n", lane().id, what);
+      std::fflush(stderr);
+      return;
+    }
+    if (marks.size() >= (1u << 20)) return;
     marks.push_back({std::chrono::steady_clock::now(), what, reset});
   }
   ~HostTrace() {
@@ -439,15 +450,20 @@ struct ProofScope {
   hipEvent_t e_total = nullptr;
   ProofScope(bool timing, StageTimes* times) : tms(times ? times : &local) {
     ev.on = timing && times;
+    if (!ev.on) {  // the probes are process-global: only a timed (single-lane) proof arms them
+      for (KernelProbe* p : {&ntt_probe(), &p2_probe(), &open_probe(), &reduce_probe()})
+        if (p->on) p->on = false;  // (left armed by a timed proof that failed)
+      return;
+    }
     ntt_probe().reset();
-    ntt_probe().on = ev.on;
+    ntt_probe().on = true;
     p2_probe().reset();
-    p2_probe().on = ev.on;
+    p2_probe().on = true;
     open_probe().reset();
-    open_probe().on = ev.on;
+    open_probe().on = true;
     reduce_probe().reset();
-    reduce_probe().on = ev.on;
-    if (ev.on) e_total = ev.begin(stream());
+    reduce_probe().on = true;
+    e_total = ev.begin(stream());
   }
   void finish() {  // collects every event of the call into *tms
     if (!ev.on) return;
@@ -506,6 +522,7 @@ void commit_main_impl(MainData& md, ProofScope& ps, bool fetch_root = true) {
     md.chip[k] = dt.chips[md.order[k]];
     md.hn[k] = dt.heights[md.order[k]];
   }
+  htrace().mark("main commit");
   hipEvent_t e0 = ps.ev.on ? ps.ev.begin(st) : nullptr;
   Span span("commit to main traces");  // (no span of its own in the reference: commit_main)
   const Plan plan = make_plan();
@@ -518,7 +535,9 @@ void commit_main_impl(MainData& md, ProofScope& ps, bool fetch_root = true) {
     if (ps.tms) ps.tms->main_cells += (double)md.hn[k] * CHIP_INFO[md.chip[k]].main_w;
   }
   hipEvent_t eh = ps.ev.on ? ps.ev.begin(st) : nullptr;
+  htrace().mark("main LDE queued");
   md.mainr.commit(st, fetch_root);
+  htrace().mark("main tree queued");
   if (ps.ev.on) ps.ev.end(eh, st, &ps.tms->main_hash);
   md.root_on_host = fetch_root;
   if (ps.ev.on) ps.ev.end(e0, st, &ps.tms->main_commit);

@@ -293,31 +293,35 @@ void Twiddles::ensure(int log_n) {
   static std::mutex mu;  // lanes may ask at once; an outgrown table stays allocated (another
   std::lock_guard<std::mutex> lk(mu);  // lane's kernels may still read it)
   if (log_n <= logmax) return;
-  if (fwd.p) {
-    static auto* old = new std::vector<DBuf<uint32_t>>();
-    old->push_back(std::move(fwd));
-    old->push_back(std::move(inv));
-  }
-  size_t N = (size_t)1 << log_n;
-  host_fwd.assign(N, 0);
-  host_inv.assign(N, 0);
+  const size_t N = (size_t)1 << log_n;
+  std::vector<uint32_t> hf(N, 0), hi(N, 0);
   for (int k = 0; k < log_n; k++) {
     size_t h = (size_t)1 << k;
     uint32_t w = kb::two_adic_gen(k + 1), wi = kb::minv(w);
     uint32_t a = kb::ONE, b = kb::ONE;
     for (size_t j = 0; j < h; j++) {
-      host_fwd[h + j] = a;
-      host_inv[h + j] = b;
+      hf[h + j] = a;
+      hi[h + j] = b;
       a = kb::mmul(a, w);
       b = kb::mmul(b, wi);
     }
   }
-  // stream-ordered: pooled buffers may still be read by kernels queued on stream()
-  fwd.reset(N);
-  inv.reset(N);
-  HIP_CHECK(hipMemcpyAsync(fwd.p, host_fwd.data(), N * 4, hipMemcpyHostToDevice, stream()));
-  HIP_CHECK(hipMemcpyAsync(inv.p, host_inv.data(), N * 4, hipMemcpyHostToDevice, stream()));
+  // The new tables are filled before they are published: another lane reads fwd.p / inv.p
+  // without the lock, so each pointer goes from the old table straight to the filled new one
+  // (one store, never null) and the old tables stay allocated -- kernels queued before the swap
+  // still read them, and they are a prefix of the new ones.
+  DBuf<uint32_t> nf(N), ni(N);  // stream-ordered: pooled buffers may be read by queued kernels
+  HIP_CHECK(hipMemcpyAsync(nf.p, hf.data(), N * 4, hipMemcpyHostToDevice, stream()));
+  HIP_CHECK(hipMemcpyAsync(ni.p, hi.data(), N * 4, hipMemcpyHostToDevice, stream()));
   HIP_CHECK(hipStreamSynchronize(stream()));
+  std::swap(fwd.p, nf.p);
+  std::swap(inv.p, ni.p);
+  std::swap(fwd.from, nf.from);
+  std::swap(inv.from, ni.from);
+  fwd.n = inv.n = N;
+  static auto* old = new std::vector<DBuf<uint32_t>>();  // outgrown tables (empty on first use)
+  old->push_back(std::move(nf));
+  old->push_back(std::move(ni));
   logmax = log_n;
 }
 
