@@ -34,7 +34,7 @@ VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 # Full-rate-equivalent VALU lane-ops of one Poseidon2 permutation in k_permute_batch
 # (gfx950 ISA instruction mix, profiles/r02/poseidon2_isa_mix.txt).
 P2_UNITS_PER_PERM = 5133
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r04", "profile_round_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05", "profile_round_pmc_summary.json")
 
 
 # VALU units (full-rate lane-ops) per radix-2 element-stage of a 2^22 coset LDE, from the gfx950
@@ -43,7 +43,7 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "r04", "profile_round_pmc_summary.j
 NTT_UNITS_PER_ELEM_STAGE = 7.023
 # Dynamic counters of the same kernels at a known element-stage count (scripts/gpu_ntt_counters.sh
 # -> scripts/ntt_counters.py): SQ_INSTS_VALU x 64 per element-stage, SQ wave-state fractions.
-NTT_COUNTERS = os.path.join(ROOT, "profiles", "r04", "ntt_counters.json")
+NTT_COUNTERS = os.path.join(ROOT, "profiles", "r05", "ntt_counters.json")
 # element-stage shares of a 2^22 coset LDE: DIT tile 14, k_lde_mid<22> 3 x 8, DIF tile 2 x 14 (of 66)
 NTT_FAMILY_SHARE = {"dit_tile": 14 / 66, "lde_mid": 24 / 66, "dif_tile": 28 / 66}
 
@@ -85,7 +85,7 @@ def ntt_roofline(tm):
             "traffic": round(traffic) if traffic else None,
             "algorithmic_per_launch": round(alg_per_launch),
             "traffic_over_algorithmic": round(traffic / alg_per_launch, 3) if traffic else None,
-            "traffic_source": "profiles/r04/profile_round_pmc_summary.json (FETCH_SIZE x2 + WRITE_SIZE per "
+            "traffic_source": "profiles/r05/profile_round_pmc_summary.json (FETCH_SIZE x2 + WRITE_SIZE per "
                               "launch, scaled to this proof's launches)",
             "basis": "SURVEY 8(d): 12*n*w B per coset LDE (read n, write 2n) / NTT kernel time",
             "kernel": "coset LDE = k_ntt_tile<false,14> (iDFT stages 0-13) + k_lde_mid<L> (iDFT "
@@ -102,7 +102,7 @@ def ntt_roofline(tm):
 
 def ntt_valu(tm):
     """VALU issue of the same NTT kernels FROM COUNTERS: the measured VALU
-    wave-instructions per element-stage of each kernel (profiles/r04/ntt_counters.json, rocprofv3
+    wave-instructions per element-stage of each kernel (profiles/r05/ntt_counters.json, rocprofv3
     SQ_INSTS_VALU at a known element-stage count), weighted by its share of a 2^22 coset LDE, x the
     proof's element-stages / NTT kernel time = lane-instructions/s, against the 78.6 T lane-ops/s
     issue peak.  frac_units weights the instructions by the ISA's half-rate share (units per
@@ -134,7 +134,7 @@ def ntt_valu(tm):
             "frac_units": round(frac * units_per_instr, 4),
             "units_per_instruction_isa": round(units_per_instr, 3),
             "sq_fractions_of_wave_cycles": sq, "per_kernel": per_kernel,
-            "source": "profiles/r04/ntt_counters.json (scripts/gpu_ntt_counters.sh: ubench_ntt "
+            "source": "profiles/r05/ntt_counters.json (scripts/gpu_ntt_counters.sh: ubench_ntt "
                       "lde 22 8 under rocprofv3 --pmc)"}
 
 

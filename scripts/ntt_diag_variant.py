@@ -11,6 +11,10 @@ wrong by construction: they exist to time one ingredient of the NTT kernels.
   syncmalloc  the device pool waits for the GPU to go idle before every hipMalloc: tests whether
            the first proof's long launches (kernel_outliers.py) are stalls caused by the pool
            growing while kernels run
+  desync1/2/3  the first blocks on each CU (one launch's first wave) start staggered: block k of a
+           CU (its arrival order, from a per-CU atomic counter) sleeps k x 1/2/3 x 8128 cycles, so
+           co-resident blocks of the tile / mid kernels leave the load -> compute -> store lockstep
+           they start in (tests whether compute and HBM phases of co-resident blocks overlap)
 
 usage: python3 scripts/ntt_diag_variant.py <name> [<name> ...]
 Then run a program against it with LD_LIBRARY_PATH=zkvm-brainfuck_amd/variants/<name>
@@ -30,7 +34,36 @@ DIAG_TW = ("__device__ __forceinline__ uint32_t diag_tw(int l) {\n"
            "  return z;\n"
            "}\n")
 
+DESYNC = ("__device__ uint32_t g_cu_arrivals[4096];\n"
+          "__device__ __forceinline__ void desync_first_wave(uint32_t* word) {\n"
+          "  const uint32_t per_cu = 2048u / blockDim.x;\n"
+          "  if (blockIdx.y * gridDim.x + blockIdx.x >= 256u * per_cu) return;\n"
+          "  if (threadIdx.x == 0) {\n"
+          "    uint32_t hw, xcc;\n"
+          "    asm volatile(\"s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\" : \"=s\"(hw));\n"
+          "    asm volatile(\"s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)\" : \"=s\"(xcc));\n"
+          "    const uint32_t cu = ((xcc & 15u) << 8) | ((hw >> 8) & 0xffu);\n"
+          "    word[0] = atomicAdd(&g_cu_arrivals[cu], 1u) % per_cu;\n"
+          "  }\n"
+          "  __syncthreads();\n"
+          "  const uint32_t k = word[0];\n"
+          "  __syncthreads();\n"
+          "  for (uint32_t i = 0; i < k * DESYNC_UNIT; i++) __builtin_amdgcn_s_sleep(127);\n"
+          "}\n")
+
+
+def desync(unit):
+    return [
+        ("ntt.hip", "constexpr int TILE_LOG = 12;", f"constexpr uint32_t DESYNC_UNIT = {unit};\n" + DESYNC + "constexpr int TILE_LOG = 12;"),
+        ("ntt.hip", "  uint32_t x[E];\n  if constexpr (DIN) {", "  uint32_t x[E];\n  desync_first_wave(lds);\n  if constexpr (DIN) {"),
+        ("ntt.hip", "  uint32_t x[16];\n  int done_lo = 0;", "  uint32_t x[16];\n  desync_first_wave(lds);\n  int done_lo = 0;"),
+    ]
+
+
 PATCHES = {
+    "desync1": desync(1),
+    "desync2": desync(2),
+    "desync3": desync(3),
     "twconst": [
         ("ntt_dev.h", "constexpr uint32_t G24 = cpow(3, 127);", DIAG_TW + "constexpr uint32_t G24 = cpow(3, 127);"),
         ("ntt_dev.h", "tws[l] = ld_b(rt, off, ((1u << (s0 + g0 + kk)) + ((uint32_t)l << (g0 + s0))) * 4u);",

@@ -67,10 +67,8 @@ __global__ __launch_bounds__(256) void k_inv_denoms(EF z, const EF* __restrict__
 }
 
 // ------------------------------------------------------------------ openings
-#ifndef BFZ_OPEN_R  // rows per thread of the openings (A/B builds; 4 or 6 measured neutral in round 4)
-#define BFZ_OPEN_R 8
-#endif
-constexpr int OPEN_T = 256, OPEN_R = BFZ_OPEN_R, OPEN_CH = OPEN_T * OPEN_R;
+// 8 rows per thread: 6 and 4 measured 0.08-0.15 ms per proof slower (profiles/r05/ab_open_rows.txt)
+constexpr int OPEN_T = 256, OPEN_R = 8, OPEN_CH = OPEN_T * OPEN_R;
 
 __device__ __forceinline__ EF wave_sum(EF v) {
 #pragma unroll
