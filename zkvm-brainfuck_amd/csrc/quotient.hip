@@ -116,18 +116,15 @@ __global__ __launch_bounds__(256, 3) void k_quotient(QuotRows in, int logN,
   const uint32_t inext = (i + 2) & (uint32_t)(N - 1);
   const size_t tn = dbitrev(inext, logN);
 
-  // buffer loads: the row is the voffset, the column offset the scalar soffset (no 64-bit
-  // address per column in VGPRs)
+  // buffer loads: one descriptor per column (its base is wave-uniform: scalar arithmetic), the
+  // row is the voffset -- no 64-bit address per column in VGPRs, and no 2 GiB limit on a whole
+  // column set (a 2^24-row LDE of 36 columns spans 2.4 GB)
   uint32_t L[MW], Nx[MW], PL[PWD], PN[PWD];
   const uint32_t vt = (uint32_t)(t - in.t0) * 4u, vn = (uint32_t)tn * 4u;
-  const uint32_t sw = (uint32_t)in.stride * 4u;
-  {
-    const __amdgpu_buffer_rsrc_t rl = rsrc_of(in.main_l + in.t0), rn = rsrc_of(in.main_n);
 #pragma unroll
-    for (int c = 0; c < MW; c++) {
-      L[c] = ld_b(rl, vt, (uint32_t)c * sw);
-      Nx[c] = ld_b(rn, vn, (uint32_t)in.nmain[c] * sw);
-    }
+  for (int c = 0; c < MW; c++) {
+    L[c] = ld_b(rsrc_of(in.main_l + (size_t)c * in.stride + in.t0), vt, 0);
+    Nx[c] = ld_b(rsrc_of(in.main_n + (size_t)in.nmain[c] * in.stride), vn, 0);
   }
 #pragma unroll
   for (int c = 0; c < PWD; c++) {
@@ -135,16 +132,13 @@ __global__ __launch_bounds__(256, 3) void k_quotient(QuotRows in, int logN,
     PN[c] = QPREP_W[CHIP] > 0 ? in.prep[(size_t)c * N + tn] : 0;
   }
   EF pl[PMW], pn[PMW];
-  {
-    const __amdgpu_buffer_rsrc_t rl = rsrc_of(in.perm_l + in.t0), rn = rsrc_of(in.perm_n);
 #pragma unroll
-    for (int e = 0; e < PMW; e++)
+  for (int e = 0; e < PMW; e++)
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        pl[e].c[k] = ld_b(rl, vt, (uint32_t)(4 * e + k) * sw);
-        pn[e].c[k] = ld_b(rn, vn, (uint32_t)in.nperm[4 * e + k] * sw);
-      }
-  }
+    for (int k = 0; k < 4; k++) {
+      pl[e].c[k] = ld_b(rsrc_of(in.perm_l + (size_t)(4 * e + k) * in.stride + in.t0), vt, 0);
+      pn[e].c[k] = ld_b(rsrc_of(in.perm_n + (size_t)in.nperm[4 * e + k] * in.stride), vn, 0);
+    }
 
   const uint32_t x = quot_point(i, (uint32_t)n, qp.shift, twf);
   const uint32_t zh = (i & 1) ? qp.zh_odd : qp.zh_even;
@@ -169,10 +163,6 @@ __global__ __launch_bounds__(256, 3) void k_quotient(QuotRows in, int logN,
 template <int CHIP>
 static void launch_q(const QuotRows& in, int logN, const QuotParams* qp_dev, const uint32_t* sel,
                      const QuotOut& qo, hipStream_t st) {
-  // the buffer loads address a column set with 32-bit offsets below the descriptor's 2^31 range
-  const size_t cols = std::max<size_t>(QMAIN_W[CHIP], 4 * (size_t)QPERM_W[CHIP]);
-  if (cols * in.stride * 4 >= ((size_t)1 << 31))
-    throw std::runtime_error("quotient: column set exceeds the 2 GiB buffer-load range");
   hipLaunchKernelGGL(k_quotient<CHIP>, dim3(ceil_div(in.count, 256)), dim3(256), 0, st, in, logN,
                      qp_dev, (const uint32_t*)twiddles().fwd.p, sel, qo);
   KCHECK();
