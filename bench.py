@@ -565,11 +565,19 @@ def sustained_lanes(pk, rec, ms_one, seconds, ref_proof):
         if _l.take_bytes(ptr, n.value) != ref_proof:
             raise SystemExit("bench: bfz_record_prove_repeat proof differs from the verified proof")
         out[str(inflight)] = round(wall.value / count, 3)
-    return {"proofs": count, "ms_per_proof_by_inflight": out,
+    pool = {}  # each lane's buffer pool after the runs: the device resident set of one proof in flight
+    for lane in range(4):
+        b = ctypes.c_uint64()
+        _l.check(L.bfz_device_pool_bytes(lane, ctypes.byref(b)))
+        if b.value:
+            pool[str(lane)] = round(b.value / 2**30, 2)
+    return {"proofs": count, "ms_per_proof_by_inflight": out, "pool_gib_by_lane": pool,
             "what": "bfz_record_prove_repeat: `proofs` proofs of the record back to back with 1, 2 or "
                     "3 in flight (one lane = stream + buffer pool + pinned mailboxes + host thread); "
                     "all byte-identical, the first checked against the verified proof; the "
-                    "headline `value` stays the single-proof latency"}
+                    "headline `value` stays the single-proof latency; pool_gib_by_lane = device "
+                    "memory each lane's buffer pool holds afterwards (bfz_device_pool_bytes; "
+                    "process-wide tables and keys not included)"}
 
 
 def timed_steps(step, steps, dist=None, sync=lambda: None):

@@ -365,6 +365,14 @@ int bfz_record_prove_shard_solo(const bfz_pk* pk, const bfz_record* rec, int ran
  * reference has no multi-GPU prover. */
 int bfz_shard_solo_exchanges(int* kinds, uint64_t* bytes, size_t cap, size_t* n);
 
+/* Device memory held by proof lane `lane`'s buffer pool (0..3, the lanes of
+ * bfz_record_prove_repeat / bfz_prove_batch; 0 = the default
+ * lane): every buffer a proof on that lane allocated, in use or cached for the next proof -- the
+ * resident set of one proof in flight (bench.py reports it beside the lanes' throughput).  The
+ * process-wide caches (twiddle and power tables, proving keys, batch event slots) are not
+ * included.  0 for a lane never used. */
+int bfz_device_pool_bytes(int lane, uint64_t* bytes);
+
 /* Column-sharded PCS commit + FRI commit phase of a synthetic trace (BASELINE.json configs 4
  * and 5).  Replaces, for one n x (world * w_local) trace, TwoAdicFriPcs::commit
  * (crates/stark/src/prover.rs:209-236: coset LDE with shift GENERATOR, bit-reversed rows,

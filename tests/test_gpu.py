@@ -258,6 +258,15 @@ def test_record_prove_repeat_two_lanes_matches_oracle(client):
         _lib.check(L.bfz_record_prove_repeat(ctypes.c_void_p(pk.handle), ctypes.c_void_p(drec.handle),
                                              2, 5, ctypes.byref(ptr), ctypes.byref(n), None))
     assert _prove_record(pk, drec) == want
+    # every lane that proved holds a pool: at least the record's LDEs (2n rows of the main trace)
+    held = []
+    for lane in range(4):
+        b = ctypes.c_uint64()
+        _lib.check(L.bfz_device_pool_bytes(lane, ctypes.byref(b)))
+        held.append(b.value)
+    assert all(h > 0 for h in held), held
+    with pytest.raises(_lib.BfzError, match="lane"):
+        _lib.check(L.bfz_device_pool_bytes(4, ctypes.byref(b)))
 
 
 def test_prove_batch_error_does_not_hang(client):

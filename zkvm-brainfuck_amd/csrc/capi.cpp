@@ -1092,6 +1092,15 @@ int bfz_record_prove_sharded(const bfz_pk* pk, const bfz_record* rec, int rank, 
   });
 }
 
+int bfz_device_pool_bytes(int lane, uint64_t* bytes) {
+  return guarded([&] {
+    if (!bytes) throw std::runtime_error("null argument");
+    if (lane < 0 || lane >= bfz::MAX_LANES) throw std::runtime_error("lane must be in 0..3");
+    *bytes = bfz::lane_pool_bytes(lane);
+    return 0;
+  });
+}
+
 int bfz_shard_solo_exchanges(int* kinds, uint64_t* bytes, size_t cap, size_t* n) {
   return guarded([&] {
     if (!n) throw std::runtime_error("null argument");

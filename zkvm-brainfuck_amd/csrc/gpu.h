@@ -69,7 +69,12 @@ class DevicePool {
     void* p = nullptr;
     HIP_CHECK(hipMalloc(&p, bytes));
     size_of_[p] = bytes;
+    held_ += bytes;
     return p;
+  }
+  size_t bytes() {  // device memory this pool holds (in use + cached)
+    std::lock_guard<std::mutex> lk(mu_);
+    return held_;
   }
   void release(void* p) {
     if (!p) return;
@@ -83,6 +88,7 @@ class DevicePool {
     for (auto& kv : free_)
       for (void* p : kv.second) {
         (void)hipFree(p);
+        held_ -= kv.first;
         size_of_.erase(p);
       }
     free_.clear();
@@ -94,6 +100,7 @@ class DevicePool {
   // end of a proof sit between the last kernel of one proof and the first of the next
   std::unordered_map<size_t, std::vector<void*>> free_;
   std::unordered_map<void*, size_t> size_of_;
+  size_t held_ = 0;
   std::mutex mu_;
 };
 
@@ -123,6 +130,7 @@ struct Lane {
 };
 Lane& lane();           // this thread's lane (the default lane unless a LaneScope is active)
 Lane* lane_at(int i);   // lane i (0 = the default lane), created on first use; lives for the process
+size_t lane_pool_bytes(int i);  // device bytes lane i's pool holds (0 if the lane was never used)
 struct LaneScope {      // runs this thread's device work on another lane while in scope
   Lane* prev;
   explicit LaneScope(Lane* l);

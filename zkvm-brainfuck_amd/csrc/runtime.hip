@@ -30,6 +30,15 @@ Lane* lane_at(int i) {
   if (!g_lanes[i]) g_lanes[i] = make_lane(i);
   return g_lanes[i];
 }
+size_t lane_pool_bytes(int i) {
+  if (i < 0 || i >= MAX_LANES) throw std::runtime_error("lane index out of range");
+  Lane* l;
+  {
+    std::lock_guard<std::mutex> lk(g_lanes_mu);
+    l = g_lanes[i];
+  }
+  return l ? l->pool.bytes() : 0;
+}
 Lane& lane() {
   if (tl_lane) return *tl_lane;
   static Lane* d = lane_at(0);
