@@ -364,9 +364,11 @@ fn memory_events(r: &ExecutionRecord) -> Vec<sys::bfz_memory_event> {
         .collect()
 }
 
-/// Cycles per bfz_cycles_push: small enough that the DMA of the first chunks starts while the
-/// rest are converted (crates/bf-hip-prover/standin/cycle_arrays.cpp times the same loop).
-const HANDOVER_CHUNK: usize = 1 << 15;
+/// Cycles per bfz_cycles_push (2 MB): small enough that the DMA of the first chunks starts while
+/// the rest are converted, large enough that the per-copy cost stays small
+/// (crates/bf-hip-prover/standin/cycle_arrays.cpp times the same loop; scripts/handover_ab.py:
+/// 2^17 cycles 29.9-30.0 ms, 2^15 30.0-30.5, 2^13 33.8, one chunk per thread at 2^19 31.2-31.4).
+const HANDOVER_CHUNK: usize = 1 << 17;
 
 impl CycleArrays {
     #[allow(dead_code)] // the one-shot hand-over (bfz_record_from_cycles); prove uses hand_over
