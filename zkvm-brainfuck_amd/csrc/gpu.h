@@ -107,8 +107,9 @@ class DevicePool {
 // A proof lane: the device context one proof runs in -- its stream, the stream-ordered buffer
 // pool of that stream, the pinned staging arena of its in-proof uploads and its transcript
 // mailboxes.  The process has a default lane; bfz_prove_batch and bfz_record_prove_repeat keep
-// two proofs in flight on two lanes (one host thread each), so the latency-bound launches of one
-// proof (tree tops, the FRI tail, transcript steps) run beside the other's bulk kernels.
+// up to MAX_LANES proofs in flight on as many lanes (one host thread each), so the latency-bound
+// launches of one proof (tree tops, the FRI tail, transcript steps) run beside another's bulk
+// kernels.
 constexpr int MAX_LANES = 4;
 constexpr int DEFAULT_INFLIGHT = 2;  // proofs in flight in bfz_prove_batch (profiles/r05)
 struct Lane {

@@ -5,9 +5,11 @@
 // Here three kinds of threads overlap:
 //   executor threads   Executor::run into pinned HostEvents (machine.h execute_into), several
 //                      jobs at once;
-//   uploader thread    in job order, one DMA per event array from pinned memory into one of two
-//                      device event slots, on its own HIP stream;
-//   calling thread     in job order, device trace generation + the proof on the prover stream.
+//   uploader thread    in job order, one DMA per event array from pinned memory into one of
+//                      NSLOT device event slots, on its own HIP stream;
+//   prover lanes       up to MAX_LANES (default 2) proofs in flight, each on its own lane (stream,
+//                      pool, mailboxes; the calling thread is lane 0): device trace generation +
+//                      the proof, jobs taken in order.
 // A device slot is refilled only after the proof that read it has finished generating its
 // traces (an event recorded on the prover stream right after tracegen).
 #include <chrono>
@@ -53,7 +55,7 @@ hipStream_t copy_stream() {
 
 // Device event arrays of one pipeline slot: plain hipMalloc memory (not the stream-ordered
 // pools, which are ordered on the lanes' streams only), grown on demand and kept for the process.
-// Job j uses slot j % NSLOT: with two proofs in flight, a third slot takes the next upload.
+// Job j uses slot j % NSLOT: every lane can hold a slot while one more takes the next upload.
 constexpr int NSLOT = MAX_LANES + 1;
 struct EventSlot {
   static constexpr int N = 6;  // cpu, alu, jump, meminstr, io, memory
