@@ -11,6 +11,9 @@ wrong by construction: they exist to time one ingredient of the NTT kernels.
   syncmalloc  the device pool waits for the GPU to go idle before every hipMalloc: tests whether
            the first proof's long launches (kernel_outliers.py) are stalls caused by the pool
            growing while kernels run
+  nohbm    the 2^14 tiles read and write only four tiles' worth of addresses (L2-resident; output
+           wrong): the butterflies + LDS exchanges + L2 traffic without HBM, to set against the
+           full pass and reps0 (HBM only) -- how much of compute and data movement overlaps
   desync1/2/3  the first blocks on each CU (one launch's first wave) start staggered: block k of a
            CU (its arrival order, from a per-CU atomic counter) sleeps k x 1/2/3 x 8128 cycles, so
            co-resident blocks of the tile / mid kernels leave the load -> compute -> store lockstep
@@ -61,6 +64,12 @@ def desync(unit):
 
 
 PATCHES = {
+    "nohbm": [
+        ("ntt.hip", "  const uint32_t* S = src + (size_t)blockIdx.y * src_stride + ((size_t)blockIdx.x << B);\n"
+                    "  uint32_t* D = dst + (size_t)blockIdx.y * dst_stride + ((size_t)blockIdx.x << B);",
+         "  const uint32_t* S = src + ((size_t)(blockIdx.x & 3) << B);\n"
+         "  uint32_t* D = dst + ((size_t)(blockIdx.x & 3) << B);  (void)src_stride; (void)dst_stride;"),
+    ],
     "desync1": desync(1),
     "desync2": desync(2),
     "desync3": desync(3),
