@@ -65,7 +65,7 @@ def main():
             hs.append((t1 - t0) * 1e3)
             ps.append((t2 - t1) * 1e3)
         print(f"{label}: hand-over {min(hs):.3f} ms, then prove {min(ps):.3f} ms", flush=True)
-    for chunk in (1 << 13, 1 << 15, 1 << 17, 1 << 19, 1 << 22):
+    for chunk in [int(c) for c in os.environ.get("CHUNKS", "8192 32768 131072 524288 4194304").split()]:
         r = bench.compiled_handover(pk, rec, prove, best, ref, chunk)
         print(f"chunk {chunk:8d}: pipelined {r['pipelined_ms']:.3f} ms (last push at "
               f"{r['pipelined_last_push_ms']:.3f}), sequential {r['sequential_ms']:.3f}, "
