@@ -284,7 +284,7 @@ int main() {
   HIP_CHECK(hipEventCreate(&e1));
   int bad = 0;
   for (int dif = 0; dif < 2; dif++) {
-    const uint32_t* tw = dif ? twiddles().fwd.p : twiddles().inv.p;
+    const uint32_t* tw = dif ? twiddles().fwd() : twiddles().inv();
     auto mfma = [&] {
       if (dif)
         hipLaunchKernelGGL(k_tile14_mfma<true>, dim3(1, W), dim3(MF_THREADS), MF_DATA * 4, st, a, out,

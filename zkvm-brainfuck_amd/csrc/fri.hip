@@ -597,7 +597,7 @@ void inv_denoms_range(const EF& z, int logH, size_t t0, size_t count, EF* out, h
   twiddles().ensure(std::max(logH, 1));
   const size_t nthreads = (count + INV_CHUNK - 1) / INV_CHUNK;
   hipLaunchKernelGGL(k_inv_denoms, dim3(ceil_div(nthreads, 256)), dim3(256), 0, st, z,
-                     (const EF*)nullptr, logH, t0, count, (const uint32_t*)twiddles().fwd.p, out);
+                     (const EF*)nullptr, logH, t0, count, (const uint32_t*)twiddles().fwd(), out);
   KCHECK();
 }
 
@@ -606,7 +606,7 @@ void inv_denoms_dev(const EF* z, int logH, EF* out, hipStream_t st) {
   const size_t count = (size_t)1 << logH;
   const size_t nthreads = (count + INV_CHUNK - 1) / INV_CHUNK;
   hipLaunchKernelGGL(k_inv_denoms, dim3(ceil_div(nthreads, 256)), dim3(256), 0, st, ef_zero(), z,
-                     logH, (size_t)0, count, (const uint32_t*)twiddles().fwd.p, out);
+                     logH, (size_t)0, count, (const uint32_t*)twiddles().fwd(), out);
   KCHECK();
 }
 
@@ -666,7 +666,7 @@ void open_batch(std::vector<OpenDesc>& ds, int np, hipStream_t st) {
   }
   KernelProbe& probe = open_probe();
   DBuf<EF> partial(std::max<uint64_t>(part, 1));
-  const uint32_t* twf = (const uint32_t*)twiddles().fwd.p;
+  const uint32_t* twf = (const uint32_t*)twiddles().fwd();
   const int nd = (int)ds.size();
   hipEvent_t ev0 = probe.on ? probe.begin(st) : nullptr;
   if (np == 2)
@@ -774,7 +774,7 @@ void fri_fold_range(const EF* in, EF* out, size_t h, size_t i0, size_t count, co
   const int logh = log2i(h);
   twiddles().ensure(logh + 1);
   hipLaunchKernelGGL(k_fri_fold_dev, dim3(ceil_div(count, 256)), dim3(256), 0, st, in, out, h,
-                     logh, i0, count, beta, (const uint32_t*)twiddles().inv.p, add);
+                     logh, i0, count, beta, (const uint32_t*)twiddles().inv(), add);
   KCHECK();
 }
 
@@ -782,7 +782,7 @@ void fri_fold_leaves(const EF* in, EF* out, size_t h, const EF* beta, const EF* 
                      uint32_t* digests, hipStream_t st) {
   const int logn = log2i(2 * h);
   twiddles().ensure(logn + 1);
-  const uint32_t* twi = (const uint32_t*)twiddles().inv.p;
+  const uint32_t* twi = (const uint32_t*)twiddles().inv();
   KernelProbe& probe = p2_probe();
   hipEvent_t ev0 = probe.on ? probe.begin(st) : nullptr;
   hipLaunchKernelGGL(k_fold_leaves, dim3(ceil_div(h, 256)), dim3(256), 0, st, in, out, h, logn,
@@ -795,7 +795,7 @@ void fri_tail_rounds(const FriTailRounds& a, hipStream_t st) {
   if (a.nr < 1 || a.nr > FRI_TAIL_MAXR || a.logh0 < a.nr || (1 << a.logh0) > FRI_TAIL_MAXH)
     throw std::runtime_error("fri_tail_rounds: bad round count");
   twiddles().ensure(a.logh0 + 1);
-  hipLaunchKernelGGL(k_fri_tail, dim3(1), dim3(1024), 0, st, a, (const uint32_t*)twiddles().inv.p);
+  hipLaunchKernelGGL(k_fri_tail, dim3(1), dim3(1024), 0, st, a, (const uint32_t*)twiddles().inv());
   KCHECK();
 }
 

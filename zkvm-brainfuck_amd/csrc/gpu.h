@@ -193,10 +193,18 @@ struct DevMatrix {
 
 // Twiddle tables: T[h + j] = w_{2h}^j for h = 2^k (k < LOGMAX), j < h   (forward)
 //                 and w_{2h}^-j                                          (inverse)
+// The tables grow (ensure) while other lanes may read them: a grown table is filled before its
+// pointer is published (release store, acquire load), and every table ever built stays allocated
+// (kernels queued before a growth still read the old one; it is a prefix of the new).
 struct Twiddles {
   std::atomic<int> logmax{0};
-  DBuf<uint32_t> fwd, inv;
+  const uint32_t* fwd() const { return fwd_.load(std::memory_order_acquire); }
+  const uint32_t* inv() const { return inv_.load(std::memory_order_acquire); }
   void ensure(int log_n);
+
+ private:
+  std::atomic<const uint32_t*> fwd_{nullptr}, inv_{nullptr};
+  std::vector<DBuf<uint32_t>> tables_;
 };
 Twiddles& twiddles();
 

@@ -572,15 +572,15 @@ static void r16_launch(const R16Pass& p, const uint32_t* in, size_t is, uint32_t
   KernelProbe& probe = ntt_probe();
   hipEvent_t ev0 = probe.on ? probe.begin(st) : nullptr;
   if (p.s0 == 0 && p.c == 0 &&
-      (dif ? tile_dispatch<true>(p.b, grid, in, is, dst, ds, (const uint32_t*)T.fwd.p, st)
-           : tile_dispatch<false>(p.b, grid, in, is, dst, ds, (const uint32_t*)T.inv.p, st))) {
+      (dif ? tile_dispatch<true>(p.b, grid, in, is, dst, ds, (const uint32_t*)T.fwd(), st)
+           : tile_dispatch<false>(p.b, grid, in, is, dst, ds, (const uint32_t*)T.inv(), st))) {
     // specialised contiguous pass
   } else if (dif)
     hipLaunchKernelGGL(k_ntt_r16<true>, grid, dim3(threads), lds * 4, st, in, dst, is, ds, p.s0,
-                       p.b, p.c, (const uint32_t*)T.fwd.p);
+                       p.b, p.c, (const uint32_t*)T.fwd());
   else
     hipLaunchKernelGGL(k_ntt_r16<false>, grid, dim3(threads), lds * 4, st, in, dst, is, ds, p.s0,
-                       p.b, p.c, (const uint32_t*)T.inv.p);
+                       p.b, p.c, (const uint32_t*)T.inv());
   KCHECK();
   if (probe.on) probe.end(ev0, st, 8.0 * (double)((size_t)1 << L) * ncols);
 }
@@ -611,10 +611,10 @@ void ntt_passes(const uint32_t* src, uint32_t* dst, size_t src_stride, size_t ds
     const size_t is = first ? src_stride : dst_stride;
     if (dif)
       hipLaunchKernelGGL(k_ntt_pass<true>, grid, dim3(256), 0, st, in, dst, is, dst_stride, s0, b,
-                         c, T.fwd.p);
+                         c, T.fwd());
     else
       hipLaunchKernelGGL(k_ntt_pass<false>, grid, dim3(256), 0, st, in, dst, is, dst_stride, s0, b,
-                         c, T.inv.p);
+                         c, T.inv());
     KCHECK();
     first = false;
   }
@@ -708,7 +708,7 @@ void coset_lde_ex(const uint32_t* evals, size_t src_stride, size_t n, int w, uin
   case LL:                                                                                       \
     static_assert(MidPlan<LL>::b2 >= 4, "plan");                                                 \
     hipLaunchKernelGGL(k_lde_mid<LL>, grid, dim3(threads), ldsz * 4, st, (const uint32_t*)coef.p, \
-                       n, lde, n, (const uint32_t*)T.inv.p, (const uint32_t*)T.fwd.p, pw, B, mp, \
+                       n, lde, n, (const uint32_t*)T.inv(), (const uint32_t*)T.fwd(), pw, B, mp, \
                        only_half);                                                               \
     break;
     switch (L) {

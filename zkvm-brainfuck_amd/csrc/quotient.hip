@@ -164,7 +164,7 @@ template <int CHIP>
 static void launch_q(const QuotRows& in, int logN, const QuotParams* qp_dev, const uint32_t* sel,
                      const QuotOut& qo, hipStream_t st) {
   hipLaunchKernelGGL(k_quotient<CHIP>, dim3(ceil_div(in.count, 256)), dim3(256), 0, st, in, logN,
-                     qp_dev, (const uint32_t*)twiddles().fwd.p, sel, qo);
+                     qp_dev, (const uint32_t*)twiddles().fwd(), sel, qo);
   KCHECK();
 }
 
@@ -179,7 +179,7 @@ static const uint32_t* sel_inv_table(int logN, const QuotParams& qp, hipStream_t
   const size_t N = (size_t)1 << logN;
   DBuf<uint32_t> d(N);
   hipLaunchKernelGGL(k_sel_inv, dim3(ceil_div(N, 256)), dim3(256), 0, st, logN, qp.shift,
-                     qp.wn_inv, (const uint32_t*)twiddles().fwd.p, d.p);
+                     qp.wn_inv, (const uint32_t*)twiddles().fwd(), d.p);
   KCHECK();
   HIP_CHECK(hipStreamSynchronize(st));  // complete before another lane's stream reads it
   const uint32_t* p = d.p;

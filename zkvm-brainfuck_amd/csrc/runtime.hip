@@ -315,23 +315,15 @@ void Twiddles::ensure(int log_n) {
       b = kb::mmul(b, wi);
     }
   }
-  // The new tables are filled before they are published: another lane reads fwd.p / inv.p
-  // without the lock, so each pointer goes from the old table straight to the filled new one
-  // (one store, never null) and the old tables stay allocated -- kernels queued before the swap
-  // still read them, and they are a prefix of the new ones.
   DBuf<uint32_t> nf(N), ni(N);  // stream-ordered: pooled buffers may be read by queued kernels
   HIP_CHECK(hipMemcpyAsync(nf.p, hf.data(), N * 4, hipMemcpyHostToDevice, stream()));
   HIP_CHECK(hipMemcpyAsync(ni.p, hi.data(), N * 4, hipMemcpyHostToDevice, stream()));
   HIP_CHECK(hipStreamSynchronize(stream()));
-  std::swap(fwd.p, nf.p);
-  std::swap(inv.p, ni.p);
-  std::swap(fwd.from, nf.from);
-  std::swap(inv.from, ni.from);
-  fwd.n = inv.n = N;
-  static auto* old = new std::vector<DBuf<uint32_t>>();  // outgrown tables (empty on first use)
-  old->push_back(std::move(nf));
-  old->push_back(std::move(ni));
-  logmax = log_n;
+  fwd_.store(nf.p, std::memory_order_release);
+  inv_.store(ni.p, std::memory_order_release);
+  tables_.push_back(std::move(nf));
+  tables_.push_back(std::move(ni));
+  logmax.store(log_n, std::memory_order_release);
 }
 
 }  // namespace bfz
