@@ -52,7 +52,10 @@ __device__ __forceinline__ uint32_t dbitrev(uint32_t x, int bits) {
 }
 
 // Size-bucketed caching allocator: proofs reuse the same buffer shapes, so after the first
-// proof no hipMalloc/hipFree happens inside the timed region.
+// proof no hipMalloc/hipFree happens inside the timed region.  A request takes a free buffer of
+// its exact size, else the smallest free one of at most twice its size (a proof of another
+// shape reuses the cached buffers instead of adding a new set: the pool stays within 2x of the
+// largest shape's working set, not the sum over every shape a long-running process proves).
 class DevicePool {
  public:
   // (locked: a buffer may be released from another lane's thread than the one that allocated it)
@@ -60,10 +63,11 @@ class DevicePool {
     std::lock_guard<std::mutex> lk(mu_);
     bytes = (bytes + 255) & ~(size_t)255;
     if (bytes == 0) bytes = 256;
-    auto it = free_.find(bytes);
-    if (it != free_.end() && !it->second.empty()) {
+    auto it = free_.lower_bound(bytes);
+    if (it != free_.end() && it->first <= 2 * bytes) {
       void* p = it->second.back();
       it->second.pop_back();
+      if (it->second.empty()) free_.erase(it);
       return p;
     }
     void* p = nullptr;
@@ -96,9 +100,9 @@ class DevicePool {
   ~DevicePool() {}
 
  private:
-  // hash maps: a proof allocates and releases a few hundred buffers, and the releases at the
-  // end of a proof sit between the last kernel of one proof and the first of the next
-  std::unordered_map<size_t, std::vector<void*>> free_;
+  // a proof allocates and releases a few hundred buffers of some tens of sizes: an ordered map of
+  // the free sizes (empty lists erased) for the best-fit lookup, a hash map for the releases
+  std::map<size_t, std::vector<void*>> free_;
   std::unordered_map<void*, size_t> size_of_;
   size_t held_ = 0;
   std::mutex mu_;
