@@ -577,7 +577,8 @@ def sustained_lanes(pk, rec, ms_one, seconds, ref_proof):
                     "all byte-identical, the first checked against the verified proof; the "
                     "headline `value` stays the single-proof latency; pool_gib_by_lane = device "
                     "memory each lane's buffer pool holds afterwards (bfz_device_pool_bytes; "
-                    "process-wide tables and keys not included)"}
+                    "process-wide tables, keys and record events not included: they "
+                    "live in a separate resident pool)"}
 
 
 def timed_steps(step, steps, dist=None, sync=lambda: None):
@@ -601,6 +602,23 @@ def timed_steps(step, steps, dist=None, sync=lambda: None):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ms = float(t.item())
     return ms
+
+
+def cold_first_proof():
+    """The first proof of a fresh process: scripts/cold_first_proof.py in a
+    child process -- init, setup, record, ONE prove (timed), host-verified, then two warm proofs
+    of the same record -- with nothing else on the GPU (it runs before this process initialises
+    the device).  The reference's `e2e=` timer brackets exactly such a single prove call
+    (crates/core/machine/src/utils/prove.rs:44-56)."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "cold_first_proof.py")],
+                         capture_output=True, text=True, timeout=300)
+    if out.returncode != 0:
+        return {"error": (out.stderr or out.stdout).strip().splitlines()[-1:]}
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    r["what"] = ("fresh child process: bfz_init, setup (ProverClient::setup), bfz_record_new "
+                 "(execute + event upload + the tables for the record's heights), then ONE "
+                 "bfz_record_prove = first_prove_ms; warm_prove_ms = the next proofs of the record")
+    return r
 
 
 def run_pcs(args, rank, world, device, dist, coll):
@@ -671,6 +689,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cold", action="store_true",
+                    help="skip the fresh-process first-proof measurement (cold_first_proof_ms)")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the end-to-end batch and drop-in-path figures")
     ap.add_argument("--mode", choices=("replicas", "sharded", "pcs"), default="replicas",
@@ -718,6 +738,10 @@ def main():
     os.dup2(saved_stdout, 1)
     os.close(saved_stdout)
 
+    cold = None
+    if world == 1 and args.mode == "replicas" and not args.no_cold:
+        cold = cold_first_proof()  # before this process touches the GPU
+
     from bfz import _lib, guests, sdk
     import ctypes
 
@@ -752,7 +776,10 @@ def main():
                                       ctypes.byref(plen), ctypes.byref(timings) if timings else None))
         return _lib.take_bytes(ptr, plen.value)
 
-    for _ in range(args.warmup):  # the lane's buffer pool fills during the first proofs
+    t_first = time.perf_counter()
+    first_proof = one()  # the first prove after setup in this process (counts as a warmup step)
+    first_ms = (time.perf_counter() - t_first) * 1e3
+    for _ in range(args.warmup - 1):  # the lane's buffer pool fills during the first proofs
         one()
     # one timed-with-events proof for the roofline (kept out of the headline timing), verified on
     # the host; the warmup is repeated after it, right before the timed steps, so the GPU is not
@@ -772,6 +799,8 @@ def main():
     # every timed step proves the same record: the last one must be the verified proof's bytes
     if last["proof"] != proof:
         raise SystemExit("bench: the last timed proof differs from the verified proof")
+    if first_proof != proof:
+        raise SystemExit("bench: the first proof differs from the verified proof")
     extra = {}
     if not sharded and args.sustain_s > 0:
         last.clear()
@@ -822,6 +851,9 @@ def main():
             "ntt_valu": ntt_valu(tm),
             "poseidon2": poseidon2_roofline(tm),
             "openings": openings_roofline(tm),
+            "first_prove_after_setup_ms": round(first_ms, 3),
+            "cold_first_proof_ms": cold.get("first_prove_ms") if cold else None,
+            "cold_first_proof": cold,
             "proof_bytes": len(proof),
             "proof_check": "host verifier accepted the proof; the last timed proof (and the last "
                            "sustained one) are byte-identical to it",

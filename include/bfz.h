@@ -369,8 +369,9 @@ int bfz_shard_solo_exchanges(int* kinds, uint64_t* bytes, size_t cap, size_t* n)
  * bfz_record_prove_repeat / bfz_prove_batch; 0 = the default
  * lane): every buffer a proof on that lane allocated, in use or cached for the next proof -- the
  * resident set of one proof in flight (bench.py reports it beside the lanes' throughput).  The
- * process-wide caches (twiddle and power tables, proving keys, batch event slots) are not
- * included.  0 for a lane never used. */
+ * process-wide device data -- twiddle, power and selector tables, proving keys, the records'
+ * device events -- lives in a separate resident pool and is not included.  0 for a lane never
+ * used. */
 int bfz_device_pool_bytes(int lane, uint64_t* bytes);
 
 /* Column-sharded PCS commit + FRI commit phase of a synthetic trace (BASELINE.json configs 4

@@ -269,6 +269,41 @@ def test_record_prove_repeat_two_lanes_matches_oracle(client):
         _lib.check(L.bfz_device_pool_bytes(4, ctypes.byref(b)))
 
 
+def test_pool_reuse_across_shapes(client):
+    """The lane pool (gpu.h DevicePool): a second proof of a shape the pool has already
+    served allocates nothing, in either order of two shapes whose buffers differ by more than 2x
+    (fibo17: Cpu 2^9 rows; fibo255: Cpu 2^20 rows), and the proving key, tables and the record's
+    events are not in the lane's pool."""
+    from bfz import events
+    L = _lib.lib()
+
+    def held():
+        b = ctypes.c_uint64()
+        _lib.check(L.bfz_device_pool_bytes(0, ctypes.byref(b)))
+        return b.value
+
+    pk, _ = client.setup(guests.FIBO)
+    small = events.record_from_events(pk, events.ExecutionRecordArrays.from_executor(guests.FIBO, [17]))
+    big = events.record_from_events(pk, events.ExecutionRecordArrays.from_executor(guests.FIBO, [255]))
+    _prove_record(pk, small)
+    _prove_record(pk, big)
+    b0 = held()
+    extra = events.record_from_events(pk, events.ExecutionRecordArrays.from_executor(guests.FIBO, [255]))
+    assert held() == b0, "a record's device events went to the lane pool"
+    del extra
+    for rec in (small, big, small, big):
+        _prove_record(pk, rec)
+        assert held() == b0
+
+
+def test_device_twiddle_table_matches_host():
+    """The twiddle table is built on the device (runtime.hip k_twiddle_table, 2 x 2^24 words, once
+    per process): identical to the host's running products (levels < 2^20 in full, a sample of
+    every higher level)."""
+    L = _lib.lib()
+    assert L.bfz_selftest(b"twiddles") == 0, L.bfz_last_error()
+
+
 def test_prove_batch_error_does_not_hang(client):
     """An executor failure (missing input) in the middle of a batch is reported, the other
     threads stop, and the library stays usable."""

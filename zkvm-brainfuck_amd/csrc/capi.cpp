@@ -257,6 +257,31 @@ int bfz_selftest(const char* name) {
       if (after != before) throw std::runtime_error("selftest emit_rollback: emitted proofs leaked");
       return 0;
     }
+    if (what == "twiddles") {  // the device-built table == the host's running products
+      bfz::Twiddles& T = bfz::twiddles();
+      T.ensure(bfz::TWIDDLE_LOG_MAX);
+      const int L = T.logmax;
+      for (int inverse = 0; inverse < 2; inverse++) {
+        // the table's levels below 2^20 (host reference in seconds) and the top level's head
+        const std::vector<uint32_t> want = bfz::host_twiddles(20, inverse);
+        std::vector<uint32_t> got((size_t)1 << L);
+        HIP_CHECK(hipMemcpy(got.data(), inverse ? T.inv() : T.fwd(), got.size() * 4,
+                            hipMemcpyDeviceToHost));
+        if (std::memcmp(got.data(), want.data(), want.size() * 4) != 0)
+          throw std::runtime_error("selftest twiddles: levels < 20 differ from the host table");
+        for (int k = 20; k < L; k++) {  // every level: first 4096 words and a strided sample
+          uint32_t w = kb::two_adic_gen(k + 1);
+          if (inverse) w = kb::minv(w);
+          const size_t h = (size_t)1 << k;
+          uint32_t a = kb::ONE;
+          for (size_t j = 0; j < 4096; j++, a = kb::mmul(a, w))
+            if (got[h + j] != a) throw std::runtime_error("selftest twiddles: high level head differs");
+          for (size_t j = 4097; j < h; j += 65521)
+            if (got[h + j] != kb::mpow(w, j)) throw std::runtime_error("selftest twiddles: high level differs");
+        }
+      }
+      return 0;
+    }
     throw std::runtime_error("bfz_selftest: unknown test '" + what + "'");
   });
 }
@@ -647,7 +672,13 @@ int bfz_prove_batch(const bfz_pk* pk, const uint8_t* const* stdins, const size_t
     bfz::BatchStats bs;
     static const int inflight = [] {  // proofs in flight (lanes); BFZ_INFLIGHT = 1..MAX_LANES
       const char* e = std::getenv("BFZ_INFLIGHT");
-      return e && *e >= '1' && *e <= '0' + bfz::MAX_LANES ? *e - '0' : bfz::DEFAULT_INFLIGHT;
+      if (!e || !*e) return bfz::DEFAULT_INFLIGHT;
+      char* end = nullptr;
+      const long v = std::strtol(e, &end, 10);
+      if (*end || v < 1 || v > bfz::MAX_LANES)
+        throw std::runtime_error(std::string("BFZ_INFLIGHT must be an integer in 1..") +
+                                 std::to_string(bfz::MAX_LANES) + ", got '" + e + "'");
+      return (int)v;
     }();
     auto v = bfz::prove_batch(*pk->pk, jobs, opts(), E, inflight, &bs);
     emit_all(v, proofs, proof_lens, (size_t)-1);
@@ -680,6 +711,7 @@ int bfz_verify(const char* elf, const uint32_t vk_commit[8], const uint8_t* proo
 int bfz_record_new(const bfz_pk* pk, const uint8_t* in, size_t nin, bfz_record** rec,
                    uint64_t* cycles) {
   return guarded([&] {
+    bfz::ResidentScope rs;  // the record's device events live outside the lane pools
     auto r = std::make_unique<bfz_record>();
     bfz::HostEvents& h = bfz::scratch_events();
     bfz::execute_into(pk->pk->program, in, nin, h);
@@ -843,6 +875,7 @@ extern "C" {
 
 int bfz_record_from_events(const bfz_pk* pk, const bfz_events* e, bfz_record** rec) {
   return guarded([&] {
+    bfz::ResidentScope rs;  // the record's device events live outside the lane pools
     if (!pk || !e || !rec) throw std::runtime_error("null argument");
     if (e->n_cpu == 0) throw std::runtime_error("record_from_events: no cpu events");
     const size_t lim = (size_t)1 << 26;  // beyond any committable trace (2^23 rows)
@@ -903,6 +936,7 @@ void bfz_host_free(void* p) {
 int bfz_record_from_cycles(const bfz_pk* pk, const bfz_cycle* cycles, size_t n_cycles,
                            const bfz_memory_event* memory, size_t n_memory, bfz_record** rec) {
   return guarded([&] {
+    bfz::ResidentScope rs;  // the record's device events live outside the lane pools
     if (!pk || !rec) throw std::runtime_error("null argument");
     check_cycle_counts(n_cycles, n_memory);
     if (!cycles) throw std::runtime_error("record_from_cycles: null cycle array");
@@ -916,6 +950,7 @@ int bfz_record_from_cycles(const bfz_pk* pk, const bfz_cycle* cycles, size_t n_c
 
 int bfz_cycles_begin(const bfz_pk* pk, size_t n_cycles, bfz_cycle_upload** up) {
   return guarded([&] {
+    bfz::ResidentScope rs;  // the record's device events live outside the lane pools
     if (!pk || !up) throw std::runtime_error("null argument");
     check_cycle_counts(n_cycles, 0);
     auto u = std::make_unique<bfz_cycle_upload>();
@@ -950,6 +985,7 @@ int bfz_cycles_finish(bfz_cycle_upload* up, const bfz_memory_event* memory, size
                       bfz_record** rec) {
   std::unique_ptr<bfz_cycle_upload> u(up);  // consumed whatever happens
   return guarded([&] {
+    bfz::ResidentScope rs;  // the record's device events live outside the lane pools
     if (!u || !rec) throw std::runtime_error("null argument");
     // the prover stream waits for the last copy on the device (no host synchronisation); done
     // first, so the buffer goes back to the stream-ordered pool after the copies on any path
@@ -1045,10 +1081,18 @@ int bfz_record_prove_repeat(const bfz_pk* pk, const bfz_record* rec, int count, 
     std::vector<uint8_t> first;
     std::mutex mu;
     std::atomic<int> next{0};
-    std::atomic<bool> differ{false};
+    std::atomic<bool> differ{false}, failed{false};
     bfz::run_lanes(inflight, [&](int) {
-      for (int k; (k = next.fetch_add(1)) < count;) {
-        auto v = bfz::prove_events(*pk->pk, rec->ev, o, nullptr);
+      // a lane that throws stops the others at their next proof (the error returns at once,
+      // not after the remaining `count` proofs)
+      for (int k; !failed.load(std::memory_order_relaxed) && (k = next.fetch_add(1)) < count;) {
+        std::vector<uint8_t> v;
+        try {
+          v = bfz::prove_events(*pk->pk, rec->ev, o, nullptr);
+        } catch (...) {
+          failed.store(true, std::memory_order_relaxed);
+          throw;
+        }
         std::lock_guard<std::mutex> lk(mu);
         if (first.empty()) {
           first = std::move(v);

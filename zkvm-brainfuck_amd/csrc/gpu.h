@@ -53,9 +53,10 @@ __device__ __forceinline__ uint32_t dbitrev(uint32_t x, int bits) {
 
 // Size-bucketed caching allocator: proofs reuse the same buffer shapes, so after the first
 // proof no hipMalloc/hipFree happens inside the timed region.  A request takes a free buffer of
-// its exact size, else the smallest free one of at most twice its size (a proof of another
-// shape reuses the cached buffers instead of adding a new set: the pool stays within 2x of the
-// largest shape's working set, not the sum over every shape a long-running process proves).
+// its exact size, else the smallest free one of at most twice its size, so a proof of a nearby
+// shape reuses cached buffers.  Buffers are never released (trim() is not called by the prover):
+// a process that proves shapes whose buffers differ by more than 2x holds a set per size class
+// (tests/test_gpu.py test_pool_reuse_across_shapes measures it).
 class DevicePool {
  public:
   // (locked: a buffer may be released from another lane's thread than the one that allocated it)
@@ -147,7 +148,16 @@ struct LaneScope {      // runs this thread's device work on another lane while 
 // the whole call).  Waits for every lane's stream; rethrows the first exception.
 void run_lanes(int n, const std::function<void(int)>& body);
 
-DevicePool& pool();
+DevicePool& pool();  // this thread's allocation pool: its lane's, or the resident pool in a ResidentScope
+// Process-lifetime device data (twiddle and power tables, selector tables, proving keys) comes
+// from one resident pool, not from the lane that happened to build it, so a lane's pool holds
+// exactly its proofs' working set (bfz_device_pool_bytes).
+DevicePool& resident_pool();
+struct ResidentScope {  // DBuf allocations of this thread go to resident_pool() while in scope
+  DevicePool* prev;
+  ResidentScope();
+  ~ResidentScope();
+};
 
 template <class T>
 struct DBuf {  // RAII device buffer from the pool (or a borrowed view of memory owned elsewhere)
@@ -211,6 +221,8 @@ struct Twiddles {
   std::vector<DBuf<uint32_t>> tables_;
 };
 Twiddles& twiddles();
+constexpr int TWIDDLE_LOG_MAX = 24;  // the first ensure() builds this size (two-adicity of KoalaBear)
+std::vector<uint32_t> host_twiddles(int log_n, bool inverse);  // host running products (selftest)
 
 hipStream_t stream();
 // Waits for everything queued on stream() if the stream exists (errors ignored): the C ABI's
@@ -266,7 +278,7 @@ void upload_bulk(void* dst, const void* src, size_t bytes, hipStream_t st);
 // events after the stream has drained.  Event creation is host work, so it is only switched
 // on for the one instrumented proof.
 struct KernelProbe {
-  bool on = false;
+  std::atomic<bool> on{false};  // read by every lane's launches, written by timed proofs
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
   std::vector<double> ev_bytes;
   double ms = 0, bytes = 0;

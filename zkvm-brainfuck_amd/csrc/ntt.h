@@ -19,6 +19,9 @@ void ntt_passes(const uint32_t* src, uint32_t* dst, size_t src_stride, size_t ds
 
 // evals: column-major, bit-reversed rows (n x w).  lde: column-major 2n x w, bit-reversed
 // rows = evaluations of the interpolant on shift * H_2n (shift = GENERATOR / domain shift).
+// Builds (once per process) the twiddle and coset-power tables a proof's LDEs of height 2^L use,
+// so no proof builds a table between its launches (bfz_record_* call it for the record's heights).
+void prepare_lde_tables(int L);
 void coset_lde(const uint32_t* evals, size_t n, int w, uint32_t shift, uint32_t* lde,
                hipStream_t st);
 // The same with the input columns at stride src_stride, and only_half = 0 / 1: write only

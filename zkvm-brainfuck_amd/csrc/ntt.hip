@@ -656,6 +656,7 @@ const uint32_t* scale_tables(uint32_t shift, int L, int B) {
     uint32_t b = ninv;
     for (size_t k = 0; k < nb; k++) { hi[k] = b; b = mmul(b, step); }
   }
+  ResidentScope rs;  // cached for the process, not part of the lane's working set
   DBuf<uint32_t> d(4 * nb);
   // stream-ordered: a pooled buffer may still be read by kernels queued on stream()
   HIP_CHECK(hipMemcpyAsync(d.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, stream()));
@@ -665,6 +666,16 @@ const uint32_t* scale_tables(uint32_t shift, int L, int B) {
   return p;
 }
 }  // namespace
+
+void prepare_lde_tables(int L) {
+  // the coset shifts a proof's LDEs use at height 2^L: GENERATOR / 1 for the traces (prover.hip
+  // lde_into), 1 and w_2n^-1 for the two quotient chunks' other halves
+  const int B = (L + 1) / 2;
+  twiddles().ensure(std::max(L + 1, 1));
+  (void)scale_tables(to_mont(3), L, B);
+  (void)scale_tables(ONE, L, B);
+  (void)scale_tables(minv(two_adic_gen(L + 1)), L, B);
+}
 
 void coset_lde(const uint32_t* evals, size_t n, int w, uint32_t shift, uint32_t* lde,
                hipStream_t st) {
@@ -773,6 +784,7 @@ static const uint32_t* residue_powers(uint32_t a, int L, int B) {
   const uint32_t step = x;  // a^(2^B)
   uint32_t y = minv(to_mont((uint32_t)(((uint64_t)1 << L) % P)));
   for (size_t k = 0; k < nb; k++) { h[nb + k] = y; y = mmul(y, step); }
+  ResidentScope rs;
   DBuf<uint32_t> d(2 * nb);
   HIP_CHECK(hipMemcpyAsync(d.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, stream()));
   HIP_CHECK(hipStreamSynchronize(stream()));

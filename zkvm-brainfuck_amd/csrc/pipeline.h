@@ -20,7 +20,7 @@ struct BatchStats {
 };
 
 // Proofs of `jobs` (stdins of pk.program), in order; byte-identical to prove() per job.
-// inflight: proofs on the GPU at once (1 or 2 lanes, gpu.h Lane).
+// inflight: proofs on the GPU at once (1..MAX_LANES lanes, gpu.h Lane).
 std::vector<std::vector<uint8_t>> prove_batch(const ProvingKey& pk, const std::vector<Job>& jobs,
                                               const ProveOptions& opt, int exec_threads,
                                               int inflight, BatchStats* stats);

@@ -376,6 +376,8 @@ void commit_lde(CMat& cm, const uint32_t* evals, size_t n, int w, uint32_t domai
 
 // ------------------------------------------------------------------------ setup
 std::unique_ptr<ProvingKey> setup(const std::string& src) {
+  ResidentScope rs;  // the key lives beside the tables, outside every lane's working set
+  twiddles().ensure(TWIDDLE_LOG_MAX);  // every transform size a proof can use (device-built)
   auto pk = std::make_unique<ProvingKey>();
   pk->program = Program::parse(src);
   hipStream_t st = stream();
@@ -497,10 +499,8 @@ struct ProofScope {
   ~ProofScope() {  // the pinned upload arena is rewound when the call is done
     (void)hipStreamSynchronize(stream());
     staging_reset();
-    ntt_probe().on = false;
-    p2_probe().on = false;
-    open_probe().on = false;
-    reduce_probe().on = false;
+    if (ev.on)  // disarm only what this scope armed (lanes of untimed proofs read the flags)
+      for (KernelProbe* p : {&ntt_probe(), &p2_probe(), &open_probe(), &reduce_probe()}) p->on = false;
   }
 };
 

@@ -21,6 +21,8 @@ int num_constraints(int chip);
 
 // Writes Q at all 2n points into qout: 8 base columns of n rows (chunk k, coefficient e at
 // column 4k+e), rows in bit-reversed order of the chunk domain.
+// Builds (once per process) the selector-denominator table of the quotient domain 3 H_N, N = 2^logN.
+void prepare_quotient_tables(int logN);
 void quotient(int chip, const uint32_t* mainc, const uint32_t* prepc, const uint32_t* permc,
               int logN, const QuotParams& qp, uint32_t* qout, hipStream_t st);
 

@@ -177,6 +177,7 @@ static const uint32_t* sel_inv_table(int logN, const QuotParams& qp, hipStream_t
   auto it = cache->find(logN);
   if (it != cache->end()) return it->second.p;
   const size_t N = (size_t)1 << logN;
+  ResidentScope rs;  // cached for the process, not part of the lane's working set
   DBuf<uint32_t> d(N);
   hipLaunchKernelGGL(k_sel_inv, dim3(ceil_div(N, 256)), dim3(256), 0, st, logN, qp.shift,
                      qp.wn_inv, (const uint32_t*)twiddles().fwd(), d.p);
@@ -185,6 +186,14 @@ static const uint32_t* sel_inv_table(int logN, const QuotParams& qp, hipStream_t
   const uint32_t* p = d.p;
   cache->emplace(logN, std::move(d));
   return p;
+}
+
+void prepare_quotient_tables(int logN) {
+  twiddles().ensure(logN);
+  QuotParams qp{};  // the fields k_sel_inv reads (prover.hip quotient stage)
+  qp.shift = to_mont(3);
+  qp.wn_inv = minv(two_adic_gen(logN - 1));
+  (void)sel_inv_table(logN, qp, stream());
 }
 
 void quotient(int chip, const uint32_t* mainc, const uint32_t* prepc, const uint32_t* permc,

@@ -47,7 +47,16 @@ Lane& lane() {
 LaneScope::LaneScope(Lane* l) : prev(tl_lane) { tl_lane = l; }
 LaneScope::~LaneScope() { tl_lane = prev; }
 
-DevicePool& pool() { return lane().pool; }
+namespace {
+thread_local DevicePool* tl_pool = nullptr;
+}
+DevicePool& pool() { return tl_pool ? *tl_pool : lane().pool; }
+DevicePool& resident_pool() {
+  static DevicePool* p = new DevicePool();  // lives for the process
+  return *p;
+}
+ResidentScope::ResidentScope() : prev(tl_pool) { tl_pool = &resident_pool(); }
+ResidentScope::~ResidentScope() { tl_pool = prev; }
 
 void run_lanes(int n, const std::function<void(int)>& body) {
   std::exception_ptr err;
@@ -297,33 +306,81 @@ int& api_lock_depth() {
   return depth;
 }
 
+// Level k of the table (h = 2^k, T[h + j] = w_2h^j) is a strided subset of the powers of
+// w_N, N = 2^log_n: w_2h = w_N^(2^(log_n - 1 - k)) (two_adic_gen(b) = g^(2^(24 - b))).  So
+// T[h + j] = w_N^e with e = j << (log_n - 1 - k) < N / 2, one product of two short power tables:
+// w_N^e = lo[e mod 2^12] * hi[e >> 12].  Field products are exact, so the table is the same
+// words as the host's running products (checked by bfz_selftest("twiddles")).
+__global__ __launch_bounds__(256) void k_twiddle_table(uint32_t* __restrict__ fwd,
+                                                       uint32_t* __restrict__ inv, int log_n,
+                                                       const uint32_t* __restrict__ pw, size_t nh) {
+  const size_t N = (size_t)1 << log_n;
+  for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < N;
+       idx += (size_t)gridDim.x * blockDim.x) {
+    if (idx == 0) {
+      fwd[0] = inv[0] = 0;
+      continue;
+    }
+    const int k = 63 - __clzll((unsigned long long)idx);
+    const size_t e = (idx - ((size_t)1 << k)) << (log_n - 1 - k);
+    const size_t lo = e & 4095, hi = e >> 12;
+    fwd[idx] = kb::mmul(pw[lo], pw[4096 + hi]);
+    inv[idx] = kb::mmul(pw[4096 + nh + lo], pw[8192 + nh + hi]);
+  }
+}
+
 void Twiddles::ensure(int log_n) {
   if (log_n <= logmax) return;
   static std::mutex mu;  // lanes may ask at once; an outgrown table stays allocated (another
   std::lock_guard<std::mutex> lk(mu);  // lane's kernels may still read it)
   if (log_n <= logmax) return;
+  if (log_n > 24) throw std::runtime_error("twiddles: KoalaBear's two-adicity is 24");
+  // one build covers every transform a proof can ask for (log 24 = an LDE of a 2^23-row trace):
+  // 2 x 64 MB of HBM, built on the device in well under a millisecond, so no proof ever grows it
+  log_n = std::max(log_n, TWIDDLE_LOG_MAX);
   const size_t N = (size_t)1 << log_n;
-  std::vector<uint32_t> hf(N, 0), hi(N, 0);
-  for (int k = 0; k < log_n; k++) {
-    size_t h = (size_t)1 << k;
-    uint32_t w = kb::two_adic_gen(k + 1), wi = kb::minv(w);
-    uint32_t a = kb::ONE, b = kb::ONE;
-    for (size_t j = 0; j < h; j++) {
-      hf[h + j] = a;
-      hi[h + j] = b;
-      a = kb::mmul(a, w);
-      b = kb::mmul(b, wi);
-    }
+  const size_t nh = std::max<size_t>(1, (N / 2) >> 12);
+  std::vector<uint32_t> pw(2 * (4096 + nh));
+  const uint32_t w = kb::two_adic_gen(log_n), wi = kb::minv(w);
+  for (int dir = 0; dir < 2; dir++) {
+    uint32_t* lo = pw.data() + dir * (4096 + nh);
+    uint32_t* hi = lo + 4096;
+    uint32_t a = kb::ONE;
+    for (size_t j = 0; j < 4096; j++) { lo[j] = a; a = kb::mmul(a, dir ? wi : w); }
+    uint32_t b = kb::ONE;  // a = w^4096 now
+    for (size_t j = 0; j < nh; j++) { hi[j] = b; b = kb::mmul(b, a); }
   }
-  DBuf<uint32_t> nf(N), ni(N);  // stream-ordered: pooled buffers may be read by queued kernels
-  HIP_CHECK(hipMemcpyAsync(nf.p, hf.data(), N * 4, hipMemcpyHostToDevice, stream()));
-  HIP_CHECK(hipMemcpyAsync(ni.p, hi.data(), N * 4, hipMemcpyHostToDevice, stream()));
-  HIP_CHECK(hipStreamSynchronize(stream()));
+  ResidentScope rs;  // process-lifetime tables, not part of any lane's working set
+  DBuf<uint32_t> nf(N), ni(N), dpw(pw.size());
+  const hipStream_t st = stream();
+  HIP_CHECK(hipMemcpyAsync(dpw.p, pw.data(), pw.size() * 4, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_twiddle_table, dim3((unsigned)std::min<size_t>(ceil_div(N, 256), 8192)),
+                     dim3(256), 0, st, nf.p, ni.p, log_n, (const uint32_t*)dpw.p, nh);
+  KCHECK();
+  HIP_CHECK(hipStreamSynchronize(st));
   fwd_.store(nf.p, std::memory_order_release);
   inv_.store(ni.p, std::memory_order_release);
   tables_.push_back(std::move(nf));
   tables_.push_back(std::move(ni));
   logmax.store(log_n, std::memory_order_release);
+}
+
+// The table the way it was built before the device kernel (running products on the host),
+// for bfz_selftest("twiddles").
+std::vector<uint32_t> host_twiddles(int log_n, bool inverse) {
+  const size_t N = (size_t)1 << log_n;
+  std::vector<uint32_t> t(N, 0);
+  for (int k = 0; k < log_n; k++) {
+    const size_t h = (size_t)1 << k;
+    uint32_t w = kb::two_adic_gen(k + 1);
+    if (inverse) w = kb::minv(w);
+    uint32_t a = kb::ONE;
+    for (size_t j = 0; j < h; j++) {
+      t[h + j] = a;
+      a = kb::mmul(a, w);
+    }
+  }
+  return t;
 }
 
 }  // namespace bfz

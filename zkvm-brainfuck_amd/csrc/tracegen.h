@@ -30,7 +30,7 @@ void upload_events(const ExecutionRecord& rec, DeviceEvents& ev, hipStream_t st)
 // one DMA per event array).  Returns when the copies are done.
 void upload_events(const HostEvents& h, const Program& prog, DeviceEvents& ev, hipStream_t st);
 // Chip inclusion, heights and counts of ev from the event counts (the device buffers are set
-// by the caller).
+// by the caller); builds the process-wide tables a proof of these heights reads (prepare_*).
 void set_event_meta(DeviceEvents& ev, const EventCounts& n, uint64_t global_clk);
 // Events that came from outside (bfz_record_from_events): the number of events a kernel must
 // not read -- a cpu pc outside the program (k_trace_cpu / k_deps index by it), an opcode or

@@ -4,6 +4,8 @@
 // contiguous segment.  Column layouts and values follow the host mirror in machine.cpp,
 // which cites the reference's generate_trace for every chip.
 #include "tracegen.h"
+#include "ntt.h"
+#include "quotient.h"
 
 namespace bfz {
 
@@ -329,6 +331,14 @@ void set_event_meta(DeviceEvents& ev, const EventCounts& n, uint64_t global_clk)
     ev.height[c] = main_trace_height(c, n);
   }
   ev.global_clk = global_clk;
+  // every twiddle / coset-power / selector table a proof of these heights reads, built now
+  // (once per process and height) instead of between the first proof's launches
+  for (int c = 0; c < NUM_CHIPS; c++)
+    if (ev.included[c] && ev.height[c]) {
+      const int L = log2i(ev.height[c]);
+      prepare_lde_tables(L);
+      prepare_quotient_tables(L + 1);
+    }
 }
 
 void upload_events(const ExecutionRecord& rec, DeviceEvents& ev, hipStream_t st) {
