@@ -39,6 +39,17 @@ void or_api_ef_inv(const uint32_t a[4], uint32_t out[4]);
 int or_api_perm_trace(int chip, const uint32_t* main, const uint32_t* prep, size_t n,
                       const uint32_t alpha[4], const uint32_t beta[4], uint32_t* out,
                       uint32_t cumsum[4]);
+/* FRI commit-phase helpers shared by the prover and the column-sharded PCS restatement */
+#include "or_hash.h"
+void or_fri_commit_layer(const ef* folded, size_t len, or_merkle* tree);
+void or_fri_fold(const ef* in, size_t len, ef beta, ef* out);
+/* Column-sharded PCS commit + FRI commit phase of one n x w trace (or_pcs.c; the product is
+ * bfz_commit_fri_sharded): root[8], fri_roots[8 * rounds] (at most cap_rounds), *nrounds, fin[4],
+ * and (if challenges is not NULL) alpha then each round's beta, 4 words each.  m: canonical
+ * words, natural row order, row-major.  Returns -1 if the fold is not constant. */
+int or_api_pcs_commit_fri(const uint32_t* m, size_t n, size_t w, uint32_t root[8],
+                          uint32_t* fri_roots, size_t cap_rounds, size_t* nrounds, uint32_t fin[4],
+                          uint32_t* challenges);
 /* sample a challenger transcript: observe `n` values then squeeze `m` samples */
 void or_api_challenger(const uint32_t* obs, size_t n, uint32_t* samples, size_t m);
 

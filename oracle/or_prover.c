@@ -245,6 +245,45 @@ static void quotient(chipdata* cd, const cmat* prep_m, const cmat* main_m, const
   }
 }
 
+/* One FRI commit-phase layer (fri::prover::commit_phase [p3-recalled]): the folded vector of
+ * `len` EF values (bit-reversed order) committed as len/2 leaves, leaf i = the pair (2i, 2i+1)
+ * with each EF flattened to its 4 base coefficients (D5; the D5 alternative interleaves them). */
+void or_fri_commit_layer(const ef* folded, size_t len, or_merkle* tree) {
+  or_mat m;
+  m.values = (fp*)folded;
+  m.height = len / 2;
+  m.width = 8;
+  fp* cm = NULL;
+  if (or_variant.fri_coeff_major) { /* D5 alternative: [a0 b0 a1 b1 a2 b2 a3 b3] per leaf */
+    cm = malloc(sizeof(fp) * 4 * len);
+    for (size_t i = 0; i < len / 2; i++)
+      for (int k = 0; k < 4; k++) {
+        cm[8 * i + 2 * k] = folded[2 * i].c[k];
+        cm[8 * i + 2 * k + 1] = folded[2 * i + 1].c[k];
+      }
+    m.values = cm;
+  }
+  or_merkle_build(tree, &m, 1);
+  tree->mats = NULL; /* m is local: a caller that opens the layer keeps its own matrix */
+  free(cm);
+}
+
+/* The fold of a committed layer with challenge beta (TwoAdicFriFolding::fold_row
+ * [p3-recalled]): out[i] = (1/2 + beta/2 x_i^-1) lo + (1/2 - beta/2 x_i^-1) hi, where (lo, hi) =
+ * (in[2i], in[2i+1]) are the evaluations at +-x_i and x_i = g_{2h}^bitrev(i). */
+void or_fri_fold(const ef* in, size_t len, ef beta, ef* out) {
+  size_t h = len / 2;
+  int lgh = or_log2(h);
+  fp g_inv = fp_inv(fp_two_adic_gen(lgh + 1));
+  fp half = fp_inv(2);
+  ef half_beta = ef_mul_fp(beta, half);
+  for (size_t i = 0; i < h; i++) {
+    ef pw = ef_mul_fp(half_beta, fp_pow(g_inv, or_bitrev(i, lgh)));
+    ef lo = in[2 * i], hi = in[2 * i + 1];
+    out[i] = ef_add(ef_mul(ef_add_fp(pw, half), lo), ef_mul(ef_sub(ef_from_fp(half), pw), hi));
+  }
+}
+
 /* reduced openings + FRI (TwoAdicFriPcs::open, fri::prover::prove) [p3-recalled] */
 typedef struct { int nmats; const cmat* m; int npts[16]; ef pts[16][2]; ef* vals[16][2]; } oround;
 
@@ -294,35 +333,17 @@ static void fri_prove(buf* b, or_challenger* ch, round_t* rounds, oround* orr, i
     R->nmats = 1;
     R->lm = calloc(1, sizeof(or_mat));
     R->lm[0].values = (fp*)folded; /* EF pairs flattened: width 8 base */
-    fp* cm = NULL;
-    if (or_variant.fri_coeff_major) { /* D5 alternative: [a0 b0 a1 b1 a2 b2 a3 b3] per leaf */
-      cm = malloc(sizeof(fp) * 4 * len);
-      for (size_t i = 0; i < len / 2; i++)
-        for (int k = 0; k < 4; k++) {
-          cm[8 * i + 2 * k] = folded[2 * i].c[k];
-          cm[8 * i + 2 * k + 1] = folded[2 * i + 1].c[k];
-        }
-      R->lm[0].values = cm;
-    }
     R->lm[0].height = len / 2;
     R->lm[0].width = 8;
-    or_merkle_build(&R->tree, R->lm, 1);
-    if (cm) { free(cm); R->lm[0].values = (fp*)folded; }
+    or_fri_commit_layer(folded, len, &R->tree);
+    R->tree.mats = R->lm;
     or_ch_observe_digest(ch, R->tree.root);
     ef beta = or_ch_sample_ef(ch);
     betas[ncommit] = beta;
     layers[ncommit] = folded;
     size_t h = len / 2;
-    int lgh = or_log2(h);
-    fp g_inv = fp_inv(fp_two_adic_gen(lgh + 1));
-    fp half = fp_inv(2);
-    ef half_beta = ef_mul_fp(beta, half);
     ef* nf = malloc(sizeof(ef) * h);
-    for (size_t i = 0; i < h; i++) {
-      ef pw = ef_mul_fp(half_beta, fp_pow(g_inv, or_bitrev(i, lgh)));
-      ef lo = folded[2 * i], hi = folded[2 * i + 1];
-      nf[i] = ef_add(ef_mul(ef_add_fp(pw, half), lo), ef_mul(ef_sub(ef_from_fp(half), pw), hi));
-    }
+    or_fri_fold(folded, len, beta, nf);
     folded = nf;
     len = h;
     ncommit++;

@@ -41,6 +41,9 @@ def lib():
                                          ctypes.POINTER(ctypes.c_size_t), ctypes.c_int, P32]
         L.or_api_two_adic_gen.restype = ctypes.c_uint32
         L.or_api_challenger.argtypes = [P32, ctypes.c_size_t, P32, ctypes.c_size_t]
+        L.or_api_pcs_commit_fri.argtypes = [P32, ctypes.c_size_t, ctypes.c_size_t, P32, P32,
+                                            ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t), P32,
+                                            P32]
         L.or_api_setup_root.argtypes = [ctypes.c_char_p, P32]
         L.or_api_perm_trace.argtypes = [ctypes.c_int, P32, P32, ctypes.c_size_t, P32, P32, P32, P32]
         L.or_set_num_queries.argtypes = [ctypes.c_int]
@@ -150,6 +153,31 @@ def merkle_root(mats):
     root = (ctypes.c_uint32 * 8)()
     lib().or_api_merkle_root(ptrs, hs, ws, len(mats), root)
     return list(root)
+
+
+def pcs_commit_fri(m, challenges=False):
+    """Column-sharded PCS restatement (oracle/or_pcs.c): commitment root of the coset LDE of the
+    n x w matrix m (canonical words, natural row order), the FRI commit-phase roots of the
+    batched column sum_c alpha^c col_c, and the final constant -- canonical words.  With
+    challenges=True also (alpha, [beta per round]) as EF word lists."""
+    import numpy as np
+    a = np.ascontiguousarray(m, dtype=np.uint32)
+    n, w = a.shape
+    cap = n.bit_length() + 1
+    root = (ctypes.c_uint32 * 8)()
+    fri = (ctypes.c_uint32 * (8 * cap))()
+    nr = ctypes.c_size_t()
+    fin = (ctypes.c_uint32 * 4)()
+    ch = (ctypes.c_uint32 * (4 + 4 * cap))()
+    rc = lib().or_api_pcs_commit_fri(a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), n, w, root,
+                                     fri, cap, ctypes.byref(nr), fin, ch)
+    if rc == -2:
+        raise MemoryError("oracle pcs: LDE allocation failed")
+    rounds = [list(fri[8 * i: 8 * i + 8]) for i in range(nr.value)]
+    out = (list(root), rounds, list(fin), rc == 0)
+    if challenges:
+        out += ((list(ch[:4]), [list(ch[4 + 4 * i: 8 + 4 * i]) for i in range(nr.value)]),)
+    return out
 
 
 def setup_root(prog: str):

@@ -140,3 +140,47 @@ def test_challenger_duplex_semantics():
     s2 = O.challenger(obs, 1)
     st2 = O.poseidon2(np.array(obs + [0] * 8, dtype=np.uint32)).tolist()
     assert s2 == [st2[7]]
+
+
+def _ef_mul(a, b):
+    """EF = F[x]/(x^4 - 3) (kb31: W = 3), canonical coefficient lists"""
+    r = [0] * 7
+    for i in range(4):
+        for j in range(4):
+            r[i + j] += a[i] * b[j]
+    return [(r[k] + 3 * (r[k + 4] if k + 4 < 7 else 0)) % P for k in range(4)]
+
+
+@pytest.mark.parametrize("logn,w", [(1, 1), (3, 2), (5, 3), (6, 5)])
+def test_oracle_pcs_commit_fri_closed_form(logn, w):
+    """The column-sharded PCS restatement (oracle/or_pcs.c, the checker of bfz_commit_fri_sharded)
+    pinned by an independent closed form: its root is the MerkleTreeMmcs root of the coset LDE
+    (O.merkle_root), it folds to a constant, and the constant is what FRI's fold does to the
+    batched polynomial f = sum_c alpha^c P_c (P_c interpolates column c over H, naive DFT here):
+    each fold keeps f_even + beta f_odd of f(3 y) -- the fold ignores the coset shift -- so
+    final = sum_j F_j 3^j prod_(r: bit r of j) beta_r."""
+    n = 1 << logn
+    rng = np.random.default_rng(1000 + logn)
+    m = rng.integers(0, P, size=(n, w), dtype=np.uint64).astype(np.uint32)
+    root, fri, fin, constant, (alpha, betas) = O.pcs_commit_fri(m, challenges=True)
+    assert constant
+    assert root == O.merkle_root([O.coset_lde(m, 3)])
+    assert len(fri) == len(betas) == logn
+    wn_inv = pow(O.two_adic_gen(logn), P - 2, P)
+    ninv = pow(n, P - 2, P)
+    F = [[0, 0, 0, 0] for _ in range(n)]
+    ap = [1, 0, 0, 0]
+    for c in range(w):
+        col = [int(v) for v in m[:, c]]
+        for k in range(n):
+            ck = sum(col[j] * pow(wn_inv, j * k, P) for j in range(n)) * ninv % P
+            F[k] = [(F[k][e] + ap[e] * ck) % P for e in range(4)]
+        ap = _ef_mul(ap, alpha)
+    want = [0, 0, 0, 0]
+    for j in range(n):
+        t = [F[j][e] * pow(3, j, P) % P for e in range(4)]
+        for r in range(logn):
+            if (j >> r) & 1:
+                t = _ef_mul(t, betas[r])
+        want = [(want[e] + t[e]) % P for e in range(4)]
+    assert fin == want
