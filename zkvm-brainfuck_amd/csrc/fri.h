@@ -39,6 +39,13 @@ struct OpenDesc {
   const uint32_t* mat;
   uint64_t height;
   int w, logH;
+  // two matrices of one height opened at the same points share a descriptor (open_batch merges
+  // them: one weight computation per row for both): columns [0, w1) from mat, [w1, w) from mat2,
+  // opened values to out_a / out_b and out_a2 / out_b2
+  const uint32_t* mat2;
+  int w1;
+  kb::EF* out_a2;
+  kb::EF* out_b2;
   const kb::EF* invd_a;
   const kb::EF* invd_b;  // nullptr: derived from invd_a (w_n^-1 folded into scale_b, see k_reduce)
   kb::EF scale_a, scale_b;

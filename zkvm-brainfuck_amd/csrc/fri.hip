@@ -67,8 +67,17 @@ __global__ __launch_bounds__(256) void k_inv_denoms(EF z, const EF* __restrict__
 }
 
 // ------------------------------------------------------------------ openings
-// 8 rows per thread: 6 and 4 measured 0.08-0.15 ms per proof slower (profiles/r05/ab_open_rows.txt)
-constexpr int OPEN_T = 256, OPEN_R = 8, OPEN_CH = OPEN_T * OPEN_R;
+// Rows per thread: 8 at two points (6 and 4 measured 0.08-0.15 ms per proof slower,
+// profiles/r05/ab_open_rows.txt); 16 at one point, where a row's weights take 4 registers
+// instead of 8 and the per-column lane reduction is paid once per 16 rows.
+#ifndef BFZ_OPEN_R1
+#define BFZ_OPEN_R1 16
+#endif
+constexpr int OPEN_T = 256, OPEN_R2 = 8;
+template <int NP>
+constexpr int open_rows() { return NP == 1 ? BFZ_OPEN_R1 : OPEN_R2; }
+template <int NP>
+constexpr int open_ch() { return OPEN_T * open_rows<NP>(); }
 
 __device__ __forceinline__ EF wave_sum(EF v) {
 #pragma unroll
@@ -93,12 +102,25 @@ __device__ __forceinline__ EF wave_sum(EF v) {
 // FULL: every thread of the chunk has all OPEN_R rows (every chunk of a matrix of >= OPEN_CH
 // low-coset rows): no per-row bounds selects.  Column words come through a buffer descriptor per
 // column with the row step in the scalar offset (no 64-bit VALU address arithmetic per load).
+// The block's reduction buffer, one per kernel: declared in the FULL and the partial-chunk
+// bodies separately it was allocated twice (67.5 KB at two points), which left room for two
+// blocks per CU where the registers allow three.
+template <int NP>
+__device__ __forceinline__ uint32_t* open_lds() {
+  constexpr int NSUM = NP * 16, PER = OPEN_T / NSUM, RS = OPEN_T + PER;
+  __shared__ uint32_t red[NSUM * RS];
+  return red;
+}
+
 template <int NP, bool TAB, bool FULL>
-__device__ __forceinline__ void open_tile_body(const uint32_t* __restrict__ mat, size_t height, int w,
+__device__ __forceinline__ void open_tile_body(const uint32_t* __restrict__ mat,
+                                               const uint32_t* __restrict__ mat2, int w1,
+                                               size_t height, int w,
                                                size_t n, int logH, const EF* __restrict__ invd_a,
                                                const EF* __restrict__ invd_b,
                                                const uint32_t* __restrict__ twf,
                                                EF* __restrict__ partial, unsigned chunk) {
+  constexpr int OPEN_R = open_rows<NP>(), OPEN_CH = open_ch<NP>();
   const size_t c0 = (size_t)chunk * OPEN_CH + threadIdx.x;
   const int nr = FULL ? OPEN_R : c0 >= n ? 0 : (int)min((size_t)OPEN_R, (n - c0 + OPEN_T - 1) / OPEN_T);
   EF W[NP][OPEN_R];
@@ -122,27 +144,32 @@ __device__ __forceinline__ void open_tile_body(const uint32_t* __restrict__ mat,
       W[k][r] = r < nr ? ef_mul_base(ld_global(tab, tk), x) : ef_zero();
     }
   }
+  auto colp = [&](int c) {  // column c of the descriptor (a second matrix from column w1 on)
+    return c < w1 ? mat + (size_t)c * height : mat2 + (size_t)(c - w1) * height;
+  };
   auto load = [&](int c, uint32_t (&v)[OPEN_R]) {
     if constexpr (FULL) {
-      const __amdgpu_buffer_rsrc_t rc = rsrc_of(mat + (size_t)c * height + (size_t)chunk * OPEN_CH);
+      const __amdgpu_buffer_rsrc_t rc = rsrc_of(colp(c) + (size_t)chunk * OPEN_CH);
 #pragma unroll
       for (int r = 0; r < OPEN_R; r++) v[r] = ld_b(rc, threadIdx.x * 4u, (uint32_t)(r * OPEN_T) * 4u);
     } else {
-      const uint32_t* col = mat + (size_t)c * height + c0;
+      const uint32_t* col = colp(c) + c0;
 #pragma unroll
       for (int r = 0; r < OPEN_R; r++) v[r] = r < nr ? ld_global(col, (size_t)r * OPEN_T) : 0u;
     }
   };
-  // four column buffers in a ring: three columns stay in flight while one is consumed
-  uint32_t vr[4][OPEN_R];
+  // column buffers in a ring: RING - 1 columns stay in flight while one is consumed (four of 8
+  // rows; two of 16 rows hold as many loads in flight in half the registers)
+  constexpr int RING = OPEN_R > 8 ? 2 : 4;
+  uint32_t vr[RING][OPEN_R];
 #pragma unroll
-  for (int j = 0; j < 4; j++)
+  for (int j = 0; j < RING; j++)
     if (j < w) load(j, vr[j]);
   constexpr int NSUM = NP * 16, PER = OPEN_T / NSUM;  // sums per group, threads per sum
   // row stride OPEN_T + PER: the PER-strided reads of the 32 / PER sums a half-wave adds up
   // land in distinct banks (stride OPEN_T put 32 / PER of them in each bank; kernel -1.6%)
   constexpr int RS = OPEN_T + PER;
-  __shared__ uint32_t red[NSUM * RS];  // [(k * 4 + col) * 4 + coef][thread]
+  uint32_t* red = open_lds<NP>();  // [(k * 4 + col) * 4 + coef][thread]
   for (int c = 0; c < w; c += 4) {
 #pragma unroll
     for (int j = 0; j < 4; j++) {
@@ -152,12 +179,12 @@ __device__ __forceinline__ void open_tile_body(const uint32_t* __restrict__ mat,
           LazyEF lz;
           lz.init();
 #pragma unroll
-          for (int r = 0; r < OPEN_R; r++) lz.add(W[k][r], vr[j][r]);
+          for (int r = 0; r < OPEN_R; r++) lz.add(W[k][r], vr[j % RING][r]);
           const EF acc = lz.get();
 #pragma unroll
           for (int e = 0; e < 4; e++) red[((k * 4 + j) * 4 + e) * RS + threadIdx.x] = acc.c[e];
         }
-        if (c + j + 4 < w) load(c + j + 4, vr[j]);
+        if (c + j + RING < w) load(c + j + RING, vr[j % RING]);
       }
     }
     __syncthreads();
@@ -181,15 +208,18 @@ __device__ __forceinline__ void open_tile_body(const uint32_t* __restrict__ mat,
 }
 
 template <int NP, bool TAB>
-__device__ __forceinline__ void open_tile(const uint32_t* __restrict__ mat, size_t height, int w,
-                                          size_t n, int logH, const EF* __restrict__ invd_a,
+__device__ __forceinline__ void open_tile(const uint32_t* __restrict__ mat,
+                                          const uint32_t* __restrict__ mat2, int w1, size_t height,
+                                          int w, size_t n, int logH, const EF* __restrict__ invd_a,
                                           const EF* __restrict__ invd_b,
                                           const uint32_t* __restrict__ twf,
                                           EF* __restrict__ partial, unsigned chunk) {
-  if ((size_t)(chunk + 1) * OPEN_CH <= n)  // uniform across the block
-    open_tile_body<NP, TAB, true>(mat, height, w, n, logH, invd_a, invd_b, twf, partial, chunk);
+  if ((size_t)(chunk + 1) * open_ch<NP>() <= n)  // uniform across the block
+    open_tile_body<NP, TAB, true>(mat, mat2, w1, height, w, n, logH, invd_a, invd_b, twf, partial,
+                                  chunk);
   else
-    open_tile_body<NP, TAB, false>(mat, height, w, n, logH, invd_a, invd_b, twf, partial, chunk);
+    open_tile_body<NP, TAB, false>(mat, mat2, w1, height, w, n, logH, invd_a, invd_b, twf, partial,
+                                   chunk);
 }
 
 template <int NP, bool TAB = false>
@@ -199,7 +229,7 @@ __global__ __launch_bounds__(OPEN_T) void k_open_partial(const uint32_t* __restr
                                                          const EF* __restrict__ invd_b,
                                                          const uint32_t* __restrict__ twf,
                                                          EF* __restrict__ partial) {
-  open_tile<NP, TAB>(mat, height, w, n, logH, invd_a, invd_b, twf, partial, blockIdx.x);
+  open_tile<NP, TAB>(mat, mat, w, height, w, n, logH, invd_a, invd_b, twf, partial, blockIdx.x);
 }
 
 // Batched barycentric openings: block b works on chunk (b - chunk0) of the matrix whose block
@@ -212,8 +242,8 @@ __global__ __launch_bounds__(OPEN_T) void k_open_partial_batch(const OpenDesc* _
   int m = 0;
   while (m + 1 < nd && d[m + 1].chunk0 <= blockIdx.x) m++;
   const OpenDesc& o = d[m];
-  open_tile<NP, false>(o.mat, o.height, o.w, o.height / 2, o.logH, o.invd_a, o.invd_b, twf,
-                       partial + o.part_off, blockIdx.x - o.chunk0);
+  open_tile<NP, false>(o.mat, o.mat2, o.w1, o.height, o.w, o.height / 2, o.logH, o.invd_a, o.invd_b,
+                       twf, partial + o.part_off, blockIdx.x - o.chunk0);
 }
 
 // out_k[c] = scale_k * sum_chunks partial[(chunk * w + c) * NP + k]   (one block per column)
@@ -264,8 +294,10 @@ __global__ __launch_bounds__(256) void k_open_final_batch(const OpenDesc* __rest
     sb = ef_mul_base(sa, o.zb);
   }
   // the partial sums are of x_t invd_k[t] col[t]: the weight's sign goes into the scale
-  open_final<NP>(partial + o.part_off, (int)o.nchunks, o.w, (int)(blockIdx.x - o.col0), ef_neg(sa),
-                 ef_neg(sb), o.out_a, o.out_b);
+  const int c = (int)(blockIdx.x - o.col0);
+  const bool second = c >= o.w1;  // a merged descriptor's second matrix: its own outputs
+  open_final<NP>(partial + o.part_off, (int)o.nchunks, o.w, c, ef_neg(sa), ef_neg(sb),
+                 second ? o.out_a2 - o.w1 : o.out_a, second ? o.out_b2 - o.w1 : o.out_b);
 }
 
 // ------------------------------------------------------------------ reduced openings
@@ -619,8 +651,8 @@ void pow_table(const EF& z, size_t j0, size_t count, EF* out, hipStream_t st) {
 void open_coefficients(const uint32_t* coef, size_t col_stride, int w, size_t count,
                        const EF* tab_a, const EF& scale_a, EF* out_a, const EF* tab_b,
                        const EF& scale_b, EF* out_b, hipStream_t st) {
-  const int nchunks = (int)ceil_div(count, OPEN_CH);
   const int np = tab_b ? 2 : 1;
+  const int nchunks = (int)ceil_div(count, np == 2 ? open_ch<2>() : open_ch<1>());
   DBuf<EF> partial((size_t)nchunks * w * np);
   if (np == 2) {
     hipLaunchKernelGGL((k_open_partial<2, true>), dim3(nchunks), dim3(OPEN_T), 0, st, coef,
@@ -638,12 +670,40 @@ void open_coefficients(const uint32_t* coef, size_t col_stride, int w, size_t co
   KCHECK();
 }
 
-void open_batch(std::vector<OpenDesc>& ds, int np, hipStream_t st) {
-  if (ds.empty()) return;
+// Two descriptors of one LDE height opened at the same points read the same weights: one
+// descriptor for both (each keeps its own outputs).
+static bool mergeable(const OpenDesc& a, const OpenDesc& b) {
+  return !a.mat2 && !b.mat2 && a.height == b.height && a.logH == b.logH && a.invd_a == b.invd_a &&
+         a.invd_b == b.invd_b && a.zeta == b.zeta && a.zlog == b.zlog && a.z3n == b.z3n &&
+         a.zc == b.zc && a.zb == b.zb && ef_eq(a.scale_a, b.scale_a) && ef_eq(a.scale_b, b.scale_b);
+}
+
+void open_batch(std::vector<OpenDesc>& in, int np, hipStream_t st) {
+  if (in.empty()) return;
+  static const bool merge = [] {  // BFZ_OPEN_MERGE=0: one descriptor per matrix (A/B)
+    const char* e = std::getenv("BFZ_OPEN_MERGE");
+    return !(e && *e == '0');
+  }();
+  std::vector<OpenDesc> ds;
+  for (const OpenDesc& o : in) {
+    if (merge && !ds.empty() && mergeable(ds.back(), o)) {
+      OpenDesc& m = ds.back();
+      m.mat2 = o.mat;
+      m.w1 = m.w;
+      m.w += o.w;
+      m.out_a2 = o.out_a;
+      m.out_b2 = o.out_b;
+      continue;
+    }
+    ds.push_back(o);
+    ds.back().mat2 = nullptr;
+    ds.back().w1 = o.w;
+  }
+  const uint32_t och = np == 2 ? open_ch<2>() : open_ch<1>();
   uint32_t chunks = 0, cols = 0;
   uint64_t part = 0;
   for (OpenDesc& o : ds) {
-    o.nchunks = ceil_div(o.height / 2, OPEN_CH);
+    o.nchunks = ceil_div(o.height / 2, och);
     o.chunk0 = chunks;
     o.col0 = cols;
     o.part_off = part;
@@ -676,7 +736,7 @@ void open_batch(std::vector<OpenDesc>& ds, int np, hipStream_t st) {
     hipLaunchKernelGGL(k_open_partial_batch<1>, dim3(chunks), dim3(OPEN_T), 0, st, dd.p, nd, twf,
                        partial.p);
   KCHECK();
-  if (probe.on) probe.end(ev0, st, obytes);
+  if (probe.on) probe.end(ev0, st, obytes, np == 2 ? "k_open_partial_batch<2>" : "k_open_partial_batch<1>");
   if (np == 2)
     hipLaunchKernelGGL(k_open_final_batch<2>, dim3(cols), dim3(256), 0, st, dd.p, nd, partial.p);
   else
