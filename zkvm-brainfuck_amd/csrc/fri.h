@@ -51,7 +51,8 @@ struct OpenDesc {
   kb::EF scale_a, scale_b;
   kb::EF* out_a;
   kb::EF* out_b;
-  uint32_t chunk0, col0, nchunks, pad;
+  uint32_t chunk0, col0, nchunks, nslab;  // first block, first column, row chunks, column slabs
+  int slab_w;                              // columns per slab (a multiple of 4)
   uint64_t part_off;
   // zeta != nullptr: the point lives on the device (sampled there) and k_open_final_batch
   // computes the scales itself: scale_a = (zeta^n - 3^n) * zc with n = 2^zlog, zc = 1/(3^n n);

@@ -73,7 +73,10 @@ __global__ __launch_bounds__(256) void k_inv_denoms(EF z, const EF* __restrict__
 #ifndef BFZ_OPEN_R1
 #define BFZ_OPEN_R1 16
 #endif
-constexpr int OPEN_T = 256, OPEN_R2 = 8;
+#ifndef BFZ_OPEN_R2
+#define BFZ_OPEN_R2 8
+#endif
+constexpr int OPEN_T = 256, OPEN_R2 = BFZ_OPEN_R2;
 template <int NP>
 constexpr int open_rows() { return NP == 1 ? BFZ_OPEN_R1 : OPEN_R2; }
 template <int NP>
@@ -119,7 +122,8 @@ __device__ __forceinline__ void open_tile_body(const uint32_t* __restrict__ mat,
                                                size_t n, int logH, const EF* __restrict__ invd_a,
                                                const EF* __restrict__ invd_b,
                                                const uint32_t* __restrict__ twf,
-                                               EF* __restrict__ partial, unsigned chunk) {
+                                               EF* __restrict__ partial, unsigned chunk, int cb,
+                                               int ce) {
   constexpr int OPEN_R = open_rows<NP>(), OPEN_CH = open_ch<NP>();
   const size_t c0 = (size_t)chunk * OPEN_CH + threadIdx.x;
   const int nr = FULL ? OPEN_R : c0 >= n ? 0 : (int)min((size_t)OPEN_R, (n - c0 + OPEN_T - 1) / OPEN_T);
@@ -164,16 +168,16 @@ __device__ __forceinline__ void open_tile_body(const uint32_t* __restrict__ mat,
   uint32_t vr[RING][OPEN_R];
 #pragma unroll
   for (int j = 0; j < RING; j++)
-    if (j < w) load(j, vr[j]);
+    if (cb + j < ce) load(cb + j, vr[j]);
   constexpr int NSUM = NP * 16, PER = OPEN_T / NSUM;  // sums per group, threads per sum
   // row stride OPEN_T + PER: the PER-strided reads of the 32 / PER sums a half-wave adds up
   // land in distinct banks (stride OPEN_T put 32 / PER of them in each bank; kernel -1.6%)
   constexpr int RS = OPEN_T + PER;
   uint32_t* red = open_lds<NP>();  // [(k * 4 + col) * 4 + coef][thread]
-  for (int c = 0; c < w; c += 4) {
+  for (int c = cb; c < ce; c += 4) {
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      if (c + j < w) {
+      if (c + j < ce) {
 #pragma unroll
         for (int k = 0; k < NP; k++) {
           LazyEF lz;
@@ -184,7 +188,7 @@ __device__ __forceinline__ void open_tile_body(const uint32_t* __restrict__ mat,
 #pragma unroll
           for (int e = 0; e < 4; e++) red[((k * 4 + j) * 4 + e) * RS + threadIdx.x] = acc.c[e];
         }
-        if (c + j + RING < w) load(c + j + RING, vr[j % RING]);
+        if (c + j + RING < ce) load(c + j + RING, vr[j % RING]);
       }
     }
     __syncthreads();
@@ -201,7 +205,7 @@ __device__ __forceinline__ void open_tile_body(const uint32_t* __restrict__ mat,
 #pragma unroll
       for (int off = 1; off < PER; off <<= 1) v = madd(v, __shfl_xor(v, off, 64));
       const int k = q / 16, j = (q / 4) % 4, e = q % 4;
-      if (part == 0 && c + j < w) partial[((size_t)chunk * w + c + j) * NP + k].c[e] = v;
+      if (part == 0 && c + j < ce) partial[((size_t)chunk * w + c + j) * NP + k].c[e] = v;
     }
     __syncthreads();
   }
@@ -213,13 +217,13 @@ __device__ __forceinline__ void open_tile(const uint32_t* __restrict__ mat,
                                           int w, size_t n, int logH, const EF* __restrict__ invd_a,
                                           const EF* __restrict__ invd_b,
                                           const uint32_t* __restrict__ twf,
-                                          EF* __restrict__ partial, unsigned chunk) {
+                                          EF* __restrict__ partial, unsigned chunk, int cb, int ce) {
   if ((size_t)(chunk + 1) * open_ch<NP>() <= n)  // uniform across the block
     open_tile_body<NP, TAB, true>(mat, mat2, w1, height, w, n, logH, invd_a, invd_b, twf, partial,
-                                  chunk);
+                                  chunk, cb, ce);
   else
     open_tile_body<NP, TAB, false>(mat, mat2, w1, height, w, n, logH, invd_a, invd_b, twf, partial,
-                                   chunk);
+                                   chunk, cb, ce);
 }
 
 template <int NP, bool TAB = false>
@@ -229,7 +233,7 @@ __global__ __launch_bounds__(OPEN_T) void k_open_partial(const uint32_t* __restr
                                                          const EF* __restrict__ invd_b,
                                                          const uint32_t* __restrict__ twf,
                                                          EF* __restrict__ partial) {
-  open_tile<NP, TAB>(mat, mat, w, height, w, n, logH, invd_a, invd_b, twf, partial, blockIdx.x);
+  open_tile<NP, TAB>(mat, mat, w, height, w, n, logH, invd_a, invd_b, twf, partial, blockIdx.x, 0, w);
 }
 
 // Batched barycentric openings: block b works on chunk (b - chunk0) of the matrix whose block
@@ -242,8 +246,11 @@ __global__ __launch_bounds__(OPEN_T) void k_open_partial_batch(const OpenDesc* _
   int m = 0;
   while (m + 1 < nd && d[m + 1].chunk0 <= blockIdx.x) m++;
   const OpenDesc& o = d[m];
+  // the matrix's blocks: chunk-major, o.nslab column slabs of o.slab_w columns per row chunk
+  const unsigned b = blockIdx.x - o.chunk0, slab = b % o.nslab;
+  const int cb = (int)slab * o.slab_w, ce = min(o.w, cb + o.slab_w);
   open_tile<NP, false>(o.mat, o.mat2, o.w1, o.height, o.w, o.height / 2, o.logH, o.invd_a, o.invd_b,
-                       twf, partial + o.part_off, blockIdx.x - o.chunk0);
+                       twf, partial + o.part_off, b / o.nslab, cb, ce);
 }
 
 // out_k[c] = scale_k * sum_chunks partial[(chunk * w + c) * NP + k]   (one block per column)
@@ -700,14 +707,28 @@ void open_batch(std::vector<OpenDesc>& in, int np, hipStream_t st) {
     ds.back().w1 = o.w;
   }
   const uint32_t och = np == 2 ? open_ch<2>() : open_ch<1>();
+  // A launch of few row chunks (short or merged matrices, 16 rows per thread at one point) splits
+  // the columns of each chunk over several blocks, so it still fills the GPU; each slab of a
+  // chunk computes the chunk's weights itself.
+  uint64_t nch = 0;
+  for (const OpenDesc& o : ds) nch += ceil_div(o.height / 2, och);
+  static const uint64_t FILL = [] {  // blocks: 8 per CU (BFZ_OPEN_FILL=0: no slabs, A/B)
+    const char* e = std::getenv("BFZ_OPEN_FILL");
+    return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)2048;
+  }();
+  const uint32_t want = nch >= FILL ? 1u : (uint32_t)((FILL + nch - 1) / nch);
   uint32_t chunks = 0, cols = 0;
   uint64_t part = 0;
   for (OpenDesc& o : ds) {
     o.nchunks = ceil_div(o.height / 2, och);
+    const uint32_t groups = ceil_div(o.w, 4);  // 4-column reduction groups
+    o.nslab = std::min(groups, want);
+    o.slab_w = 4 * (int)ceil_div(groups, o.nslab);
+    o.nslab = ceil_div(o.w, o.slab_w);
     o.chunk0 = chunks;
     o.col0 = cols;
     o.part_off = part;
-    chunks += o.nchunks;
+    chunks += o.nchunks * o.nslab;
     cols += (uint32_t)o.w;
     part += (uint64_t)o.nchunks * o.w * np;
   }

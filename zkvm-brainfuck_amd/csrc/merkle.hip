@@ -117,14 +117,6 @@ __global__ __launch_bounds__(256) void k_compress(const uint32_t* __restrict__ p
   store8(out + 8 * j, st);
 }
 
-// Medium layers in one launch: a block takes MULTI_NODES consecutive nodes of the first layer
-// (children read from HBM) and builds the next tl.n - 1 layers of its subtree from LDS, one
-// thread per node (MULTI_NODES >> l threads at layer l), every digest also written to HBM.
-// A layer of 2^15 - 2^18 nodes run as a launch of its own is dominated by the launch's ramp
-// and tail (11 us for 2^15 nodes, where the permutations take ~5 us: profiles/r04/
-// probe_p2_rates.txt); here a block goes on to the next layer as soon as its own nodes are done.
-constexpr int MULTI_NODES = 256;
-constexpr size_t MULTI_FIRST_MAX = (size_t)1 << 18;  // first layer of a multi-layer launch
 // Merkle node j in lane mode (see poseidon2_permute_lane): lane l of the node's 16-lane row
 // holds word l of the state; the digest ends up in lanes 0..7.
 __device__ __forceinline__ uint32_t merkle_node_lane(uint32_t v, const ColList& cl, int c0, int c1,
@@ -201,34 +193,6 @@ __global__ __launch_bounds__(1024) void k_compress_top(const uint32_t* __restric
       rc.state[lane] = v;
       if (lane >= 4 && lane < 8) rc.beta->c[7 - lane] = v;
     }
-  }
-}
-
-__global__ __launch_bounds__(MULTI_NODES) void k_compress_multi(const uint32_t* __restrict__ prev,
-                                                               ColList inj, TopLayers tl) {
-  __shared__ uint4 buf[2][MULTI_NODES * 2];  // a layer's digests of this block (8 words each)
-  for (int l = 0; l < tl.n; l++) {
-    const int m = MULTI_NODES >> l;
-    const size_t g = (size_t)blockIdx.x * m + threadIdx.x;  // this thread's node
-    if ((int)threadIdx.x < m) {
-      uint32_t st[16];
-      if (l == 0) {
-        load16(st, prev + 16 * g);
-      } else {
-        const uint4* s = &buf[(l - 1) & 1][4 * threadIdx.x];
-        const uint4 a = s[0], b = s[1], c = s[2], d = s[3];
-        st[0] = a.x; st[1] = a.y; st[2] = a.z; st[3] = a.w;
-        st[4] = b.x; st[5] = b.y; st[6] = b.z; st[7] = b.w;
-        st[8] = c.x; st[9] = c.y; st[10] = c.z; st[11] = c.w;
-        st[12] = d.x; st[13] = d.y; st[14] = d.z; st[15] = d.w;
-      }
-      merkle_node(st, inj, tl.c0[l], tl.c1[l], g);
-      store8(tl.out[l] + 8 * g, st);
-      uint4* o = &buf[l & 1][2 * threadIdx.x];
-      o[0] = make_uint4(st[0], st[1], st[2], st[3]);
-      o[1] = make_uint4(st[4], st[5], st[6], st[7]);
-    }
-    __syncthreads();
   }
 }
 
@@ -334,39 +298,8 @@ static void build_layers(MerkleTree& t, int L0, size_t len, const std::vector<co
                          RootChallenge rc = {}) {
   const int nl = (int)t.layers.size() - 1;
   int L = L0;
-  static const bool multi = [] {  // BFZ_MERKLE_MULTI=0: one launch per layer (A/B)
-    const char* e = std::getenv("BFZ_MERKLE_MULTI");
-    return !(e && *e == '0');
-  }();
   for (; L <= nl && (len >> 1) > LANE_LAYER_MAX; L++) {  // throughput layers
     const size_t nlen = len >> 1;
-    if (multi && nlen <= MULTI_FIRST_MAX) {  // the layers down to 2 LANE_LAYER_MAX in one launch
-      TopLayers tl{};
-      tl.n = std::min(log2i(nlen) - log2i(LANE_LAYER_MAX), nl - L + 1);
-      std::vector<const MatRef*> all;
-      size_t ln = nlen;
-      double perms = 0;
-      for (int l = 0; l < tl.n; l++, ln >>= 1) {
-        tl.c0[l] = 0;
-        for (const MatRef* m : all) tl.c0[l] += m->width;
-        while (next < sorted.size() && sorted[next]->height == ln) all.push_back(sorted[next++]);
-        tl.c1[l] = 0;
-        for (const MatRef* m : all) tl.c1[l] += m->width;
-        t.layers[L + l].reset(8 * ln);
-        tl.out[l] = t.layers[L + l].p;
-        const int w = tl.c1[l] - tl.c0[l];
-        perms += (double)ln * (w ? 2 + (w + 7) / 8 : 1);
-      }
-      KernelProbe& probe = p2_probe();
-      hipEvent_t ev0 = probe.on ? probe.begin(st) : nullptr;
-      hipLaunchKernelGGL(k_compress_multi, dim3((unsigned)(nlen / MULTI_NODES)), dim3(MULTI_NODES), 0,
-                         st, (const uint32_t*)t.layers[L - 1].p, make_cols(all), tl);
-      KCHECK();
-      if (probe.on) probe.end(ev0, st, perms, "k_compress_multi");
-      L += tl.n - 1;  // (the loop adds the last one)
-      len = nlen >> (tl.n - 1);
-      continue;
-    }
     std::vector<const MatRef*> grp;
     while (next < sorted.size() && sorted[next]->height == nlen) grp.push_back(sorted[next++]);
     t.layers[L].reset(8 * nlen);
