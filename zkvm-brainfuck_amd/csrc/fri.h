@@ -46,6 +46,9 @@ struct OpenDesc {
   int w1;
   kb::EF* out_a2;
   kb::EF* out_b2;
+  // wtab != nullptr: the weights x_t / (x_t - z) are read from this table (inv_denoms_dev's wout)
+  // for both points (the second at t', see open_tile_body) and zb must be 1
+  const kb::EF* wtab;
   const kb::EF* invd_a;
   const kb::EF* invd_b;  // nullptr: derived from invd_a (w_n^-1 folded into scale_b, see k_reduce)
   kb::EF scale_a, scale_b;
@@ -65,7 +68,9 @@ struct OpenDesc {
 // their row chunks, one final launch over all of their columns.
 void open_batch(std::vector<OpenDesc>& ds, int np, hipStream_t st);
 // 1 / (x_t - z) over the whole 2^logH coset with z read from device memory (sampled there)
-void inv_denoms_dev(const kb::EF* z, int logH, kb::EF* out, hipStream_t st);
+// wout != nullptr: also the low coset's barycentric weights x_t / (x_t - z), t < 2^(logH-1)
+// (every smaller height's low coset is a prefix, as for out)
+void inv_denoms_dev(const kb::EF* z, int logH, kb::EF* out, hipStream_t st, kb::EF* wout = nullptr);
 // ro[t] = (sum_c ca_c v_c[t] - ya) invd_a[t] + (sum_m kb_m sum_(c in m) ca_c v_c[t] - yb) invd_b[t]
 // for the positions [t0, t0 + count) of a height-`height` LDE (all of it, or a shard's range);
 // cols / mats: device descriptor arrays of one height (RedMat::first indexes cols); every

@@ -38,20 +38,25 @@ constexpr int INV_CHUNK = 8;
 
 // out[t - t0] = 1 / (x_t - z) for t in [t0, t0 + count)
 // zp != nullptr: the point is read from device memory (sampled on the device)
+// wout != nullptr: also the barycentric weights wout[t - t0] = x_t / (x_t - z) for t < wcount
+// (the openings' weight table, see open_tile_body)
 __global__ __launch_bounds__(256) void k_inv_denoms(EF z, const EF* __restrict__ zp, int logH,
                                                     size_t t0, size_t count,
                                                     const uint32_t* __restrict__ twf,
-                                                    EF* __restrict__ out) {
+                                                    EF* __restrict__ out, EF* __restrict__ wout,
+                                                    size_t wcount) {
   const size_t base = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * INV_CHUNK;
   if (base >= count) return;
   if (zp) z = *zp;
   EF d[INV_CHUNK], pre[INV_CHUNK];
+  uint32_t xs[INV_CHUNK];
   const int cnt = (int)min((size_t)INV_CHUNK, count - base);
   EF run = ef_one();
 #pragma unroll
   for (int k = 0; k < INV_CHUNK; k++) {
     if (k < cnt) {
-      d[k] = ef_sub(ef_base(coset_point((uint32_t)(t0 + base + k), logH, twf)), z);
+      xs[k] = coset_point((uint32_t)(t0 + base + k), logH, twf);
+      d[k] = ef_sub(ef_base(xs[k]), z);
       run = ef_mul(run, d[k]);
     }
     pre[k] = run;
@@ -60,7 +65,9 @@ __global__ __launch_bounds__(256) void k_inv_denoms(EF z, const EF* __restrict__
 #pragma unroll
   for (int k = INV_CHUNK - 1; k >= 0; k--) {
     if (k < cnt) {
-      out[base + k] = k ? ef_mul(inv, pre[k - 1]) : inv;
+      const EF r = k ? ef_mul(inv, pre[k - 1]) : inv;
+      out[base + k] = r;
+      if (wout && base + k < wcount) wout[base + k] = ef_mul_base(r, xs[k]);
       inv = ef_mul(inv, d[k]);
     }
   }
@@ -123,7 +130,7 @@ __device__ __forceinline__ void open_tile_body(const uint32_t* __restrict__ mat,
                                                const EF* __restrict__ invd_b,
                                                const uint32_t* __restrict__ twf,
                                                EF* __restrict__ partial, unsigned chunk, int cb,
-                                               int ce) {
+                                               int ce, const EF* __restrict__ wtab) {
   constexpr int OPEN_R = open_rows<NP>(), OPEN_CH = open_ch<NP>();
   const size_t c0 = (size_t)chunk * OPEN_CH + threadIdx.x;
   const int nr = FULL ? OPEN_R : c0 >= n ? 0 : (int)min((size_t)OPEN_R, (n - c0 + OPEN_T - 1) / OPEN_T);
@@ -134,6 +141,13 @@ __device__ __forceinline__ void open_tile_body(const uint32_t* __restrict__ mat,
     if (TAB) {
 #pragma unroll
       for (int k = 0; k < NP; k++) W[k][r] = r < nr ? ld_global(k ? invd_b : invd_a, t) : ef_zero();
+      continue;
+    }
+    if (wtab) {  // weights x_t / (x_t - z) from k_inv_denoms; the second point z w_n reads the
+                 // first's at t' (natural index i - 2): x_t / (x_t - z w_n) = x_t' / (x_t' - z)
+#pragma unroll
+      for (int k = 0; k < NP; k++)
+        W[k][r] = r < nr ? ld_global(wtab, k ? prev2_pos(t, logH) : t) : ef_zero();
       continue;
     }
     const uint32_t x = r < nr ? coset_point((uint32_t)t, logH, twf) : 0u;
@@ -217,13 +231,14 @@ __device__ __forceinline__ void open_tile(const uint32_t* __restrict__ mat,
                                           int w, size_t n, int logH, const EF* __restrict__ invd_a,
                                           const EF* __restrict__ invd_b,
                                           const uint32_t* __restrict__ twf,
-                                          EF* __restrict__ partial, unsigned chunk, int cb, int ce) {
+                                          EF* __restrict__ partial, unsigned chunk, int cb, int ce,
+                                          const EF* __restrict__ wtab = nullptr) {
   if ((size_t)(chunk + 1) * open_ch<NP>() <= n)  // uniform across the block
     open_tile_body<NP, TAB, true>(mat, mat2, w1, height, w, n, logH, invd_a, invd_b, twf, partial,
-                                  chunk, cb, ce);
+                                  chunk, cb, ce, wtab);
   else
     open_tile_body<NP, TAB, false>(mat, mat2, w1, height, w, n, logH, invd_a, invd_b, twf, partial,
-                                   chunk, cb, ce);
+                                   chunk, cb, ce, wtab);
 }
 
 template <int NP, bool TAB = false>
@@ -250,7 +265,7 @@ __global__ __launch_bounds__(OPEN_T) void k_open_partial_batch(const OpenDesc* _
   const unsigned b = blockIdx.x - o.chunk0, slab = b % o.nslab;
   const int cb = (int)slab * o.slab_w, ce = min(o.w, cb + o.slab_w);
   open_tile<NP, false>(o.mat, o.mat2, o.w1, o.height, o.w, o.height / 2, o.logH, o.invd_a, o.invd_b,
-                       twf, partial + o.part_off, b / o.nslab, cb, ce);
+                       twf, partial + o.part_off, b / o.nslab, cb, ce, o.wtab);
 }
 
 // out_k[c] = scale_k * sum_chunks partial[(chunk * w + c) * NP + k]   (one block per column)
@@ -636,16 +651,18 @@ void inv_denoms_range(const EF& z, int logH, size_t t0, size_t count, EF* out, h
   twiddles().ensure(std::max(logH, 1));
   const size_t nthreads = (count + INV_CHUNK - 1) / INV_CHUNK;
   hipLaunchKernelGGL(k_inv_denoms, dim3(ceil_div(nthreads, 256)), dim3(256), 0, st, z,
-                     (const EF*)nullptr, logH, t0, count, (const uint32_t*)twiddles().fwd(), out);
+                     (const EF*)nullptr, logH, t0, count, (const uint32_t*)twiddles().fwd(), out,
+                     (EF*)nullptr, (size_t)0);
   KCHECK();
 }
 
-void inv_denoms_dev(const EF* z, int logH, EF* out, hipStream_t st) {
+void inv_denoms_dev(const EF* z, int logH, EF* out, hipStream_t st, EF* wout) {
   twiddles().ensure(std::max(logH, 1));
   const size_t count = (size_t)1 << logH;
   const size_t nthreads = (count + INV_CHUNK - 1) / INV_CHUNK;
   hipLaunchKernelGGL(k_inv_denoms, dim3(ceil_div(nthreads, 256)), dim3(256), 0, st, ef_zero(), z,
-                     logH, (size_t)0, count, (const uint32_t*)twiddles().fwd(), out);
+                     logH, (size_t)0, count, (const uint32_t*)twiddles().fwd(), out, wout,
+                     count / 2);
   KCHECK();
 }
 
@@ -682,7 +699,8 @@ void open_coefficients(const uint32_t* coef, size_t col_stride, int w, size_t co
 static bool mergeable(const OpenDesc& a, const OpenDesc& b) {
   return !a.mat2 && !b.mat2 && a.height == b.height && a.logH == b.logH && a.invd_a == b.invd_a &&
          a.invd_b == b.invd_b && a.zeta == b.zeta && a.zlog == b.zlog && a.z3n == b.z3n &&
-         a.zc == b.zc && a.zb == b.zb && ef_eq(a.scale_a, b.scale_a) && ef_eq(a.scale_b, b.scale_b);
+         a.zc == b.zc && a.zb == b.zb && a.wtab == b.wtab && ef_eq(a.scale_a, b.scale_a) &&
+         ef_eq(a.scale_b, b.scale_b);
 }
 
 void open_batch(std::vector<OpenDesc>& in, int np, hipStream_t st) {

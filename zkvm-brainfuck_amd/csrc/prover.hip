@@ -899,10 +899,15 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
       rep_at[lh] |= !rounds[r]->mats[i].sharded;
     }
   htrace().mark("inv_denoms launch");
-  DBuf<EF> invd_zeta;
+  DBuf<EF> invd_zeta, w_zeta;
+  static const bool wtab_on = [] {  // BFZ_OPEN_WTAB=0: weights computed in the openings (A/B)
+    const char* e = std::getenv("BFZ_OPEN_WTAB");
+    return !(e && *e == '0');
+  }();
   if (!plan.on()) {
     invd_zeta.reset((size_t)1 << Lmax);
-    inv_denoms_dev(zeta_d, Lmax, invd_zeta.p, st);
+    if (wtab_on) w_zeta.reset((size_t)1 << (Lmax - 1));
+    inv_denoms_dev(zeta_d, Lmax, invd_zeta.p, st, w_zeta.p);
   }
   std::map<int, Invd> invd;
   for (const auto& [lh, two] : two_at) {
@@ -985,7 +990,8 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
       o.invd_b = two ? d.full_b() : o.invd_a;  // nullptr: derived from the zeta table
       // scale = (z^n - 3^n) / (3^n n), the same for both points ((zeta w_n)^n = zeta^n); with
       // derived second-point denominators it also carries w_n^-1 (see k_reduce)
-      const uint32_t zb = two && !o.invd_b ? minv(two_adic_gen(m.log_n)) : ONE;
+      o.wtab = w_zeta.p;  // unsharded: the weight table (nullptr: weights computed per row)
+      const uint32_t zb = two && !o.invd_b && !o.wtab ? minv(two_adic_gen(m.log_n)) : ONE;
       if (dev_zeta) {  // computed by k_open_final_batch from the device's zeta
         o.zeta = zeta_d;
         o.zlog = m.log_n;
