@@ -16,7 +16,7 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 S=$TMPDIR/prof_round
 rm -rf $S && mkdir -p $S
-B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-extra --sustain-s 0 --solo-world 0"
+B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-extra --no-cold --sustain-s 0 --solo-world 0"
 step() { echo "step $1 ($(date +%T))" >> gpurun_out/profile_round.status; }
 rm -f gpurun_out/profile_round.status
 step bench && timeout -k 10 400 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err && \
@@ -24,7 +24,7 @@ step stats && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format
 cp $S/prof/run_kernel_stats.csv gpurun_out/kernel_stats.csv && \
 python3 scripts/kernel_outliers.py $S/prof/run_kernel_trace.csv 16 > gpurun_out/outliers_stats.txt && \
 step trace && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $S/kt -o run \
-  -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extra --sustain-s 0 --solo-world 0 > $S/kt.log 2>&1 && \
+  -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extra --no-cold --sustain-s 0 --solo-world 0 > $S/kt.log 2>&1 && \
 python3 scripts/timeline.py $S/kt/run_kernel_trace.csv > gpurun_out/timeline.txt && \
 python3 scripts/kernel_outliers.py $S/kt/run_kernel_trace.csv 16 > gpurun_out/outliers_trace.txt && \
 step fetch && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $S/pmc_FETCH_SIZE -o run -- $B > $S/pmc_f.log 2>&1 && \
