@@ -52,42 +52,6 @@ __device__ __forceinline__ void store_row(uint32_t* out, size_t h, size_t t, con
   for (int k = 0; k < W; k++) out[(size_t)k * h + t] = c[k];
 }
 
-__device__ __forceinline__ uint32_t rev4(uint32_t x) { return __brev(x) >> 28; }
-
-// One trace row per thread, written at its bit-reversed position (column-major).  With one thread
-// per OUTPUT position (h < 256) the writes are coalesced but every event read is a gather from
-// another part of the record.  From h = 256 on a block takes the events i = A 2^(L-4) + M 16 + B
-// (M = the block, A, B = 4 bits each: sixteen runs of sixteen consecutive events), whose
-// positions bitrev(i) = rev(B) 2^(L-4) + rev(M) 16 + rev(A) are sixteen runs of sixteen
-// consecutive rows: the rows go through LDS and are written in those runs.  row(i, c) fills
-// c for event row i (zeros past the events).
-template <int W, class Row>
-__device__ __forceinline__ void trace_rows(uint32_t* __restrict__ out, size_t h, int logh, Row row) {
-  if (logh < 8) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= h) return;
-    uint32_t c[W] = {};
-    row((size_t)dbitrev((uint32_t)t, logh), c);
-    store_row(out, h, t, c);
-    return;
-  }
-  constexpr int RS = 256 + 16;  // one pad word per 16 rows
-  __shared__ uint32_t tile[W * RS];
-  const uint32_t j = threadIdx.x, M = blockIdx.x;
-  {
-    const uint32_t A = j >> 4, B = j & 15;
-    uint32_t c[W] = {};
-    row(((size_t)A << (logh - 4)) | ((size_t)M << 4) | B, c);
-    const uint32_t q = rev4(B) * 16 + rev4(A);  // the row's place among the block's 256
-#pragma unroll
-    for (int k = 0; k < W; k++) tile[k * RS + q + (q >> 4)] = c[k];
-  }
-  __syncthreads();
-  const size_t pos = ((size_t)(j >> 4) << (logh - 4)) | ((size_t)dbitrev(M, logh - 8) << 4) | (j & 15);
-#pragma unroll
-  for (int k = 0; k < W; k++) out[(size_t)k * h + pos] = tile[k * RS + j + (j >> 4)];
-}
-
 // ---------------------------------------------------------------- generate_dependencies
 constexpr int LOW16 = 8192;    // u16 bins kept in LDS per block (small timestamp gaps dominate)
 constexpr int PROG_LDS = 4096; // program counts in LDS when the program is this short
@@ -166,62 +130,68 @@ __global__ __launch_bounds__(256) void k_deps(const CpuEvent* __restrict__ cpu, 
 __global__ __launch_bounds__(256) void k_trace_cpu(const CpuEvent* __restrict__ ev, size_t n,
                                                    const Instruction* __restrict__ prog,
                                                    uint32_t* __restrict__ out, size_t h, int logh) {
-  trace_rows<31>(out, h, logh, [&](size_t i, uint32_t (&c)[31]) {
-    if (i < n) {
-      const CpuEvent e = ev[i];
-      const Instruction ins = prog[e.pc];
-      const int op = ins.opcode;
-      c[0] = to_mont(e.clk & 0xffff);
-      c[1] = to_mont((e.clk >> 16) & 0xff);
-      c[2] = to_mont(e.pc);
-      c[3] = to_mont(e.next_pc);
-      c[4] = to_mont(e.mp);
-      c[5] = to_mont(e.next_mp);
-      c[6] = to_mont(e.mv);
-      c[7] = to_mont(e.next_mv);
-      c[8] = to_mont((uint32_t)op);
-      put_word(&c[9], ins.op_a);
-      c[14] = to_mont(e.mv);
-      c[19] = to_mont(e.next_mv);
-      if (e.mv_access.kind) {
-        put_access(&c[13], &c[14], e.mv_access);
-        c[23] = ONE;
-      }
-      if (e.next_mv_access.kind == 2) {
-        put_access(&c[18], &c[19], e.next_mv_access);
-        c[24] = ONE;
-      }
-      const bool alu = op == OP_ADD || op == OP_SUB;
-      const bool jump = op == OP_LOOP_START || op == OP_LOOP_END;
-      const bool mi = op == OP_MEM_FWD || op == OP_MEM_BWD;
-      const bool io = op == OP_INPUT || op == OP_OUTPUT;
-      c[25] = mb(alu || jump || op == OP_OUTPUT);
-      c[26] = mb(alu);
-      c[27] = mb(jump);
-      c[28] = mb(io);
-      c[29] = mb(mi);
-      c[30] = to_mont((uint32_t)alu + jump + mi + io);
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= h) return;
+  const size_t i = dbitrev((uint32_t)t, logh);
+  uint32_t c[31] = {};
+  if (i < n) {
+    const CpuEvent e = ev[i];
+    const Instruction ins = prog[e.pc];
+    const int op = ins.opcode;
+    c[0] = to_mont(e.clk & 0xffff);
+    c[1] = to_mont((e.clk >> 16) & 0xff);
+    c[2] = to_mont(e.pc);
+    c[3] = to_mont(e.next_pc);
+    c[4] = to_mont(e.mp);
+    c[5] = to_mont(e.next_mp);
+    c[6] = to_mont(e.mv);
+    c[7] = to_mont(e.next_mv);
+    c[8] = to_mont((uint32_t)op);
+    put_word(&c[9], ins.op_a);
+    c[14] = to_mont(e.mv);
+    c[19] = to_mont(e.next_mv);
+    if (e.mv_access.kind) {
+      put_access(&c[13], &c[14], e.mv_access);
+      c[23] = ONE;
     }
-  });
+    if (e.next_mv_access.kind == 2) {
+      put_access(&c[18], &c[19], e.next_mv_access);
+      c[24] = ONE;
+    }
+    const bool alu = op == OP_ADD || op == OP_SUB;
+    const bool jump = op == OP_LOOP_START || op == OP_LOOP_END;
+    const bool mi = op == OP_MEM_FWD || op == OP_MEM_BWD;
+    const bool io = op == OP_INPUT || op == OP_OUTPUT;
+    c[25] = mb(alu || jump || op == OP_OUTPUT);
+    c[26] = mb(alu);
+    c[27] = mb(jump);
+    c[28] = mb(io);
+    c[29] = mb(mi);
+    c[30] = to_mont((uint32_t)alu + jump + mi + io);
+  }
+  store_row(out, h, t, c);
 }
 
 // AddSubChip: alu/mod.rs:63-146
 __global__ __launch_bounds__(256) void k_trace_addsub(const AluEvent* __restrict__ ev, size_t n,
                                                       uint32_t* __restrict__ out, size_t h,
                                                       int logh) {
-  trace_rows<7>(out, h, logh, [&](size_t i, uint32_t (&c)[7]) {
-    if (i < n) {
-      const AluEvent e = ev[i];
-      const uint8_t a = e.opcode == OP_ADD ? e.mv : e.next_mv;
-      c[0] = to_mont(e.pc);
-      c[1] = to_mont((uint8_t)(a + 1));
-      c[2] = mb((unsigned)a + 1u > 255u);
-      c[3] = to_mont(a);
-      c[4] = ONE;
-      c[5] = mb(e.opcode == OP_ADD);
-      c[6] = mb(e.opcode == OP_SUB);
-    }
-  });
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= h) return;
+  const size_t i = dbitrev((uint32_t)t, logh);
+  uint32_t c[7] = {};
+  if (i < n) {
+    const AluEvent e = ev[i];
+    const uint8_t a = e.opcode == OP_ADD ? e.mv : e.next_mv;
+    c[0] = to_mont(e.pc);
+    c[1] = to_mont((uint8_t)(a + 1));
+    c[2] = mb((unsigned)a + 1u > 255u);
+    c[3] = to_mont(a);
+    c[4] = ONE;
+    c[5] = mb(e.opcode == OP_ADD);
+    c[6] = mb(e.opcode == OP_SUB);
+  }
+  store_row(out, h, t, c);
 }
 
 // JumpChip: jump/trace.rs:32-97; layout jump/cols.rs:12-31 (IsZero inverse from a table)
@@ -230,77 +200,89 @@ __global__ __launch_bounds__(256) void k_trace_jump(const JumpEvent* __restrict_
   __shared__ uint32_t inv[256];
   if (threadIdx.x < 256) inv[threadIdx.x] = threadIdx.x ? minv(to_mont(threadIdx.x)) : 0u;
   __syncthreads();
-  trace_rows<45>(out, h, logh, [&](size_t i, uint32_t (&c)[45]) {
-    if (i < n) {
-      const JumpEvent e = ev[i];
-      put_word(&c[0], e.pc);
-      put_word_rc(&c[4], e.pc);
-      put_word(&c[18], e.next_pc);
-      put_word_rc(&c[22], e.next_pc);
-      put_word(&c[36], e.dst);
-      c[40] = to_mont(e.mv);
-      c[41] = inv[e.mv];  // IsZeroOperation::populate (operations/is_zero.rs:29-40)
-      c[42] = mb(e.mv == 0);
-      c[43] = mb(e.opcode == OP_LOOP_START);
-      c[44] = mb(e.opcode == OP_LOOP_END);
-    }
-  });
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= h) return;
+  const size_t i = dbitrev((uint32_t)t, logh);
+  uint32_t c[45] = {};
+  if (i < n) {
+    const JumpEvent e = ev[i];
+    put_word(&c[0], e.pc);
+    put_word_rc(&c[4], e.pc);
+    put_word(&c[18], e.next_pc);
+    put_word_rc(&c[22], e.next_pc);
+    put_word(&c[36], e.dst);
+    c[40] = to_mont(e.mv);
+    c[41] = inv[e.mv];  // IsZeroOperation::populate (operations/is_zero.rs:29-40)
+    c[42] = mb(e.mv == 0);
+    c[43] = mb(e.opcode == OP_LOOP_START);
+    c[44] = mb(e.opcode == OP_LOOP_END);
+  }
+  store_row(out, h, t, c);
 }
 
 // MemoryChip: memory/memory.rs:84-129 (two address entries per row)
 __global__ __launch_bounds__(256) void k_trace_memory(const MemoryEvent* __restrict__ ev, size_t n,
                                                       uint32_t* __restrict__ out, size_t h,
                                                       int logh) {
-  trace_rows<12>(out, h, logh, [&](size_t i, uint32_t (&c)[12]) {
-  #pragma unroll
-    for (int k = 0; k < 2; k++) {
-      const size_t j = 2 * i + k;
-      if (j < n) {
-        const MemoryEvent e = ev[j];
-        c[6 * k + 0] = to_mont(e.addr);
-        c[6 * k + 1] = to_mont(e.init_ts);
-        c[6 * k + 2] = to_mont(e.final_ts);
-        c[6 * k + 3] = to_mont(e.init_v);
-        c[6 * k + 4] = to_mont(e.final_v);
-        c[6 * k + 5] = ONE;
-      }
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= h) return;
+  const size_t i = dbitrev((uint32_t)t, logh);
+  uint32_t c[12] = {};
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const size_t j = 2 * i + k;
+    if (j < n) {
+      const MemoryEvent e = ev[j];
+      c[6 * k + 0] = to_mont(e.addr);
+      c[6 * k + 1] = to_mont(e.init_ts);
+      c[6 * k + 2] = to_mont(e.final_ts);
+      c[6 * k + 3] = to_mont(e.init_v);
+      c[6 * k + 4] = to_mont(e.final_v);
+      c[6 * k + 5] = ONE;
     }
-  });
+  }
+  store_row(out, h, t, c);
 }
 
 // MemoryInstructionsChip: memory/instructions/trace.rs:30-97; cols.rs:13-35
 __global__ __launch_bounds__(256) void k_trace_meminstr(const MemInstrEvent* __restrict__ ev,
                                                         size_t n, uint32_t* __restrict__ out,
                                                         size_t h, int logh) {
-  trace_rows<41>(out, h, logh, [&](size_t i, uint32_t (&c)[41]) {
-    if (i < n) {
-      const MemInstrEvent e = ev[i];
-      c[0] = to_mont(e.pc);
-      c[1] = to_mont(e.clk);
-      put_word(&c[2], e.mp);
-      put_word_rc(&c[6], e.mp);
-      put_word(&c[20], e.next_mp);
-      put_word_rc(&c[24], e.next_mp);
-      c[38] = mb(e.opcode == OP_MEM_FWD);
-      c[39] = mb(e.opcode == OP_MEM_BWD);
-      c[40] = ONE;
-    }
-  });
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= h) return;
+  const size_t i = dbitrev((uint32_t)t, logh);
+  uint32_t c[41] = {};
+  if (i < n) {
+    const MemInstrEvent e = ev[i];
+    c[0] = to_mont(e.pc);
+    c[1] = to_mont(e.clk);
+    put_word(&c[2], e.mp);
+    put_word_rc(&c[6], e.mp);
+    put_word(&c[20], e.next_mp);
+    put_word_rc(&c[24], e.next_mp);
+    c[38] = mb(e.opcode == OP_MEM_FWD);
+    c[39] = mb(e.opcode == OP_MEM_BWD);
+    c[40] = ONE;
+  }
+  store_row(out, h, t, c);
 }
 
 // IoChip: io/mod.rs:72-121
 __global__ __launch_bounds__(256) void k_trace_io(const IoEvent* __restrict__ ev, size_t n,
                                                   uint32_t* __restrict__ out, size_t h, int logh) {
-  trace_rows<5>(out, h, logh, [&](size_t i, uint32_t (&c)[5]) {
-    if (i < n) {
-      const IoEvent e = ev[i];
-      c[0] = to_mont(e.pc);
-      c[1] = to_mont(e.mp);
-      c[2] = to_mont(e.mv);
-      c[3] = mb(e.opcode == OP_INPUT);
-      c[4] = mb(e.opcode == OP_OUTPUT);
-    }
-  });
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= h) return;
+  const size_t i = dbitrev((uint32_t)t, logh);
+  uint32_t c[5] = {};
+  if (i < n) {
+    const IoEvent e = ev[i];
+    c[0] = to_mont(e.pc);
+    c[1] = to_mont(e.mp);
+    c[2] = to_mont(e.mv);
+    c[3] = mb(e.opcode == OP_INPUT);
+    c[4] = mb(e.opcode == OP_OUTPUT);
+  }
+  store_row(out, h, t, c);
 }
 
 // ProgramChip main trace (program/mod.rs:100-135): execution count per instruction.
