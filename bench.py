@@ -34,7 +34,7 @@ VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 # Full-rate-equivalent VALU lane-ops of one Poseidon2 permutation in k_permute_batch
 # (gfx950 ISA instruction mix, profiles/r02/poseidon2_isa_mix.txt).
 P2_UNITS_PER_PERM = 5133
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05", "profile_round_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r06", "profile_round_pmc_summary.json")
 
 
 # VALU units (full-rate lane-ops) per radix-2 element-stage of a 2^22 coset LDE, from the gfx950
@@ -85,7 +85,7 @@ def ntt_roofline(tm):
             "traffic": round(traffic) if traffic else None,
             "algorithmic_per_launch": round(alg_per_launch),
             "traffic_over_algorithmic": round(traffic / alg_per_launch, 3) if traffic else None,
-            "traffic_source": "profiles/r05/profile_round_pmc_summary.json (FETCH_SIZE x2 + WRITE_SIZE per "
+            "traffic_source": "profiles/r06/profile_round_pmc_summary.json (FETCH_SIZE x2 + WRITE_SIZE per "
                               "launch, scaled to this proof's launches)",
             "basis": "SURVEY 8(d): 12*n*w B per coset LDE (read n, write 2n) / NTT kernel time",
             "kernel": "coset LDE = k_ntt_tile<false,14> (iDFT stages 0-13) + k_lde_mid<L> (iDFT "
