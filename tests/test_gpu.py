@@ -743,3 +743,19 @@ def test_record_from_cycles_refuses_cycles_no_record_holds(client):
     with pytest.raises(_lib.BfzError, match="no cycles"):
         events.record_from_cycles(pk, cyc[:0], rec.memory)
     assert _record_proof(pk, rec, cycles=True) == O.prove(prog, stdin)
+
+
+def test_first_proof_of_a_fresh_process_costs_a_warm_proof():
+    """a fresh process (init, setup, record, one prove -- what a
+    ProverClient::prove().run() process does) proves the headline workload in about the time of
+    a warm proof: no table is built between the first proof's launches (twiddles on the device in
+    setup, coset-power and selector tables when the record is created).  scripts/cold_first_proof.py
+    in a child process; bench.py reports the same figure as cold_first_proof_ms."""
+    import subprocess
+    import sys
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "cold_first_proof.py"),
+                          "--warm", "2"], capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert r["cycles"] == 3767729
+    assert r["first_prove_ms"] <= 1.5 * min(r["warm_prove_ms"]), r
