@@ -45,6 +45,7 @@ use p3_field::FieldAlgebra;
 use p3_koala_bear::KoalaBear;
 use p3_matrix::{dense::RowMajorMatrix, Matrix};
 use p3_maybe_rayon::prelude::*;
+use p3_symmetric::Hash;
 
 type SC = KoalaBearPoseidon2;
 type A = BfAir<KoalaBear>;
@@ -84,6 +85,15 @@ fn words<T>(v: &[T]) -> &[u32] {
 fn field_words(w: &[u32]) -> Vec<KoalaBear> {
     assert_eq!(core::mem::size_of::<KoalaBear>(), 4);
     w.iter().map(|&x| unsafe { core::mem::transmute::<u32, KoalaBear>(x) }).collect()
+}
+
+/// This configuration's commitment is MerkleTreeMmcs's `Hash<KoalaBear, KoalaBear, 8>`
+/// (`p3_symmetric::Hash: From<[W; N]>`), built here from the device root's Montgomery words: a
+/// configuration whose commitment were another type fails to compile instead of being
+/// transmuted into.
+fn commitment(root: &[u32; 8]) -> Com<SC> {
+    let w: [KoalaBear; 8] = field_words(root).try_into().expect("8 digest words");
+    Hash::<KoalaBear, KoalaBear, 8>::from(w)
 }
 
 #[derive(Debug, Clone, Copy)]
@@ -502,7 +512,7 @@ impl MachineProver<SC, A> for HipProver {
         });
         let chip_ordering =
             named_traces.iter().enumerate().map(|(i, (name, _))| (name.to_owned(), i)).collect();
-        let main_commit: Com<SC> = unsafe { core::mem::transmute_copy(&root) };
+        let main_commit = commitment(&root);
         let traces = named_traces.into_iter().map(|(_, t)| t).collect();
         ShardMainData::new(traces, main_commit, HipMainData(data), chip_ordering)
     }
@@ -546,7 +556,7 @@ impl MachineProver<SC, A> for HipProver {
         sys::check(unsafe {
             sys::bfz_record_main_commit(pk.dev, rec.0, &mut data, root.as_mut_ptr())
         });
-        let main_commit: Com<SC> = unsafe { core::mem::transmute_copy(&root) };
+        let main_commit = commitment(&root);
         // open reads the device data only: no host traces, chip ordering fixed by libbfz
         let data = ShardMainData::new(Vec::new(), main_commit, HipMainData(data), HashMap::new());
         let shard_proof = self.open(pk, data, &mut challenger.clone())?; // prover.rs:578
