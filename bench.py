@@ -691,6 +691,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cold", action="store_true",
                     help="skip the fresh-process first-proof measurement (cold_first_proof_ms)")
+    ap.add_argument("--rccl-sharded", action="store_true",
+                    help="replicas mode at N > 1: also time one proof split over all ranks over RCCL "
+                         "(sharded_proof; never run on hardware with more than one rank -- opt-in "
+                         "so a hang in an unvalidated collective cannot cost the replica line)")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the end-to-end batch and drop-in-path figures")
     ap.add_argument("--mode", choices=("replicas", "sharded", "pcs"), default="replicas",
@@ -811,7 +815,7 @@ def main():
         extra["sustained"]["last_proof_checked"] = True
         extra["sustained"]["lanes"] = sustained_lanes(pk, rec, ms, args.sustain_s, proof)
     hung = False
-    if world > 1 and not sharded and not args.no_extra:  # every rank takes part
+    if world > 1 and not sharded and args.rccl_sharded:  # every rank takes part
         # RCCL has no run on this pool's one-GPU boxes: a hang in it must not cost the replica
         # line, so the attempt runs in a thread with a wall-clock limit of its own
         res = run_with_limit(lambda: sharded_latency(dist, pk, rec, rank, world, device, proof),
@@ -860,7 +864,7 @@ def main():
         }
         if "sustained" in extra:
             line["sustained"] = extra["sustained"]
-        if world > 1 and not sharded and not args.no_extra and "sharded_proof" in extra:
+        if world > 1 and not sharded and "sharded_proof" in extra:
             line["sharded_proof"] = extra["sharded_proof"]
         solo = [int(x) for x in str(args.solo_world).split(",") if x.strip() and int(x) > 1]
         if world == 1 and solo:
