@@ -353,8 +353,10 @@ int bfz_record_prove_sharded(const bfz_pk* pk, const bfz_record* rec, int rank, 
 /* Timing of ONE rank's share of a world-rank sharded proof, run alone on this GPU: the same
  * kernels and sizes bfz_record_prove_sharded runs on rank `rank`, with every exchange a no-op
  * (receive buffers keep whatever they hold, so the result is not a proof and is discarded;
- * the FRI final-constant check is skipped).  Stage times and kernel counters go to *timings.
- * Predicts the per-rank critical path of an N-GPU proof without N GPUs. */
+ * the FRI final-constant check is skipped).  Stage times and kernel counters go to *timings;
+ * timings == NULL runs the share without stage events or per-launch kernel probes (the caller
+ * times it on the wall clock, as the single-GPU headline is timed).  Predicts the per-rank
+ * critical path of an N-GPU proof without N GPUs. */
 int bfz_record_prove_shard_solo(const bfz_pk* pk, const bfz_record* rec, int rank, int world,
                                 bfz_timings* timings);
 

@@ -159,12 +159,13 @@ struct TopLayers {
   int n;  // layers in this launch
 };
 
+// base: the first node of the launch's first layer (a rank's subtree of a sharded tree; 0 else)
 __global__ __launch_bounds__(1024) void k_compress_top(const uint32_t* __restrict__ prev,
                                                        size_t nlen, ColList inj, TopLayers tl,
-                                                       RootChallenge rc) {
+                                                       RootChallenge rc, size_t base) {
   __shared__ uint32_t buf[2][TOP_NODES * 8];
   const size_t per = nlen < (size_t)TOP_NODES ? nlen : (size_t)TOP_NODES;
-  const size_t g0 = (size_t)blockIdx.x * per;  // first-layer node of this block
+  const size_t g0 = base + (size_t)blockIdx.x * per;  // first-layer node of this block
   const int lane = threadIdx.x & 15;
   const LaneConsts kc = lane_consts(lane);
   for (int l = 0; l < tl.n; l++) {
@@ -326,7 +327,7 @@ static void build_layers(MerkleTree& t, int L0, size_t len, const std::vector<co
     const bool root_launch = L + tl.n > nl;
     hipLaunchKernelGGL(k_compress_top, dim3(blocks), dim3(16 * TOP_NODES), 0, st,
                        (const uint32_t*)t.layers[L - 1].p, first, make_cols(all), tl,
-                       root_launch ? rc : RootChallenge{});
+                       root_launch ? rc : RootChallenge{}, (size_t)0);
     KCHECK();
     L += tl.n;
     len = first >> (tl.n - 1);
@@ -361,13 +362,40 @@ static void build_sharded(MerkleTree& t, size_t h0, const std::vector<const MatR
   t.shard_log = lg;
   leaves(k * (h0 / G), h0 / G);
   size_t len = h0;
-  for (int L = 1; L <= nl - lg; L++) {
+  int L = 1;
+  for (; L <= nl - lg && (len >> 1) / G > LANE_LAYER_MAX; L++) {  // throughput layers
     const size_t nlen = len >> 1;
     std::vector<const MatRef*> grp;
     while (next < sorted.size() && sorted[next]->height == nlen) grp.push_back(sorted[next++]);
     t.layers[L].reset(8 * nlen);
     launch_layer(t, L, k * (nlen / G), nlen / G, grp, st);
     len = nlen;
+  }
+  // the rank's subtree below the shard level: up to TOP_LAYERS layers per k_compress_top launch
+  // (a layer per launch made the small shares of a many-rank proof launch-bound)
+  while (L <= nl - lg) {
+    const size_t first = (len >> 1) / G;  // this rank's nodes of the launch's first layer
+    const int sub = first > (size_t)TOP_NODES ? TOP_LAYERS : log2i(first) + 1;
+    TopLayers tl{};
+    tl.n = std::min(sub, nl - lg - L + 1);
+    std::vector<const MatRef*> all;
+    size_t nlen = len >> 1;
+    for (int l = 0; l < tl.n; l++, nlen >>= 1) {
+      tl.c0[l] = 0;
+      for (const MatRef* m : all) tl.c0[l] += m->width;
+      while (next < sorted.size() && sorted[next]->height == nlen) all.push_back(sorted[next++]);
+      tl.c1[l] = 0;
+      for (const MatRef* m : all) tl.c1[l] += m->width;
+      t.layers[L + l].reset(8 * nlen);
+      tl.out[l] = t.layers[L + l].p;
+    }
+    const unsigned blocks = first > (size_t)TOP_NODES ? (unsigned)(first / TOP_NODES) : 1u;
+    hipLaunchKernelGGL(k_compress_top, dim3(blocks), dim3(16 * TOP_NODES), 0, st,
+                       (const uint32_t*)t.layers[L - 1].p, first, make_cols(all), tl,
+                       RootChallenge{}, k * first);
+    KCHECK();
+    L += tl.n;
+    len >>= tl.n;
   }
   // layer nl - lg has G nodes; node k is ours: all-gather them device to device
   DBuf<uint32_t>& lay = t.layers[nl - lg];
