@@ -757,17 +757,28 @@ void coset_lde_ex(const uint32_t* evals, size_t src_stride, size_t n, int w, uin
 struct ColMap {  // output column y reads input column col[y]
   uint8_t col[64];
 };
+// a^(u + l m) = a^u (a^m)^l: one table power per output and the launch constants (a^m)^l, so a
+// term is one product, summed lazily in 64 bits (four products < 2^64 between folds).
+constexpr int FOLD_MAX_TERMS = 64;
+struct FoldPowers {
+  uint32_t p[FOLD_MAX_TERMS];  // (a^m)^l, l < n / m
+};
 __global__ __launch_bounds__(256) void k_fold_residue(const uint32_t* __restrict__ coef, size_t n,
                                                       uint32_t* __restrict__ out, size_t m, int B,
-                                                      const uint32_t* __restrict__ pw, ColMap cm) {
+                                                      const uint32_t* __restrict__ pw, ColMap cm,
+                                                      FoldPowers fp) {
   const uint32_t* c = coef + (size_t)cm.col[blockIdx.y] * n;
   uint32_t* o = out + (size_t)blockIdx.y * m;
   const size_t mask = ((size_t)1 << B) - 1, nb = mask + 1;
+  const int terms = (int)(n / m);
   for (size_t u = (size_t)blockIdx.x * blockDim.x + threadIdx.x; u < m;
        u += (size_t)gridDim.x * blockDim.x) {
-    uint32_t acc = 0;
-    for (size_t j = u; j < n; j += m) acc = madd(acc, mmul(c[j], mmul(pw[j & mask], pw[nb + (j >> B)])));
-    o[u] = acc;
+    uint64_t acc = 0;
+    for (int l = 0; l < terms; l++) {
+      acc += (uint64_t)c[u + (size_t)l * m] * fp.p[l];
+      if ((l & 3) == 3) acc = fold32(acc);
+    }
+    o[u] = mmul(mreduce(acc), mmul(pw[u & mask], pw[nb + (u >> B)]));
   }
 }
 
@@ -816,8 +827,14 @@ void coset_residue_cols(const uint32_t* coef, size_t n, const std::vector<int>& 
   const uint32_t a = mmul(shift, mpow(two_adic_gen(L + 1), (uint64_t)r));
   const int B = (L + 1) / 2;
   const uint32_t* pw = residue_powers(a, L, B);
+  const size_t terms = n >= m ? n / m : 1;
+  if (terms > (size_t)FOLD_MAX_TERMS) throw std::runtime_error("coset_residue: more than 64 folds");
+  FoldPowers fp{};
+  const uint32_t am = mpow(a, (uint64_t)m);
+  fp.p[0] = ONE;
+  for (size_t l = 1; l < terms; l++) fp.p[l] = mmul(fp.p[l - 1], am);
   const dim3 grid(std::min<unsigned>(ceil_div(m, 256), 2048), w);
-  hipLaunchKernelGGL(k_fold_residue, grid, dim3(256), 0, st, coef, n, out, m, B, pw, map);
+  hipLaunchKernelGGL(k_fold_residue, grid, dim3(256), 0, st, coef, n, out, m, B, pw, map, fp);
   KCHECK();
   ntt_passes(out, out, m, m, w, log2i(m), /*dif=*/true, st);
 }
