@@ -332,16 +332,24 @@ struct MidPlan {
                                                   : (R16_TILE_LOG - b2 < MID_CMAX ? R16_TILE_LOG - b2 : MID_CMAX);
 };
 
+#ifndef BFZ_MID_CPB
+#define BFZ_MID_CPB 1
+#endif
+// Columns per block (one tile position, its stage twiddles reused from the first column): 2 and 4
+// cut k_lde_mid<22>'s FETCH_SIZE 221 -> 205 / 194 MB per launch but not its time, and cost
+// +0.08 ms of NTT kernel time per proof at 2 (profiles/r06/ab_mid_cpb.txt): 1.
+constexpr int MID_CPB = BFZ_MID_CPB;
+
 template <int L>
-__global__ __launch_bounds__(1 << (MidPlan<L>::b2 + MidPlan<L>::c2 - 4)) void k_lde_mid(
+__device__ __forceinline__ void lde_mid_col(
     const uint32_t* __restrict__ src, size_t src_stride, uint32_t* __restrict__ lde, size_t n,
     const uint32_t* __restrict__ tw_inv, const uint32_t* __restrict__ tw_fwd,
-    const uint32_t* __restrict__ pw, int B, MidPowers mp, int only_half) {
+    const uint32_t* __restrict__ pw, int B, const MidPowers& mp, int only_half, uint32_t by) {
   constexpr int s0 = MidPlan<L>::b1, b = MidPlan<L>::b2, c = MidPlan<L>::c2;
   extern __shared__ uint32_t lds[];
   const int tid = threadIdx.x;
   const int nlo_log = s0 - c;
-  const uint32_t bx = blockIdx.x, by = blockIdx.y;
+  const uint32_t bx = blockIdx.x;
   const size_t lo_blk = bx & ((1u << nlo_log) - 1);
   const size_t hi = (size_t)bx >> nlo_log;
   const size_t base = (hi << (s0 + b)) + (lo_blk << c);
@@ -422,6 +430,19 @@ __global__ __launch_bounds__(1 << (MidPlan<L>::b2 + MidPlan<L>::c2 - 4)) void k_
         }
       }
     }
+  }
+}
+
+template <int L>
+__global__ __launch_bounds__(1 << (MidPlan<L>::b2 + MidPlan<L>::c2 - 4)) void k_lde_mid(
+    const uint32_t* __restrict__ src, size_t src_stride, uint32_t* __restrict__ lde, size_t n,
+    const uint32_t* __restrict__ tw_inv, const uint32_t* __restrict__ tw_fwd,
+    const uint32_t* __restrict__ pw, int B, MidPowers mp, int only_half, int w) {
+  for (int cc = 0; cc < MID_CPB; cc++) {
+    const uint32_t by = blockIdx.y * MID_CPB + cc;
+    if (by >= (uint32_t)w) break;  // uniform across the block
+    if (cc) __syncthreads();       // the previous column's last LDS reads are done
+    lde_mid_col<L>(src, src_stride, lde, n, tw_inv, tw_fwd, pw, B, mp, only_half, by);
   }
 }
 
@@ -714,13 +735,13 @@ void coset_lde_ex(const uint32_t* evals, size_t src_stride, size_t n, int w, uin
     const size_t ldsz = ((size_t)1 << (p2.b + p2.c)) + ((size_t)1 << (p2.b + p2.c - 4));
     KernelProbe& probe = ntt_probe();
     hipEvent_t ev0 = probe.on ? probe.begin(st) : nullptr;
-    const dim3 grid(1u << (L - p2.b - p2.c), w);
+    const dim3 grid(1u << (L - p2.b - p2.c), ceil_div(w, MID_CPB));
 #define BFZ_MID(LL)                                                                              \
   case LL:                                                                                       \
     static_assert(MidPlan<LL>::b2 >= 4, "plan");                                                 \
     hipLaunchKernelGGL(k_lde_mid<LL>, grid, dim3(threads), ldsz * 4, st, (const uint32_t*)coef.p, \
                        n, lde, n, (const uint32_t*)T.inv(), (const uint32_t*)T.fwd(), pw, B, mp, \
-                       only_half);                                                               \
+                       only_half, w);                                                            \
     break;
     switch (L) {
       BFZ_MID(14) BFZ_MID(15) BFZ_MID(16) BFZ_MID(17) BFZ_MID(18) BFZ_MID(19) BFZ_MID(20) BFZ_MID(21)
