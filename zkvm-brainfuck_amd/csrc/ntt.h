@@ -42,6 +42,16 @@ void coset_residue(const uint32_t* coef, size_t n, int w, uint32_t shift, int lo
 void coset_residue_cols(const uint32_t* coef, size_t n, const std::vector<int>& cols,
                         uint32_t shift, int logG, int r, uint32_t* out, hipStream_t st);
 
+// The same in one pass over the coefficients (k_coef_fold): the iDFT's second pass keeps each
+// column's coefficients in registers, writes coef only for [j0, j0 + len) (column stride n) and
+// folds them into out (residue r, m x w, m = 2n / G) and, with next_cols, into nxt (residue r2,
+// the listed columns) -- natural order; residue_dft then finishes each (the forward DFT).
+// Returns false (nothing launched) where it does not apply (log n <= 14 or > 23, G > 32).
+bool coef_fold_residues(const uint32_t* evals, size_t n, int w, uint32_t* coef, size_t j0,
+                        size_t len, uint32_t shift, int logG, int r, uint32_t* out,
+                        const std::vector<int>* next_cols, int r2, uint32_t* nxt, hipStream_t st);
+void residue_dft(uint32_t* out, size_t m, int w, hipStream_t st);
+
 // Row-major natural-order host layout -> column-major bit-reversed device layout.
 void transpose_bitrev(const uint32_t* rowmajor, size_t n, int w, uint32_t* colmajor,
                       hipStream_t st);

@@ -433,6 +433,113 @@ __device__ __forceinline__ void lde_mid_col(
   }
 }
 
+// Sharded LDE, fused: the second iDFT pass of a column (stages s0.., as the
+// middle pass above) leaves each thread 16 coefficients n c_k at k = k0 + i D (D = 2^(L-4));
+// instead of a coset DFT the thread stores the coefficients of the rank's opening range and
+// folds them onto the rank's residue coset in registers -- d_u = a^u/n sum_l c_(u + l m) (a^m)^l
+// with u = k0 + i0 D, i0 < m / D (the terms of an output are i0 + l m/D of the same thread) --
+// plus the next-row residue for the columns the quotient reads there.  The coefficients are
+// never read back for the folds (round 5 read them twice from HBM, once per residue).
+struct ResidueFold {
+  uint32_t A[4];       // halving stage j (h = 8 >> j): (a^m)^(h / S)
+  uint32_t Q[16];      // (a^D)^i
+  const uint32_t* pw;  // a^j / n two-level table (residue_powers)
+  uint32_t* out;       // m x w
+};
+struct CoefFold {
+  uint32_t* coef;   // coefficients (column stride n), written for k in [j0, j0 + len)
+  size_t j0, len, m;
+  int B, S;          // table split; S = m / D outputs per thread
+  ResidueFold r[2];  // r[1]: the next-row residue (out == nullptr: none)
+  uint8_t nidx[64];  // input column -> r[1] output column (0xff: not read at the next row)
+};
+
+template <int L>
+__device__ __forceinline__ void coef_fold_col(const uint32_t* __restrict__ src, size_t n,
+                                              const uint32_t* __restrict__ tw_inv,
+                                              const CoefFold& cf, uint32_t by) {
+  constexpr int s0 = MidPlan<L>::b1, b = MidPlan<L>::b2, c = MidPlan<L>::c2;
+  extern __shared__ uint32_t lds[];
+  const int tid = threadIdx.x;
+  const int nlo_log = s0 - c;
+  const uint32_t bx = blockIdx.x;
+  const size_t lo_blk = bx & ((1u << nlo_log) - 1);
+  const size_t hi = (size_t)bx >> nlo_log;
+  const size_t base = (hi << (s0 + b)) + (lo_blk << c);
+  const uint32_t* S = src + (size_t)by * n + base;
+  const int lo = tid & ((1 << c) - 1);
+  const uint32_t lo_g = (uint32_t)(lo_blk << c) + lo;
+  const int rest = tid >> c;
+  const int nwin = (b + 3) >> 2;
+  uint32_t x[16];
+  int done_lo = 0;
+#pragma unroll
+  for (int w = 0; w < nwin; w++) {  // iDFT, as lde_mid_col
+    const int g0 = min(4 * w, b - 4);
+    const uint32_t m_low = rest & ((1 << g0) - 1);
+    const uint32_t m_base = m_low | ((uint32_t)(rest >> g0) << (g0 + 4));
+    if (w == 0) {
+      const __amdgpu_buffer_rsrc_t rs = rsrc_of(S);
+      const uint32_t off = ((m_base << s0) + lo) * 4u;
+#pragma unroll
+      for (int i = 0; i < 16; i++) x[i] = ld_b(rs, off, ((uint32_t)i << (g0 + s0)) * 4u);
+    } else {
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 16; i++)
+        x[i] = lds[lds_pad((int)(((m_base | ((uint32_t)i << g0)) << c) | lo), c)];
+    }
+    const int kk_lo = max(0, done_lo - g0);
+    done_lo = g0 + 4;
+    r16_window<false, false, true>(x, g0, kk_lo, 4, s0, m_low, lo_g, tw_inv);
+    if (w < nwin - 1) {
+#pragma unroll
+      for (int i = 0; i < 16; i++)
+        lds[lds_pad((int)(((m_base | ((uint32_t)i << g0)) << c) | lo), c)] = x[i];
+    }
+  }
+  const int g0 = b - 4;
+  const uint32_t m_base = (rest & ((1 << g0) - 1)) | ((uint32_t)(rest >> g0) << (g0 + 4));
+  const size_t k0 = base + ((size_t)m_base << s0) + lo;
+  constexpr size_t D = (size_t)1 << (L - 4);
+  uint32_t* C = cf.coef + (size_t)by * n;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const size_t k = k0 + (size_t)i * D;
+    if (k - cf.j0 < cf.len) C[k] = x[i];  // the rank's opening range only
+  }
+  const size_t mask = ((size_t)1 << cf.B) - 1, nb = mask + 1;
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const ResidueFold& rf = cf.r[q];
+    if (!rf.out) break;  // uniform
+    const int oc = q ? cf.nidx[by] : (int)by;
+    if (oc == 0xff) break;  // uniform: the whole block is one column
+    // y[i0] = sum_l x[i0 + l S] (a^m)^l by halving stages y[i] += y[i + h] (a^m)^(h/S), h = 8..S
+    uint32_t y[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) y[i] = x[i];
+#pragma unroll
+    for (int st = 0; st < 4; st++) {
+      const int h = 8 >> st;
+      if (h < cf.S) break;
+#pragma unroll
+      for (int i = 0; i < h; i++) y[i] = madd(y[i], mmul(y[i + h], rf.A[st]));
+    }
+    const uint32_t ak0 = mmul(rf.pw[k0 & mask], rf.pw[nb + (k0 >> cf.B)]);  // a^k0 / n
+    uint32_t* O = rf.out + (size_t)oc * cf.m + k0;
+#pragma unroll
+    for (int i = 0; i < 16; i++)
+      if (i < cf.S) O[(size_t)i * D] = mmul(y[i], mmul(ak0, rf.Q[i]));
+  }
+}
+
+template <int L>
+__global__ __launch_bounds__(1 << (MidPlan<L>::b2 + MidPlan<L>::c2 - 4)) void k_coef_fold(
+    const uint32_t* __restrict__ src, size_t n, const uint32_t* __restrict__ tw_inv, CoefFold cf) {
+  coef_fold_col<L>(src, n, tw_inv, cf, blockIdx.y);
+}
+
 template <int L>
 __global__ __launch_bounds__(1 << (MidPlan<L>::b2 + MidPlan<L>::c2 - 4)) void k_lde_mid(
     const uint32_t* __restrict__ src, size_t src_stride, uint32_t* __restrict__ lde, size_t n,
@@ -539,6 +646,11 @@ static void r16_attrs() {
                       (const void*)&k_lde_mid<18>, (const void*)&k_lde_mid<19>,
                       (const void*)&k_lde_mid<20>, (const void*)&k_lde_mid<21>,
                       (const void*)&k_lde_mid<22>, (const void*)&k_lde_mid<23>,
+                      (const void*)&k_coef_fold<15>, (const void*)&k_coef_fold<16>,
+                      (const void*)&k_coef_fold<17>, (const void*)&k_coef_fold<18>,
+                      (const void*)&k_coef_fold<19>, (const void*)&k_coef_fold<20>,
+                      (const void*)&k_coef_fold<21>, (const void*)&k_coef_fold<22>,
+                      (const void*)&k_coef_fold<23>,
                       (const void*)&k_ntt_tile<true, R16_TILE_LOG, false, true, true>,
                       (const void*)&k_ntt_tile<false, R16_TILE_LOG, true, true, true>,
                       (const void*)&k_ntt_tile<false, R16_TILE_LOG, false, true, true>};
@@ -857,6 +969,77 @@ void coset_residue_cols(const uint32_t* coef, size_t n, const std::vector<int>& 
   const dim3 grid(std::min<unsigned>(ceil_div(m, 256), 2048), w);
   hipLaunchKernelGGL(k_fold_residue, grid, dim3(256), 0, st, coef, n, out, m, B, pw, map, fp);
   KCHECK();
+  ntt_passes(out, out, m, m, w, log2i(m), /*dif=*/true, st);
+}
+
+// The launch constants of one residue's fold in k_coef_fold: a = shift w_2n^r, S = m / D.
+static ResidueFold residue_fold(uint32_t shift, int L, int logG, int r, int S, uint32_t* out) {
+  ResidueFold f{};
+  const size_t m = ((size_t)2 << L) >> logG;
+  const uint32_t a = mmul(shift, mpow(two_adic_gen(L + 1), (uint64_t)r));
+  f.pw = residue_powers(a, L, (L + 1) / 2);
+  f.out = out;
+  const uint32_t am = mpow(a, (uint64_t)m);
+  for (int j = 0; j < 4; j++) f.A[j] = (8 >> j) >= S ? mpow(am, (uint64_t)((8 >> j) / S)) : ONE;
+  const uint32_t aD = mpow(a, (uint64_t)1 << (L - 4));
+  uint32_t q = ONE;
+  for (int i = 0; i < 16; i++) { f.Q[i] = q; q = mmul(q, aD); }
+  return f;
+}
+
+static bool fused_residues_on() {
+  static const bool on = [] {
+    const char* e = getenv("BFZ_FUSED_RESIDUE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+bool coef_fold_residues(const uint32_t* evals, size_t n, int w, uint32_t* coef, size_t j0,
+                        size_t len, uint32_t shift, int logG, int r, uint32_t* out,
+                        const std::vector<int>* next_cols, int r2, uint32_t* nxt, hipStream_t st) {
+  const int L = log2i(n);
+  if (!fused_residues_on() || L <= R16_TILE_LOG || L > 23 || logG < 1 || logG > 5 || w < 1 ||
+      w > 64)
+    return false;
+  Twiddles& T = twiddles();
+  T.ensure(L);
+  r16_attrs();
+  const auto plan = r16_plan(L);
+  const R16Pass& p1 = plan[0];
+  const R16Pass& p2 = plan[1];
+  r16_launch(p1, evals, n, coef, n, w, L, false, st);
+  CoefFold cf{};
+  cf.coef = coef;
+  cf.j0 = j0;
+  cf.len = len;
+  cf.m = ((size_t)2 << L) >> logG;
+  cf.B = (L + 1) / 2;
+  cf.S = 1 << (5 - logG);
+  cf.r[0] = residue_fold(shift, L, logG, r, cf.S, out);
+  std::fill(std::begin(cf.nidx), std::end(cf.nidx), (uint8_t)0xff);
+  if (next_cols && !next_cols->empty()) {
+    cf.r[1] = residue_fold(shift, L, logG, r2, cf.S, nxt);
+    for (size_t y = 0; y < next_cols->size(); y++) cf.nidx[(*next_cols)[y]] = (uint8_t)y;
+  }
+  const int threads = 1 << (p2.b + p2.c - 4);
+  const size_t ldsz = ((size_t)1 << (p2.b + p2.c)) + ((size_t)1 << (p2.b + p2.c - 4));
+  const dim3 grid(1u << (L - p2.b - p2.c), w);
+#define BFZ_CF(LL)                                                                           \
+  case LL:                                                                                   \
+    hipLaunchKernelGGL(k_coef_fold<LL>, grid, dim3(threads), ldsz * 4, st,                   \
+                       (const uint32_t*)coef, n, (const uint32_t*)T.inv(), cf);              \
+    break;
+  switch (L) {
+    BFZ_CF(15) BFZ_CF(16) BFZ_CF(17) BFZ_CF(18) BFZ_CF(19) BFZ_CF(20) BFZ_CF(21) BFZ_CF(22)
+    BFZ_CF(23)
+  }
+#undef BFZ_CF
+  KCHECK();
+  return true;
+}
+
+void residue_dft(uint32_t* out, size_t m, int w, hipStream_t st) {
   ntt_passes(out, out, m, m, w, log2i(m), /*dif=*/true, st);
 }
 

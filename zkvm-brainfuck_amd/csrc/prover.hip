@@ -338,18 +338,31 @@ static void lde_into(CMat& cm, const uint32_t* evals, size_t n, int w, uint32_t 
     cm.row0 = plan->row0(2 * n);
     cm.coef.reset(n * (size_t)w);
     cm.lde.buf.reset(cm.blk * (size_t)w);
+    cm.nxt_row0 = (size_t)plan->k2 * cm.blk;  // = row0 for G = 2
+    const bool nx = next_cols && !next_cols->empty() && plan->G >= 4;
+    if (nx) {
+      cm.nxt.reset(cm.blk * next_cols->size());
+      cm.nmap.fill(0);  // columns not read at the next row: any valid column
+      for (size_t y = 0; y < next_cols->size(); y++) cm.nmap[(*next_cols)[y]] = (uint8_t)y;
+    }
+    const size_t len = n >> plan->lg;  // the coefficient range this rank opens (open_ood)
     hipEvent_t b0 = timed ? tm->begin(st) : nullptr;
+    // iDFT + folds in one pass over the coefficients (the fold time counts as iDFT here)
+    if (coef_fold_residues(evals, n, w, cm.coef.p, (size_t)plan->k * len, len, lde_shift, plan->lg,
+                           plan->r, cm.lde.buf.p, nx ? next_cols : nullptr, plan->r2, cm.nxt.p,
+                           st)) {
+      if (timed) tm->end(b0, st, split->idft);
+      hipEvent_t b1 = timed ? tm->begin(st) : nullptr;
+      residue_dft(cm.lde.buf.p, cm.blk, w, st);
+      if (nx) residue_dft(cm.nxt.p, cm.blk, (int)next_cols->size(), st);
+      if (timed) tm->end(b1, st, split->dft);
+      return;
+    }
     lde_coefficients(evals, n, w, cm.coef.p, st);
     if (timed) tm->end(b0, st, split->idft);
     hipEvent_t b1 = timed ? tm->begin(st) : nullptr;
     coset_residue(cm.coef.p, n, w, lde_shift, plan->lg, plan->r, cm.lde.buf.p, st);
-    cm.nxt_row0 = (size_t)plan->k2 * cm.blk;  // = row0 for G = 2
-    if (next_cols && !next_cols->empty() && plan->G >= 4) {
-      cm.nxt.reset(cm.blk * next_cols->size());
-      coset_residue_cols(cm.coef.p, n, *next_cols, lde_shift, plan->lg, plan->r2, cm.nxt.p, st);
-      cm.nmap.fill(0);  // columns not read at the next row: any valid column
-      for (size_t y = 0; y < next_cols->size(); y++) cm.nmap[(*next_cols)[y]] = (uint8_t)y;
-    }
+    if (nx) coset_residue_cols(cm.coef.p, n, *next_cols, lde_shift, plan->lg, plan->r2, cm.nxt.p, st);
     if (timed) tm->end(b1, st, split->dft);
     return;
   }
