@@ -273,6 +273,15 @@ void spin_sync(hipStream_t st);
 // returns when the data has arrived.
 void upload_bulk(void* dst, const void* src, size_t bytes, hipStream_t st);
 
+// Many strided 2D word copies in one launch (runtime.hip): rows x width words from src (row
+// stride sstride words) to dst (dstride), 16-byte vectors where every copy allows them.
+struct Copy2D {
+  const uint32_t* src;
+  uint32_t* dst;
+  size_t sstride, dstride, width, rows;
+};
+void copy2d_batch(const std::vector<Copy2D>& v, hipStream_t st);
+
 // Per-launch HIP-event timing of one kernel family (the roofline kernel of bench.py):
 // when `on`, callers bracket each launch with begin()/end(bytes); collect() resolves the
 // events after the stream has drained.  Event creation is host work, so it is only switched

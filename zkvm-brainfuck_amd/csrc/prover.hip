@@ -579,21 +579,23 @@ void gather_quotients(const Round& mainr, const std::vector<size_t>& hn,
     return qv[k].p + (t0 / n) * 4 * n + (t0 % n);
   };
   DBuf<uint32_t> send(total), recv(total * plan.G);
+  std::vector<Copy2D> cp;  // pack this rank's parts, then (after the all-gather) unpack the others
   for (int k = 0; k < nc; k++)
     if (mainr.mats[k].sharded) {
       const size_t n = hn[k], b = plan.blk(2 * n);
-      HIP_CHECK(hipMemcpy2DAsync(send.p + off[k], b * 4, part(k, plan.k), n * 4, b * 4, 4,
-                                 hipMemcpyDeviceToDevice, st));
+      cp.push_back({part(k, plan.k), send.p + off[k], n, b, b, 4});
     }
+  copy2d_batch(cp, st);
   HIP_CHECK(hipStreamSynchronize(st));
   sc.allgather(send.p, total * 4, recv.p);
+  cp.clear();
   for (int j = 0; j < plan.G; j++)
     for (int k = 0; k < nc; k++)
       if (mainr.mats[k].sharded && j != plan.k) {
         const size_t n = hn[k], b = plan.blk(2 * n);
-        HIP_CHECK(hipMemcpy2DAsync(part(k, j), n * 4, recv.p + (size_t)j * total + off[k], b * 4,
-                                   b * 4, 4, hipMemcpyDeviceToDevice, st));
+        cp.push_back({recv.p + (size_t)j * total + off[k], part(k, j), b, n, b, 4});
       }
+  copy2d_batch(cp, st);
 }
 }  // namespace
 
@@ -1127,10 +1129,12 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   if (plan.on()) {  // one all-gather; sharded matrices' slices summed, replicated ones kept
     DBuf<EF> all(nvals * plan.G);
     HIP_CHECK(hipStreamSynchronize(st));
+    htrace().mark("sharded openings done");
     shard->allgather(opened_d.p, nvals * sizeof(EF), all.p);
     std::vector<EF> h(nvals * plan.G);
     HIP_CHECK(hipMemcpyAsync(h.data(), all.p, h.size() * sizeof(EF), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
+    htrace().mark("sharded openings on host");
     for (int r = 0; r < 4; r++)
       for (size_t i = 0; i < rounds[r]->mats.size(); i++) {
         const CMat& m = rounds[r]->mats[i];
@@ -1177,6 +1181,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     while (have < NGROUP - 1) wait_group(++have);
     htrace().mark("opened observed");
   } else if (opt.observe_openings) {
+    htrace().mark("opened summed");
     for (int r = 0; r < 4; r++)
       for (size_t i = 0; i < rounds[r]->mats.size(); i++)
         for (int j = 0; j < mp[r][i].npts; j++)

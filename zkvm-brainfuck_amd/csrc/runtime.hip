@@ -384,3 +384,49 @@ std::vector<uint32_t> host_twiddles(int log_n, bool inverse) {
 }
 
 }  // namespace bfz
+
+namespace bfz {
+// ------------------------------------------------------------------------ batched 2D copies
+constexpr int COPY2D_MAX = 40;  // per launch (kernel-argument space)
+struct Copy2DBatch {
+  Copy2D c[COPY2D_MAX];
+};
+template <int V>  // words per access (4: uint4)
+__global__ __launch_bounds__(256) void k_copy2d_batch(Copy2DBatch b) {
+  const Copy2D c = b.c[blockIdx.y];
+  const size_t wv = c.width / V, total = wv * c.rows;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (size_t)gridDim.x * blockDim.x) {
+    const size_t r = e / wv, x = (e - r * wv) * V;
+    if constexpr (V == 4)
+      *reinterpret_cast<uint4*>(c.dst + r * c.dstride + x) =
+          *reinterpret_cast<const uint4*>(c.src + r * c.sstride + x);
+    else
+      c.dst[r * c.dstride + x] = c.src[r * c.sstride + x];
+  }
+}
+
+void copy2d_batch(const std::vector<Copy2D>& v, hipStream_t st) {
+  for (size_t i0 = 0; i0 < v.size(); i0 += COPY2D_MAX) {
+    Copy2DBatch b{};
+    const int cnt = (int)std::min<size_t>(COPY2D_MAX, v.size() - i0);
+    bool vec = true;
+    size_t most = 0;
+    for (int i = 0; i < cnt; i++) {
+      const Copy2D& c = v[i0 + i];
+      b.c[i] = c;
+      vec = vec && c.width % 4 == 0 && c.sstride % 4 == 0 && c.dstride % 4 == 0 &&
+            ((uintptr_t)c.src & 15) == 0 && ((uintptr_t)c.dst & 15) == 0;
+      most = std::max(most, c.width * c.rows);
+    }
+    if (!most) continue;
+    const dim3 grid((unsigned)std::min<size_t>(ceil_div(most, (size_t)(vec ? 4 : 1) * 256), 1024),
+                    cnt);
+    if (vec)
+      hipLaunchKernelGGL(k_copy2d_batch<4>, grid, dim3(256), 0, st, b);
+    else
+      hipLaunchKernelGGL(k_copy2d_batch<1>, grid, dim3(256), 0, st, b);
+    KCHECK();
+  }
+}
+}  // namespace bfz
