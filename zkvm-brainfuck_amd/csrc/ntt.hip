@@ -340,11 +340,21 @@ struct MidPlan {
 // +0.08 ms of NTT kernel time per proof at 2 (profiles/r06/ab_mid_cpb.txt): 1.
 constexpr int MID_CPB = BFZ_MID_CPB;
 
+// Where k_lde_mid writes: column y's half h at lde + y dstride + h hoff (the coset LDE: 2n, n;
+// a 2-GPU shard, one half per rank: n, 0), plus -- coef != nullptr -- the coefficients k in
+// [j0, j0 + len) of column y at coef + y n (the sharded proof's opening range).
+struct MidOut {
+  size_t dstride, hoff;
+  uint32_t* coef;
+  size_t j0, len;
+};
+
 template <int L>
 __device__ __forceinline__ void lde_mid_col(
     const uint32_t* __restrict__ src, size_t src_stride, uint32_t* __restrict__ lde, size_t n,
     const uint32_t* __restrict__ tw_inv, const uint32_t* __restrict__ tw_fwd,
-    const uint32_t* __restrict__ pw, int B, const MidPowers& mp, int only_half, uint32_t by) {
+    const uint32_t* __restrict__ pw, int B, const MidPowers& mp, int only_half, uint32_t by,
+    const MidOut& mo) {
   constexpr int s0 = MidPlan<L>::b1, b = MidPlan<L>::b2, c = MidPlan<L>::c2;
   extern __shared__ uint32_t lds[];
   const int tid = threadIdx.x;
@@ -354,7 +364,7 @@ __device__ __forceinline__ void lde_mid_col(
   const size_t hi = (size_t)bx >> nlo_log;
   const size_t base = (hi << (s0 + b)) + (lo_blk << c);
   const uint32_t* S = src + (size_t)by * src_stride + base;
-  uint32_t* D = lde + (size_t)by * 2 * n + base;
+  uint32_t* D = lde + (size_t)by * mo.dstride + base;
   const int lo = tid & ((1 << c) - 1);
   const uint32_t lo_g = (uint32_t)(lo_blk << c) + lo;
   const int rest = tid >> c;
@@ -393,6 +403,14 @@ __device__ __forceinline__ void lde_mid_col(
     const int g0 = b - 4;
     const uint32_t m_base = (rest & ((1 << g0) - 1)) | ((uint32_t)(rest >> g0) << (g0 + 4));
     const size_t k0 = base + ((size_t)m_base << s0) + lo;
+    if (mo.coef) {  // the sharded proof's opening range of the coefficients (see k_coef_fold)
+      uint32_t* C = mo.coef + (size_t)by * n;
+#pragma unroll
+      for (int i = 0; i < 16; i++) {
+        const size_t k = k0 + ((size_t)i << (L - 4));
+        if (k - mo.j0 < mo.len) C[k] = coef[i];
+      }
+    }
     const size_t mask = ((size_t)1 << B) - 1, nb = mask + 1;
     const uint32_t S0 = mmul(pw[k0 & mask], pw[nb + (k0 >> B)]);
     const uint32_t T0 = mmul(pw[2 * nb + (k0 & mask)], pw[3 * nb + (k0 >> B)]);
@@ -402,7 +420,7 @@ __device__ __forceinline__ void lde_mid_col(
 #pragma unroll
       for (int i = 0; i < 16; i++) x[i] = mmul(coef[i], mmul(P0, half ? mp.hi[i] : mp.lo[i]));
       if (half && nwin > 1) __syncthreads();  // the lo half's last LDS reads are done
-      uint32_t* Dh = D + (size_t)half * n;
+      uint32_t* Dh = D + (size_t)half * mo.hoff;
       int done_hi = b;
 #pragma unroll
       for (int w = 0; w < nwin; w++) {  // DFT of this half
@@ -454,9 +472,15 @@ struct CoefFold {
   uint8_t nidx[64];  // input column -> r[1] output column (0xff: not read at the next row)
 };
 
-template <int L>
+// R > 0 (S = 2^R outputs per thread, G = 2^(5 - R) ranks): the thread's S outputs d_u are the
+// first radix-S window of the residue's size-m DIF (stride D = m / S), and the block's outputs
+// are a whole tile of its strided stages [s0, log m): those run here too (radix-S windows through
+// LDS), so only the contiguous tile pass of stages [0, s0) is left (residue_dft).  R = 0: the
+// folds alone, S at run time.
+template <int L, int R>
 __device__ __forceinline__ void coef_fold_col(const uint32_t* __restrict__ src, size_t n,
                                               const uint32_t* __restrict__ tw_inv,
+                                              const uint32_t* __restrict__ tw_fwd,
                                               const CoefFold& cf, uint32_t by) {
   constexpr int s0 = MidPlan<L>::b1, b = MidPlan<L>::b2, c = MidPlan<L>::c2;
   extern __shared__ uint32_t lds[];
@@ -509,6 +533,7 @@ __device__ __forceinline__ void coef_fold_col(const uint32_t* __restrict__ src, 
     if (k - cf.j0 < cf.len) C[k] = x[i];  // the rank's opening range only
   }
   const size_t mask = ((size_t)1 << cf.B) - 1, nb = mask + 1;
+  const int SS = R ? 1 << R : cf.S;
 #pragma unroll
   for (int q = 0; q < 2; q++) {
     const ResidueFold& rf = cf.r[q];
@@ -522,34 +547,69 @@ __device__ __forceinline__ void coef_fold_col(const uint32_t* __restrict__ src, 
 #pragma unroll
     for (int st = 0; st < 4; st++) {
       const int h = 8 >> st;
-      if (h < cf.S) break;
+      if (h < SS) break;
 #pragma unroll
       for (int i = 0; i < h; i++) y[i] = madd(y[i], mmul(y[i + h], rf.A[st]));
     }
     const uint32_t ak0 = mmul(rf.pw[k0 & mask], rf.pw[nb + (k0 >> cf.B)]);  // a^k0 / n
-    uint32_t* O = rf.out + (size_t)oc * cf.m + k0;
+    if constexpr (R == 0) {
+      uint32_t* O = rf.out + (size_t)oc * cf.m + k0;
 #pragma unroll
-    for (int i = 0; i < 16; i++)
-      if (i < cf.S) O[(size_t)i * D] = mmul(y[i], mmul(ak0, rf.Q[i]));
+      for (int i = 0; i < 16; i++)
+        if (i < SS) O[(size_t)i * D] = mmul(y[i], mmul(ak0, rf.Q[i]));
+    } else {
+      constexpr int E = 1 << R, bp = b - 4 + R, nw = (bp + R - 1) / R;
+      uint32_t z[E];
+#pragma unroll
+      for (int i = 0; i < E; i++) z[i] = mmul(y[i], mmul(ak0, rf.Q[i]));
+      uint32_t* O = rf.out + (size_t)oc * cf.m + base;
+      __syncthreads();  // the previous phase's LDS reads are done
+      int done_hi = bp;
+#pragma unroll
+      for (int w = 0; w < nw; w++) {  // DIF stages [s0, s0 + bp) of the size-m transform
+        const int gg = max(bp - R - R * w, 0);
+        const uint32_t m_low = rest & ((1 << gg) - 1);
+        const uint32_t mb = m_low | ((uint32_t)(rest >> gg) << (gg + R));
+        if (w > 0) {
+          __syncthreads();
+#pragma unroll
+          for (int i = 0; i < E; i++)
+            z[i] = lds[lds_pad((int)(((mb | ((uint32_t)i << gg)) << c) | lo), c)];
+        }
+        const int kk_hi = min(R, done_hi - gg);
+        done_hi = gg;
+        r16_window<true, false, true, R>(z, gg, 0, kk_hi, s0, m_low, lo_g, tw_fwd);
+        if (w == nw - 1) {
+#pragma unroll
+          for (int i = 0; i < E; i++)
+            O[((size_t)mb << s0) + lo + ((size_t)i << (gg + s0))] = z[i];
+        } else {
+#pragma unroll
+          for (int i = 0; i < E; i++)
+            lds[lds_pad((int)(((mb | ((uint32_t)i << gg)) << c) | lo), c)] = z[i];
+        }
+      }
+    }
   }
 }
 
-template <int L>
+template <int L, int R>
 __global__ __launch_bounds__(1 << (MidPlan<L>::b2 + MidPlan<L>::c2 - 4)) void k_coef_fold(
-    const uint32_t* __restrict__ src, size_t n, const uint32_t* __restrict__ tw_inv, CoefFold cf) {
-  coef_fold_col<L>(src, n, tw_inv, cf, blockIdx.y);
+    const uint32_t* __restrict__ src, size_t n, const uint32_t* __restrict__ tw_inv,
+    const uint32_t* __restrict__ tw_fwd, CoefFold cf) {
+  coef_fold_col<L, R>(src, n, tw_inv, tw_fwd, cf, blockIdx.y);
 }
 
 template <int L>
 __global__ __launch_bounds__(1 << (MidPlan<L>::b2 + MidPlan<L>::c2 - 4)) void k_lde_mid(
     const uint32_t* __restrict__ src, size_t src_stride, uint32_t* __restrict__ lde, size_t n,
     const uint32_t* __restrict__ tw_inv, const uint32_t* __restrict__ tw_fwd,
-    const uint32_t* __restrict__ pw, int B, MidPowers mp, int only_half, int w) {
+    const uint32_t* __restrict__ pw, int B, MidPowers mp, int only_half, int w, MidOut mo) {
   for (int cc = 0; cc < MID_CPB; cc++) {
     const uint32_t by = blockIdx.y * MID_CPB + cc;
     if (by >= (uint32_t)w) break;  // uniform across the block
     if (cc) __syncthreads();       // the previous column's last LDS reads are done
-    lde_mid_col<L>(src, src_stride, lde, n, tw_inv, tw_fwd, pw, B, mp, only_half, by);
+    lde_mid_col<L>(src, src_stride, lde, n, tw_inv, tw_fwd, pw, B, mp, only_half, by, mo);
   }
 }
 
@@ -646,16 +706,18 @@ static void r16_attrs() {
                       (const void*)&k_lde_mid<18>, (const void*)&k_lde_mid<19>,
                       (const void*)&k_lde_mid<20>, (const void*)&k_lde_mid<21>,
                       (const void*)&k_lde_mid<22>, (const void*)&k_lde_mid<23>,
-                      (const void*)&k_coef_fold<15>, (const void*)&k_coef_fold<16>,
-                      (const void*)&k_coef_fold<17>, (const void*)&k_coef_fold<18>,
-                      (const void*)&k_coef_fold<19>, (const void*)&k_coef_fold<20>,
-                      (const void*)&k_coef_fold<21>, (const void*)&k_coef_fold<22>,
-                      (const void*)&k_coef_fold<23>,
                       (const void*)&k_ntt_tile<true, R16_TILE_LOG, false, true, true>,
                       (const void*)&k_ntt_tile<false, R16_TILE_LOG, true, true, true>,
                       (const void*)&k_ntt_tile<false, R16_TILE_LOG, false, true, true>};
   for (const void* f : fs)
     HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+#define BFZ_CF_ATTR(LL)                                                                        \
+  for (const void* f : {(const void*)&k_coef_fold<LL, 0>, (const void*)&k_coef_fold<LL, 2>,   \
+                        (const void*)&k_coef_fold<LL, 3>})                                     \
+    HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  BFZ_CF_ATTR(15) BFZ_CF_ATTR(16) BFZ_CF_ATTR(17) BFZ_CF_ATTR(18) BFZ_CF_ATTR(19) BFZ_CF_ATTR(20)
+  BFZ_CF_ATTR(21) BFZ_CF_ATTR(22) BFZ_CF_ATTR(23)
+#undef BFZ_CF_ATTR
   });
 }
 
@@ -810,6 +872,49 @@ void prepare_lde_tables(int L) {
   (void)scale_tables(minv(two_adic_gen(L + 1)), L, B);
 }
 
+// The fused middle pass (k_lde_mid) of an L > 14 coset LDE over the iDFT's first-pass output
+// `coef` (w columns of n): coefficients, scaled by the coset powers, DIF stages of pass 2.
+static void mid_launch(const uint32_t* coef, size_t n, int w, uint32_t shift, uint32_t* lde,
+                       int only_half, const MidOut& mo, hipStream_t st) {
+  const int L = log2i(n);
+  Twiddles& T = twiddles();
+  T.ensure(L);
+  r16_attrs();
+  const R16Pass p2 = r16_plan(L)[1];
+  const int B = (L + 1) / 2;
+  const uint32_t* pw = scale_tables(shift, L, B);
+  MidPowers mp;
+  const uint64_t D = (uint64_t)1 << (p2.s0 + p2.b - 4);
+  const uint32_t gs = mpow(shift, D), gt = mpow(mmul(shift, two_adic_gen(L + 1)), D);
+  uint32_t a = ONE, c = ONE;
+  for (int i = 0; i < 16; i++) {
+    mp.lo[i] = a;
+    mp.hi[i] = c;
+    a = mmul(a, gs);
+    c = mmul(c, gt);
+  }
+  const int threads = 1 << (p2.b + p2.c - 4);
+  const size_t ldsz = ((size_t)1 << (p2.b + p2.c)) + ((size_t)1 << (p2.b + p2.c - 4));
+  KernelProbe& probe = ntt_probe();
+  hipEvent_t ev0 = probe.on ? probe.begin(st) : nullptr;
+  const dim3 grid(1u << (L - p2.b - p2.c), ceil_div(w, MID_CPB));
+#define BFZ_MID(LL)                                                                              \
+  case LL:                                                                                       \
+    static_assert(MidPlan<LL>::b2 >= 4, "plan");                                                 \
+    hipLaunchKernelGGL(k_lde_mid<LL>, grid, dim3(threads), ldsz * 4, st, coef, n, lde, n,        \
+                       (const uint32_t*)T.inv(), (const uint32_t*)T.fwd(), pw, B, mp, only_half, \
+                       w, mo);                                                                   \
+    break;
+  switch (L) {
+    BFZ_MID(14) BFZ_MID(15) BFZ_MID(16) BFZ_MID(17) BFZ_MID(18) BFZ_MID(19) BFZ_MID(20) BFZ_MID(21)
+    BFZ_MID(22) BFZ_MID(23)
+    default: throw std::runtime_error("coset_lde: log height above 23");
+  }
+#undef BFZ_MID
+  KCHECK();
+  if (probe.on) probe.end(ev0, st, (only_half >= 0 ? 8.0 : 12.0) * (double)n * w);
+}
+
 void coset_lde(const uint32_t* evals, size_t n, int w, uint32_t shift, uint32_t* lde,
                hipStream_t st) {
   coset_lde_ex(evals, n, n, w, shift, lde, -1, st);
@@ -823,47 +928,11 @@ void coset_lde_ex(const uint32_t* evals, size_t src_stride, size_t n, int w, uin
   const size_t dft_stride = only_half >= 0 ? 2 * n : n;
   const int dft_cols = only_half >= 0 ? w : 2 * w;
   if (L > R16_TILE_LOG) {  // iDFT pass 1 -> fused middle -> DFT last pass (3 HBM passes)
-    Twiddles& T = twiddles();
-    T.ensure(L);
-    r16_attrs();
     const auto plan = r16_plan(L);  // {(0, b1, 0), (b1, b2, c2)}
-    const R16Pass& p1 = plan[0];
-    const R16Pass& p2 = plan[1];
     DBuf<uint32_t> coef(n * (size_t)w);
-    r16_launch(p1, evals, src_stride, coef.p, n, w, L, false, st);
-    const int B = (L + 1) / 2;
-    const uint32_t* pw = scale_tables(shift, L, B);
-    MidPowers mp;
-    const uint64_t D = (uint64_t)1 << (p2.s0 + p2.b - 4);
-    const uint32_t gs = mpow(shift, D), gt = mpow(mmul(shift, two_adic_gen(L + 1)), D);
-    uint32_t a = ONE, c = ONE;
-    for (int i = 0; i < 16; i++) {
-      mp.lo[i] = a;
-      mp.hi[i] = c;
-      a = mmul(a, gs);
-      c = mmul(c, gt);
-    }
-    const int threads = 1 << (p2.b + p2.c - 4);
-    const size_t ldsz = ((size_t)1 << (p2.b + p2.c)) + ((size_t)1 << (p2.b + p2.c - 4));
-    KernelProbe& probe = ntt_probe();
-    hipEvent_t ev0 = probe.on ? probe.begin(st) : nullptr;
-    const dim3 grid(1u << (L - p2.b - p2.c), ceil_div(w, MID_CPB));
-#define BFZ_MID(LL)                                                                              \
-  case LL:                                                                                       \
-    static_assert(MidPlan<LL>::b2 >= 4, "plan");                                                 \
-    hipLaunchKernelGGL(k_lde_mid<LL>, grid, dim3(threads), ldsz * 4, st, (const uint32_t*)coef.p, \
-                       n, lde, n, (const uint32_t*)T.inv(), (const uint32_t*)T.fwd(), pw, B, mp, \
-                       only_half, w);                                                            \
-    break;
-    switch (L) {
-      BFZ_MID(14) BFZ_MID(15) BFZ_MID(16) BFZ_MID(17) BFZ_MID(18) BFZ_MID(19) BFZ_MID(20) BFZ_MID(21)
-      BFZ_MID(22) BFZ_MID(23)
-      default: throw std::runtime_error("coset_lde: log height above 23");
-    }
-#undef BFZ_MID
-    KCHECK();
-    if (probe.on) probe.end(ev0, st, (only_half >= 0 ? 8.0 : 12.0) * (double)n * w);
-    r16_launch(p1, dft_base, dft_stride, dft_base, dft_stride, dft_cols, L, true, st);
+    r16_launch(plan[0], evals, src_stride, coef.p, n, w, L, false, st);
+    mid_launch(coef.p, n, w, shift, lde, only_half, MidOut{2 * n, n, nullptr, 0, 0}, st);
+    r16_launch(plan[0], dft_base, dft_stride, dft_base, dft_stride, dft_cols, L, true, st);
     return;
   }
   DBuf<uint32_t> coef(n * (size_t)w);
@@ -987,21 +1056,30 @@ static ResidueFold residue_fold(uint32_t shift, int L, int logG, int r, int S, u
   return f;
 }
 
-static bool fused_residues_on() {
-  static const bool on = [] {
-    const char* e = getenv("BFZ_FUSED_RESIDUE");
-    return !(e && e[0] == '0');
-  }();
+static bool env_on(const char* name) {
+  const char* e = getenv(name);
+  return !(e && e[0] == '0');
+}
+static bool fused_residues_on() {  // BFZ_FUSED_RESIDUE=0: the unfused round-5 path (A/B)
+  static const bool on = env_on("BFZ_FUSED_RESIDUE");
+  return on;
+}
+static bool mid_half_on() {  // BFZ_MID_HALF=0: two ranks use k_coef_fold too (A/B)
+  static const bool on = env_on("BFZ_MID_HALF");
+  return on;
+}
+static bool fused_dif_on() {  // BFZ_FUSED_DIF=0: k_coef_fold leaves the whole DFT (A/B)
+  static const bool on = env_on("BFZ_FUSED_DIF");
   return on;
 }
 
-bool coef_fold_residues(const uint32_t* evals, size_t n, int w, uint32_t* coef, size_t j0,
-                        size_t len, uint32_t shift, int logG, int r, uint32_t* out,
-                        const std::vector<int>* next_cols, int r2, uint32_t* nxt, hipStream_t st) {
+int coef_fold_residues(const uint32_t* evals, size_t n, int w, uint32_t* coef, size_t j0,
+                       size_t len, uint32_t shift, int logG, int r, uint32_t* out,
+                       const std::vector<int>* next_cols, int r2, uint32_t* nxt, hipStream_t st) {
   const int L = log2i(n);
   if (!fused_residues_on() || L <= R16_TILE_LOG || L > 23 || logG < 1 || logG > 5 || w < 1 ||
       w > 64)
-    return false;
+    return 0;
   Twiddles& T = twiddles();
   T.ensure(L);
   r16_attrs();
@@ -1009,6 +1087,12 @@ bool coef_fold_residues(const uint32_t* evals, size_t n, int w, uint32_t* coef, 
   const R16Pass& p1 = plan[0];
   const R16Pass& p2 = plan[1];
   r16_launch(p1, evals, n, coef, n, w, L, false, st);
+  if (logG == 1 && !(next_cols && !next_cols->empty()) && mid_half_on()) {
+    // two ranks: the residue coset is one half of the coset LDE -- k_lde_mid's half r, written
+    // at stride n, with the coefficient range on the side; only the DIF tile pass is left
+    mid_launch(coef, n, w, shift, out, r, MidOut{n, 0, coef, j0, len}, st);
+    return 100 + p2.s0;
+  }
   CoefFold cf{};
   cf.coef = coef;
   cf.j0 = j0;
@@ -1025,10 +1109,21 @@ bool coef_fold_residues(const uint32_t* evals, size_t n, int w, uint32_t* coef, 
   const int threads = 1 << (p2.b + p2.c - 4);
   const size_t ldsz = ((size_t)1 << (p2.b + p2.c)) + ((size_t)1 << (p2.b + p2.c - 4));
   const dim3 grid(1u << (L - p2.b - p2.c), w);
-#define BFZ_CF(LL)                                                                           \
-  case LL:                                                                                   \
-    hipLaunchKernelGGL(k_coef_fold<LL>, grid, dim3(threads), ldsz * 4, st,                   \
-                       (const uint32_t*)coef, n, (const uint32_t*)T.inv(), cf);              \
+  // the strided DIF stages run in the kernel for 4 and 8 ranks (R = 3, 2)
+  const int R = fused_dif_on() && (logG == 2 || logG == 3) ? 5 - logG : 0;
+  const uint32_t* ti = (const uint32_t*)T.inv();
+  const uint32_t* tf = (const uint32_t*)T.fwd();
+#define BFZ_CF(LL)                                                                             \
+  case LL:                                                                                     \
+    if (R == 3)                                                                                \
+      hipLaunchKernelGGL((k_coef_fold<LL, 3>), grid, dim3(threads), ldsz * 4, st,              \
+                         (const uint32_t*)coef, n, ti, tf, cf);                                \
+    else if (R == 2)                                                                           \
+      hipLaunchKernelGGL((k_coef_fold<LL, 2>), grid, dim3(threads), ldsz * 4, st,              \
+                         (const uint32_t*)coef, n, ti, tf, cf);                                \
+    else                                                                                       \
+      hipLaunchKernelGGL((k_coef_fold<LL, 0>), grid, dim3(threads), ldsz * 4, st,              \
+                         (const uint32_t*)coef, n, ti, tf, cf);                                \
     break;
   switch (L) {
     BFZ_CF(15) BFZ_CF(16) BFZ_CF(17) BFZ_CF(18) BFZ_CF(19) BFZ_CF(20) BFZ_CF(21) BFZ_CF(22)
@@ -1036,11 +1131,16 @@ bool coef_fold_residues(const uint32_t* evals, size_t n, int w, uint32_t* coef, 
   }
 #undef BFZ_CF
   KCHECK();
-  return true;
+  return R ? 100 + p2.s0 : 1;
 }
 
-void residue_dft(uint32_t* out, size_t m, int w, hipStream_t st) {
-  ntt_passes(out, out, m, m, w, log2i(m), /*dif=*/true, st);
+void residue_dft(uint32_t* out, size_t m, int w, int done, hipStream_t st) {
+  const int Lm = log2i(m);
+  if (done >= 100) {  // stages [done - 100, log m) ran in the fold kernel: the contiguous tile pass
+    r16_launch(R16Pass{0, done - 100, 0}, out, m, out, m, w, Lm, true, st);
+    return;
+  }
+  ntt_passes(out, out, m, m, w, Lm, /*dif=*/true, st);
 }
 
 void transpose_to_rowmajor(const uint32_t* colmajor, size_t H, int w, uint32_t* rowmajor,
