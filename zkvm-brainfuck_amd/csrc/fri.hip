@@ -378,16 +378,31 @@ __global__ __launch_bounds__(256) void k_reduce(const RedCol* __restrict__ cols,
   }
 }
 
-// out[t] = z^(j0 + t), t < count (eight consecutive powers per thread)
-__global__ __launch_bounds__(256) void k_pow_table(EF z, size_t j0, size_t count,
+// out[t] = z^(j0 + t), t < count.  A block writes POW_RUN x 256 consecutive powers, lane-
+// interleaved (thread tid: t = block start + tid + 256 k, stepping by z^256); a thread's first
+// power is the uniform z^(j0 + block start) times z^tid, products of the launch's squares
+// z^(2^k) (no squaring chain).
+constexpr int POW_RUN = 16;
+struct PowSquares {
+  EF sq[32];  // z^(2^k)
+};
+__global__ __launch_bounds__(256) void k_pow_table(PowSquares ps, size_t j0, size_t count,
                                                    EF* __restrict__ out) {
-  const size_t b = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
-  if (b >= count) return;
-  EF p = ef_pow(z, j0 + b);
-  const int cnt = (int)min((size_t)8, count - b);
-  for (int k = 0; k < cnt; k++) {
-    out[b + k] = p;
-    p = ef_mul(p, z);
+  const size_t b0 = (size_t)blockIdx.x * 256 * POW_RUN;
+  const uint64_t eb = j0 + b0;
+  EF p = ef_base(ONE);
+#pragma unroll
+  for (int k = 0; k < 32; k++)
+    if ((eb >> k) & 1) p = ef_mul(p, ps.sq[k]);
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    if ((threadIdx.x >> k) & 1) p = ef_mul(p, ps.sq[k]);
+#pragma unroll 4
+  for (int k = 0; k < POW_RUN; k++) {
+    const size_t t = b0 + threadIdx.x + 256 * (size_t)k;
+    if (t >= count) break;
+    out[t] = p;
+    p = ef_mul(p, ps.sq[8]);
   }
 }
 
@@ -667,8 +682,12 @@ void inv_denoms_dev(const EF* z, int logH, EF* out, hipStream_t st, EF* wout) {
 }
 
 void pow_table(const EF& z, size_t j0, size_t count, EF* out, hipStream_t st) {
-  hipLaunchKernelGGL(k_pow_table, dim3(ceil_div(ceil_div(count, 8), 256)), dim3(256), 0, st, z, j0,
-                     count, out);
+  if ((j0 + count) >> 32) throw std::runtime_error("pow_table: exponent above 2^32");
+  PowSquares ps;
+  ps.sq[0] = z;
+  for (int k = 1; k < 32; k++) ps.sq[k] = ef_mul(ps.sq[k - 1], ps.sq[k - 1]);
+  hipLaunchKernelGGL(k_pow_table, dim3(ceil_div(count, (size_t)256 * POW_RUN)), dim3(256), 0, st,
+                     ps, j0, count, out);
   KCHECK();
 }
 

@@ -761,6 +761,10 @@ static bool tile_dispatch(int b, dim3 grid, const uint32_t* in, size_t is, uint3
 static void r16_launch(const R16Pass& p, const uint32_t* in, size_t is, uint32_t* dst, size_t ds,
                        int ncols, int L, bool dif, hipStream_t st) {
   Twiddles& T = twiddles();
+  // a pass reads table entries below 2^L: a caller that skipped ensure() must not reach the GPU
+  if (T.logmax.load(std::memory_order_acquire) < L || !T.fwd())
+    throw std::logic_error("r16_launch: twiddle table not built for this height");
+  r16_attrs();  // the 2^14 tiles need more than the default dynamic LDS (once per process)
   const int threads = 1 << (p.b + p.c - 4);
   const size_t lds = ((size_t)1 << (p.b + p.c)) + ((size_t)1 << (p.b + p.c - 4));
   dim3 grid(1u << (L - p.b - p.c), ncols);
@@ -928,6 +932,8 @@ void coset_lde_ex(const uint32_t* evals, size_t src_stride, size_t n, int w, uin
   const size_t dft_stride = only_half >= 0 ? 2 * n : n;
   const int dft_cols = only_half >= 0 ? w : 2 * w;
   if (L > R16_TILE_LOG) {  // iDFT pass 1 -> fused middle -> DFT last pass (3 HBM passes)
+    twiddles().ensure(L);  // before the first pass (a process's first LDE may be this one)
+    r16_attrs();
     const auto plan = r16_plan(L);  // {(0, b1, 0), (b1, b2, c2)}
     DBuf<uint32_t> coef(n * (size_t)w);
     r16_launch(plan[0], evals, src_stride, coef.p, n, w, L, false, st);
