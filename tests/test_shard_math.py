@@ -78,3 +78,37 @@ def test_second_point_denominators_from_the_zeta_table(logh):
         lhs = pow((x - z * wn) % P, P - 2, P)
         rhs = pow(wn, P - 2, P) * pow((x2 - z) % P, P - 2, P) % P
         assert lhs == rhs
+
+
+@pytest.mark.parametrize("lg", [1, 2, 3, 4])
+def test_register_fold_halving_steps(lg):
+    """ntt.hip k_coef_fold: a thread of the iDFT's second pass holds the 16 coefficients
+    c_(k0 + i D), D = n / 16.  For G = 2^lg ranks (m = 2n / G = S D, S = 2^(5 - lg) outputs per
+    thread) the fold d_u = a^u sum_l c_(u + l m) (a^m)^l of u = k0 + i0 D, i0 < S, uses exactly the
+    thread's terms i0 + l S, and the halving steps y_i += y_(i + h) (a^m)^(h / S), h = 8 .. S,
+    compute the sums sum_l x_(i0 + l S) (a^m)^l."""
+    rng = random.Random(lg)
+    logn = 8
+    n = 1 << logn
+    D = n // 16
+    m = 2 * n >> lg
+    S = m // D
+    assert S == 1 << (5 - lg)
+    c = [rng.randrange(P) for _ in range(n)]
+    a = rng.randrange(1, P)
+    am = pow(a, m, P)
+    ref = [sum(c[j] * pow(a, j, P) for j in range(u, n, m)) % P for u in range(m)]
+    got = [None] * m
+    for k0 in range(D):
+        x = [c[k0 + i * D] for i in range(16)]
+        y = list(x)
+        h = 8
+        while h >= S:
+            f = pow(am, h // S, P)
+            for i in range(h):
+                y[i] = (y[i] + y[i + h] * f) % P
+            h //= 2
+        for i0 in range(S):
+            u = k0 + i0 * D
+            got[u] = y[i0] * pow(a, u, P) % P
+    assert got == ref
