@@ -906,9 +906,12 @@ def main():
                 "logup_stage_parts": {
                     "replicated": ["perm_rows_ms (permutation rows + cumulative-sum scan: whole "
                                    "rows of the trace domain)",
-                                   "perm_idft_ms (iDFT of every permutation column)"],
-                    "split": ["perm_dft_ms (fold onto the rank's residue coset + forward DFT of "
-                              "size 2n/N, plus the next-residue shards at N >= 4)",
+                                   "perm_idft_ms (iDFT of every permutation column; since "
+                                   "round 6 with the residue folds and, at N = 2 / 4 / 8, the "
+                                   "strided stages of the forward DFT fused into its second pass "
+                                   "-- k_lde_mid / k_coef_fold)"],
+                    "split": ["perm_dft_ms (the contiguous tile pass of the size-2n/N forward "
+                              "DFT, for the next-residue shards too at N >= 4)",
                               "perm_hash_ms (this rank's Merkle subtree)"]}}
         if world == 1 and not args.no_extra:
             line["end_to_end"] = end_to_end(client, pk, prog, stdin)
