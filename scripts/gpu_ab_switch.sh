@@ -21,7 +21,7 @@ for rep in $(seq 1 ${AB_REPS:-3}); do
     env $arm timeout -k 10 300 python bench.py ${AB_ARGS:---steps 10 --warmup 2 --no-cpu-baseline --no-extra --no-cold --sustain-s 0 --solo-world 0} > gpurun_out/ab_${N}_$i.json 2>gpurun_out/ab_${N}_$i.err || { tail -20 gpurun_out/ab_${N}_$i.err; exit 1; }
     python3 -c "
 import json;d=json.loads(open('gpurun_out/ab_${N}_$i.json').read().strip().splitlines()[-1]);s=d['stages_ms']
-print('$arm', d['value'], 'ntt', s['ntt_kernel_ms'], 'p2', s['p2_kernel_ms'], 'open', s['open_kernel_ms'], 'reduce', s['reduce_kernel_ms'], 'stages', [round(s[k],3) for k in ('main_commit_ms','perm_ms','quotient_ms','open_ms','fri_ms')])" | tee -a $O
+print('$arm', d['value'], 'ntt', s['ntt_kernel_ms'], 'p2', s['p2_kernel_ms'], 'open', s['open_kernel_ms'], 'reduce', s['reduce_kernel_ms'], 'perm_rows', s.get('perm_rows_ms'), 'stages', [round(s[k],3) for k in ('main_commit_ms','perm_ms','quotient_ms','open_ms','fri_ms')])" | tee -a $O
   done
 done
 cat $O

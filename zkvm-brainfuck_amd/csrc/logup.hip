@@ -196,6 +196,99 @@ void ef_inclusive_scan(EF* data, size_t n, hipStream_t st) {
   }
 }
 
+// ------------------------------------------------ LogUp running sum by tiles (n >= 2^11)
+// Natural row i = x 2^(L-5) + z (x < 32, z < Z = n / 32) is stored at t = rev(z) 32 + rev5(x):
+// for a fixed z the 32 rows x fill one contiguous run of storage.  A block owns the tile of
+// every x and PHI_Z consecutive z and reads / writes whole runs (no bit-reversed gather):
+//   k_phi_sums: the tile's sum per x -> S[x nb + b] (row-major = the natural order of tile rows);
+//   ef_inclusive_scan(S): the natural-order prefix of every tile row;
+//   k_phi_write: the tile's scans plus that prefix, written as the last EF column.
+constexpr int PHI_X = 32, PHI_Z = 64, PHI_T = 256;  // 2048 rows per tile, 8 per thread
+constexpr int PHI_LOG_MIN = 11;                      // Z >= PHI_Z
+
+struct PhiTile {
+  EF m[PHI_X][PHI_Z + 1];  // natural (x, z) order, padded
+  EF part[PHI_T];
+};
+
+__device__ __forceinline__ void phi_load(PhiTile& tl, const EF* __restrict__ rows, int logn,
+                                         size_t z0) {
+  const int lz = logn - 5;
+#pragma unroll
+  for (int q = 0; q < PHI_X * PHI_Z / PHI_T; q++) {
+    const int e = q * PHI_T + threadIdx.x, zl = e >> 5, xr = e & 31;
+    const size_t t = ((size_t)dbitrev((uint32_t)(z0 + zl), lz) << 5) | (size_t)xr;
+    tl.m[dbitrev((uint32_t)xr, 5)][zl] = rows[t];
+  }
+}
+
+// this thread's 8 elements of tile row x = tid / 8 (z in [8 part, 8 part + 8)): local sum
+__device__ __forceinline__ EF phi_part_sum(const PhiTile& tl) {
+  const int x = threadIdx.x >> 3, part = threadIdx.x & 7;
+  EF s = ef_zero();
+#pragma unroll
+  for (int k = 0; k < 8; k++) s = ef_add(s, tl.m[x][8 * part + k]);
+  return s;
+}
+
+__global__ __launch_bounds__(PHI_T) void k_phi_sums(const EF* __restrict__ rows, int logn,
+                                                    EF* __restrict__ sums) {
+  __shared__ PhiTile tl;
+  const size_t nb = ((size_t)1 << (logn - 5)) / PHI_Z, b = blockIdx.x;
+  phi_load(tl, rows, logn, b * PHI_Z);
+  __syncthreads();
+  tl.part[threadIdx.x] = phi_part_sum(tl);
+  __syncthreads();
+  if ((threadIdx.x & 7) == 0) {
+    EF s = ef_zero();
+#pragma unroll
+    for (int k = 0; k < 8; k++) s = ef_add(s, tl.part[threadIdx.x + k]);
+    sums[(size_t)(threadIdx.x >> 3) * nb + b] = s;
+  }
+}
+
+__global__ __launch_bounds__(PHI_T) void k_phi_write(const EF* __restrict__ rows, int logn,
+                                                     const EF* __restrict__ scanned,
+                                                     uint32_t* __restrict__ perm, int col0,
+                                                     EF* __restrict__ cumsum) {
+  __shared__ PhiTile tl;
+  const size_t n = (size_t)1 << logn, nb = (n >> 5) / PHI_Z, b = blockIdx.x;
+  const int lz = logn - 5;
+  phi_load(tl, rows, logn, b * PHI_Z);
+  __syncthreads();
+  const int x = threadIdx.x >> 3, part = threadIdx.x & 7;
+  tl.part[threadIdx.x] = phi_part_sum(tl);
+  __syncthreads();
+  // prefix of this thread's run: every earlier tile row (scan of S), then the earlier parts
+  const size_t r = (size_t)x * nb + b;
+  EF run = r ? scanned[r - 1] : ef_zero();
+  for (int k = 0; k < part; k++) run = ef_add(run, tl.part[threadIdx.x - part + k]);
+  __syncthreads();  // every part read before the tile is overwritten
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    run = ef_add(run, tl.m[x][8 * part + k]);
+    tl.m[x][8 * part + k] = run;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < PHI_X * PHI_Z / PHI_T; q++) {
+    const int e = q * PHI_T + threadIdx.x, zl = e >> 5, xr = e & 31;
+    const size_t t = ((size_t)dbitrev((uint32_t)(b * PHI_Z + zl), lz) << 5) | (size_t)xr;
+    const EF v = tl.m[dbitrev((uint32_t)xr, 5)][zl];
+#pragma unroll
+    for (int c = 0; c < 4; c++) perm[(size_t)(col0 + c) * n + t] = v.c[c];
+    if (t == n - 1) *cumsum = v;
+  }
+}
+
+static bool phi_tiles_on() {  // BFZ_PHI_TILES=0: the round-5 gather scan (A/B)
+  static const bool on = [] {
+    const char* e = std::getenv("BFZ_PHI_TILES");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <int CHIP>
 static void launch_rows(const uint32_t* mainc, const uint32_t* prepc, size_t n,
                         const PermChallenges* ch, uint32_t* perm, EF* rowsum, hipStream_t st) {
@@ -207,7 +300,7 @@ static void launch_rows(const uint32_t* mainc, const uint32_t* prepc, size_t n,
 void perm_trace(int chip, const uint32_t* mainc, const uint32_t* prepc, size_t n,
                 const PermChallenges* ch, uint32_t* perm, EF* cumsum_dev, hipStream_t st) {
   const int logn = log2i(n);
-  DBuf<EF> rows(n), nat(n);
+  DBuf<EF> rows(n);
   switch (chip) {
     case CHIP_CPU: launch_rows<CHIP_CPU>(mainc, prepc, n, ch, perm, rows.p, st); break;
     case CHIP_PROGRAM: launch_rows<CHIP_PROGRAM>(mainc, prepc, n, ch, perm, rows.p, st); break;
@@ -219,16 +312,28 @@ void perm_trace(int chip, const uint32_t* mainc, const uint32_t* prepc, size_t n
     case CHIP_IO: launch_rows<CHIP_IO>(mainc, prepc, n, ch, perm, rows.p, st); break;
     default: throw std::runtime_error("perm_trace: bad chip");
   }
+  const int col0 = 4 * (perm_width(chip) - 1);
+  if (logn >= PHI_LOG_MIN && phi_tiles_on()) {  // running sum by tiles of whole storage runs
+    const size_t nt = (n >> 5) / PHI_Z;          // tiles per tile row
+    DBuf<EF> sums(PHI_X * nt);
+    hipLaunchKernelGGL(k_phi_sums, dim3((unsigned)nt), dim3(PHI_T), 0, st, (const EF*)rows.p, logn,
+                       sums.p);
+    KCHECK();
+    ef_inclusive_scan(sums.p, PHI_X * nt, st);
+    hipLaunchKernelGGL(k_phi_write, dim3((unsigned)nt), dim3(PHI_T), 0, st, (const EF*)rows.p,
+                       logn, (const EF*)sums.p, perm, col0, cumsum_dev);
+    KCHECK();
+    return;
+  }
   // running sum in natural row order: block-local scans read the bit-reversed row sums
   // directly, the block sums are scanned, and k_write_phi adds each block's prefix while
   // scattering phi back to bit-reversed storage
   const size_t nb = (n + SCAN_BLOCK - 1) / SCAN_BLOCK;
-  DBuf<EF> sums(nb);
+  DBuf<EF> sums(nb), nat(n);
   hipLaunchKernelGGL(k_scan_block, dim3((unsigned)nb), dim3(SCAN_T), 0, st, (const EF*)rows.p,
                      logn, nat.p, n, sums.p);
   KCHECK();
   if (nb > 1) ef_inclusive_scan(sums.p, nb, st);
-  const int col0 = 4 * (perm_width(chip) - 1);
   hipLaunchKernelGGL(k_write_phi, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const EF*)nat.p, n,
                      logn, nb > 1 ? (const EF*)sums.p : nullptr, perm, col0, cumsum_dev);
   KCHECK();
