@@ -46,14 +46,15 @@ void coset_residue_cols(const uint32_t* coef, size_t n, const std::vector<int>& 
 // column's coefficients in registers, writes coef only for [j0, j0 + len) (column stride n) and
 // folds them into out (residue r, m x w, m = 2n / G) and, with next_cols, into nxt (residue r2,
 // the listed columns) -- natural order; residue_dft then finishes each (the forward DFT).
-// Returns 0 (nothing launched) where it does not apply (log n <= 14 or > 23, G > 32), else the
-// `done` to pass to residue_dft (for out and nxt alike): 1 = the whole DFT is left, 100 + s = its
-// stages [s, log m) ran in the same kernel (2, 4 and 8 ranks: at 2 ranks without a next residue
-// out is k_lde_mid's half r, at 4 and 8 the fold kernel continues with the strided DIF stages).
-int coef_fold_residues(const uint32_t* evals, size_t n, int w, uint32_t* coef, size_t j0,
+// Returns false (nothing launched) where it does not apply (log n <= 14 or > 23, G > 32);
+// else *dft_low is what residue_dft has left to do for out and nxt alike: -1 = the whole DFT,
+// s >= 0 = only its stages [0, s) (2, 4 and 8 ranks: at 2 ranks without a next residue out is
+// k_lde_mid's half r, at 4 and 8 the fold kernel continues with the strided DIF stages).
+bool coef_fold_residues(const uint32_t* evals, size_t n, int w, uint32_t* coef, size_t j0,
                         size_t len, uint32_t shift, int logG, int r, uint32_t* out,
-                        const std::vector<int>* next_cols, int r2, uint32_t* nxt, hipStream_t st);
-void residue_dft(uint32_t* out, size_t m, int w, int done, hipStream_t st);
+                        const std::vector<int>* next_cols, int r2, uint32_t* nxt, int* dft_low,
+                        hipStream_t st);
+void residue_dft(uint32_t* out, size_t m, int w, int dft_low, hipStream_t st);
 
 // Row-major natural-order host layout -> column-major bit-reversed device layout.
 void transpose_bitrev(const uint32_t* rowmajor, size_t n, int w, uint32_t* colmajor,

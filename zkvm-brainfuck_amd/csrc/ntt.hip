@@ -1079,13 +1079,14 @@ static bool fused_dif_on() {  // BFZ_FUSED_DIF=0: k_coef_fold leaves the whole D
   return on;
 }
 
-int coef_fold_residues(const uint32_t* evals, size_t n, int w, uint32_t* coef, size_t j0,
-                       size_t len, uint32_t shift, int logG, int r, uint32_t* out,
-                       const std::vector<int>* next_cols, int r2, uint32_t* nxt, hipStream_t st) {
+bool coef_fold_residues(const uint32_t* evals, size_t n, int w, uint32_t* coef, size_t j0,
+                        size_t len, uint32_t shift, int logG, int r, uint32_t* out,
+                        const std::vector<int>* next_cols, int r2, uint32_t* nxt, int* dft_low,
+                        hipStream_t st) {
   const int L = log2i(n);
   if (!fused_residues_on() || L <= R16_TILE_LOG || L > 23 || logG < 1 || logG > 5 || w < 1 ||
       w > 64)
-    return 0;
+    return false;
   Twiddles& T = twiddles();
   T.ensure(L);
   r16_attrs();
@@ -1097,7 +1098,8 @@ int coef_fold_residues(const uint32_t* evals, size_t n, int w, uint32_t* coef, s
     // two ranks: the residue coset is one half of the coset LDE -- k_lde_mid's half r, written
     // at stride n, with the coefficient range on the side; only the DIF tile pass is left
     mid_launch(coef, n, w, shift, out, r, MidOut{n, 0, coef, j0, len}, st);
-    return 100 + p2.s0;
+    *dft_low = p2.s0;
+    return true;
   }
   CoefFold cf{};
   cf.coef = coef;
@@ -1137,13 +1139,14 @@ int coef_fold_residues(const uint32_t* evals, size_t n, int w, uint32_t* coef, s
   }
 #undef BFZ_CF
   KCHECK();
-  return R ? 100 + p2.s0 : 1;
+  *dft_low = R ? p2.s0 : -1;
+  return true;
 }
 
-void residue_dft(uint32_t* out, size_t m, int w, int done, hipStream_t st) {
+void residue_dft(uint32_t* out, size_t m, int w, int dft_low, hipStream_t st) {
   const int Lm = log2i(m);
-  if (done >= 100) {  // stages [done - 100, log m) ran in the fold kernel: the contiguous tile pass
-    r16_launch(R16Pass{0, done - 100, 0}, out, m, out, m, w, Lm, true, st);
+  if (dft_low >= 0) {  // stages [dft_low, log m) ran in the fold kernel: the contiguous tile pass
+    r16_launch(R16Pass{0, dft_low, 0}, out, m, out, m, w, Lm, true, st);
     return;
   }
   ntt_passes(out, out, m, m, w, Lm, /*dif=*/true, st);

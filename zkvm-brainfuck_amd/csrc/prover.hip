@@ -348,13 +348,14 @@ static void lde_into(CMat& cm, const uint32_t* evals, size_t n, int w, uint32_t 
     const size_t len = n >> plan->lg;  // the coefficient range this rank opens (open_ood)
     hipEvent_t b0 = timed ? tm->begin(st) : nullptr;
     // iDFT + folds in one pass over the coefficients (the fold time counts as iDFT here)
-    if (const int done = coef_fold_residues(evals, n, w, cm.coef.p, (size_t)plan->k * len, len,
-                                            lde_shift, plan->lg, plan->r, cm.lde.buf.p,
-                                            nx ? next_cols : nullptr, plan->r2, cm.nxt.p, st)) {
+    int dft_low = -1;
+    if (coef_fold_residues(evals, n, w, cm.coef.p, (size_t)plan->k * len, len, lde_shift,
+                           plan->lg, plan->r, cm.lde.buf.p, nx ? next_cols : nullptr, plan->r2,
+                           cm.nxt.p, &dft_low, st)) {
       if (timed) tm->end(b0, st, split->idft);
       hipEvent_t b1 = timed ? tm->begin(st) : nullptr;
-      residue_dft(cm.lde.buf.p, cm.blk, w, done, st);
-      if (nx) residue_dft(cm.nxt.p, cm.blk, (int)next_cols->size(), done, st);
+      residue_dft(cm.lde.buf.p, cm.blk, w, dft_low, st);
+      if (nx) residue_dft(cm.nxt.p, cm.blk, (int)next_cols->size(), dft_low, st);
       if (timed) tm->end(b1, st, split->dft);
       return;
     }
