@@ -79,7 +79,7 @@ def test_poseidon2_lane_mode_parity():
     assert np.array_equal(got, O.poseidon2(ref_in).reshape(-1, 16))
 
 
-@pytest.mark.parametrize("logn,w", [(0, 3), (1, 2), (4, 31), (5, 1), (10, 45), (13, 7), (14, 5),
+@pytest.mark.parametrize("logn,w", [(0, 3), (1, 2), (4, 31), (5, 1), (6, 64), (8, 3), (9, 2), (10, 45), (13, 7), (14, 5),
                                     (16, 4), (17, 9), (18, 3), (20, 2), (22, 1)])
 def test_coset_lde_parity(logn, w):
     rng = np.random.default_rng(logn * 100 + w)

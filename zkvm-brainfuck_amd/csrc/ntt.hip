@@ -635,6 +635,61 @@ __global__ __launch_bounds__(256) void k_scale_split(const uint32_t* __restrict_
   }
 }
 
+// Coset LDE of a column of n <= 2^TINY_LOG_MAX rows in one block, through LDS: iDFT (DIT,
+// bit-reversed in -> natural coefficients, no 1/n), the coset scale of both halves (as
+// k_scale_split), the DIF of each half.  At these sizes the general path's three launches
+// (iDFT, k_scale_split, DFT) cost more than their work.
+constexpr int TINY_LOG_MAX = 8;
+__global__ __launch_bounds__(256) void k_lde_tiny(const uint32_t* __restrict__ evals,
+                                                  size_t src_stride, uint32_t* __restrict__ lde,
+                                                  int L, const uint32_t* __restrict__ tw_inv,
+                                                  const uint32_t* __restrict__ tw_fwd,
+                                                  const uint32_t* __restrict__ pw, int B,
+                                                  int only_half) {
+  __shared__ uint32_t a[1 << TINY_LOG_MAX], h[2][1 << TINY_LOG_MAX];
+  const int n = 1 << L, tid = threadIdx.x;
+  const uint32_t* S = evals + (size_t)blockIdx.x * src_stride;
+  if (tid < n) a[tid] = S[tid];
+  __syncthreads();
+  for (int s = 0; s < L; s++) {
+    const int hh = 1 << s;
+    if (tid < n / 2) {
+      const int j = tid & (hh - 1), i0 = ((tid >> s) << (s + 1)) + j, i1 = i0 + hh;
+      const uint32_t u = a[i0], v = mmul(a[i1], tw_inv[hh + j]);
+      a[i0] = madd(u, v);
+      a[i1] = msub(u, v);
+    }
+    __syncthreads();
+  }
+  const int mask = (1 << B) - 1, nb = mask + 1;
+  if (tid < n) {
+    const uint32_t c = a[tid];
+    const int kl = tid & mask, kh = tid >> B;
+    h[0][tid] = mmul(c, mmul(pw[kl], pw[nb + kh]));
+    h[1][tid] = mmul(c, mmul(pw[2 * nb + kl], pw[3 * nb + kh]));
+  }
+  __syncthreads();
+  for (int s = L - 1; s >= 0; s--) {
+    const int hh = 1 << s;
+    if (tid < n / 2) {
+      const int j = tid & (hh - 1), i0 = ((tid >> s) << (s + 1)) + j, i1 = i0 + hh;
+      const uint32_t w = tw_fwd[hh + j];
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const uint32_t u = h[q][i0], v = h[q][i1];
+        h[q][i0] = madd(u, v);
+        h[q][i1] = mmul(msub(u, v), w);
+      }
+    }
+    __syncthreads();
+  }
+  uint32_t* D = lde + (size_t)blockIdx.x * 2 * n;
+  if (tid < n) {
+    if (only_half != 1) D[tid] = h[0][tid];
+    if (only_half != 0) D[n + tid] = h[1][tid];
+  }
+}
+
 // out[c][t] = in[bitrev(t)][c]: row-major natural -> column-major bit-reversed.
 __global__ __launch_bounds__(256) void k_transpose_bitrev(const uint32_t* __restrict__ in,
                                                           uint32_t* __restrict__ out, size_t n,
@@ -876,6 +931,14 @@ void prepare_lde_tables(int L) {
   (void)scale_tables(minv(two_adic_gen(L + 1)), L, B);
 }
 
+static bool lde_tiny_on() {  // BFZ_LDE_TINY=0: the three-launch path for n <= 2^8 too (A/B)
+  static const bool on = [] {
+    const char* e = getenv("BFZ_LDE_TINY");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // The fused middle pass (k_lde_mid) of an L > 14 coset LDE over the iDFT's first-pass output
 // `coef` (w columns of n): coefficients, scaled by the coset powers, DIF stages of pass 2.
 static void mid_launch(const uint32_t* coef, size_t n, int w, uint32_t shift, uint32_t* lde,
@@ -939,6 +1002,16 @@ void coset_lde_ex(const uint32_t* evals, size_t src_stride, size_t n, int w, uin
     r16_launch(plan[0], evals, src_stride, coef.p, n, w, L, false, st);
     mid_launch(coef.p, n, w, shift, lde, only_half, MidOut{2 * n, n, nullptr, 0, 0}, st);
     r16_launch(plan[0], dft_base, dft_stride, dft_base, dft_stride, dft_cols, L, true, st);
+    return;
+  }
+  if (L >= 1 && L <= TINY_LOG_MAX && lde_tiny_on()) {  // one launch, one block per column
+    Twiddles& T = twiddles();
+    T.ensure(L);
+    const int B = (L + 1) / 2;
+    const uint32_t* pw = scale_tables(shift, L, B);
+    hipLaunchKernelGGL(k_lde_tiny, dim3(w), dim3(256), 0, st, evals, src_stride, lde, L,
+                       (const uint32_t*)T.inv(), (const uint32_t*)T.fwd(), pw, B, only_half);
+    KCHECK();
     return;
   }
   DBuf<uint32_t> coef(n * (size_t)w);
