@@ -1,43 +1,37 @@
-"""The launch sequence of one proof from a rocprofv3 --kernel-trace CSV: every dispatch of the
-chosen proof (the k-th k_trace_cpu starts proof k) with its start offset, duration, idle gap before
-it and grid size, then the kernels' summed time per phase (runs of launches between transcript
-points: the phases are cut at the challenge kernels).
-
-usage: python3 scripts/proof_sequence.py run_kernel_trace.csv [proof_index]
-"""
+#!/usr/bin/env python3
+"""The last proof of a rocprofv3 --kernel-trace CSV as a launch sequence (a proof starts at its
+k_trace_cpu): start offset (us), kernel, run length of consecutive same-name launches, summed
+duration (us), and the idle time before the run.
+  python3 scripts/proof_sequence.py run_kernel_trace.csv > sequence.txt"""
+import csv
 import sys
-
-from kernel_outliers import load
-
-CUT = ("k_challenge_perm", "k_challenge_quot", "k_challenge_zeta", "k_inv_denoms", "k_fri_finish")
 
 
 def main():
-    rows = load(sys.argv[1])
-    k = int(sys.argv[2]) if len(sys.argv) > 2 else 2
-    starts = [i for i, r in enumerate(rows) if r["name"].endswith("k_trace_cpu")]
-    a = starts[k]
-    b = starts[k + 1] if k + 1 < len(starts) else len(rows)
-    t0 = rows[a]["start"]
-    phase, phases, acc = "tracegen", [], {}
-    prev_end = rows[a]["start"]
-    for i in range(a, b):
-        r = rows[i]
-        name = r["name"]
-        if any(c in name for c in CUT):
-            phases.append((phase, acc))
-            phase, acc = name, {}
-        d = (r["end"] - r["start"]) / 1e3
-        gap = (r["start"] - prev_end) / 1e3
-        prev_end = max(prev_end, r["end"])
-        acc[name] = acc.get(name, 0.0) + d
-        print(f"{(r['start'] - t0) / 1e3:9.1f} us  {d:8.1f} us  gap {gap:6.1f}  {r['wgs']:7d} x {r['wg']:4d}  {name}")
-    phases.append((phase, acc))
-    print("\nper phase (kernel us):")
-    for name, acc in phases:
-        tot = sum(acc.values())
-        top = sorted(acc.items(), key=lambda kv: -kv[1])[:6]
-        print(f"  {name}: {tot:.1f} us; " + ", ".join(f"{n} {v:.0f}" for n, v in top))
+    rows = list(csv.DictReader(open(sys.argv[1])))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    starts = [i for i, r in enumerate(rows) if "k_trace_cpu" in r["Kernel_Name"]]
+    last = rows[starts[-1]:] if starts else rows
+    t0 = int(last[0]["Start_Timestamp"])
+    runs = []
+    prev_end = t0
+    for r in last:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        name = r["Kernel_Name"].replace("bfz::", "").split("(")[0][:56]
+        gap = max(0, s - prev_end)
+        if runs and runs[-1][1] == name:
+            runs[-1][2] += 1
+            runs[-1][3] += e - s
+            runs[-1][4] += gap
+        else:
+            runs.append([s - t0, name, 1, e - s, gap])
+        prev_end = max(prev_end, e)
+    busy = sum(r[3] for r in runs)
+    idle = sum(r[4] for r in runs)
+    print(f"launches {len(last)}, span {(prev_end - t0) / 1e3:.1f} us, busy {busy / 1e3:.1f} us, "
+          f"idle {idle / 1e3:.1f} us")
+    for off, name, cnt, dur, gap in runs:
+        print(f"{off / 1e3:9.1f} {name:56s} x{cnt:<3d} {dur / 1e3:8.1f} idle {gap / 1e3:6.1f}")
 
 
 if __name__ == "__main__":

@@ -26,6 +26,21 @@ void inv_denoms_range(const kb::EF& z, int logH, size_t t0, size_t count, kb::EF
                       hipStream_t st);
 // out[t] = z^(j0 + t), t < count
 void pow_table(const kb::EF& z, size_t j0, size_t count, kb::EF* out, hipStream_t st);
+// Several of either in one launch (a sharded proof's openings: one table per point and height,
+// one denominator range per height and point)
+struct PowJob {
+  kb::EF z;
+  size_t j0, count;
+  kb::EF* out;
+};
+void pow_tables(const std::vector<PowJob>& jobs, hipStream_t st);
+struct InvJob {
+  kb::EF z;
+  int logH;
+  size_t t0, count;
+  kb::EF* out;
+};
+void inv_denoms_ranges(const std::vector<InvJob>& jobs, hipStream_t st);
 // Coefficient-form opening (sharded proofs): out[c] = scale * sum_(t < count) coef[c * col_stride
 // + t] tab[t] for each point (tab = powers of the point from the range's first exponent).
 void open_coefficients(const uint32_t* coef, size_t col_stride, int w, size_t count,
@@ -63,6 +78,11 @@ struct OpenDesc {
   const kb::EF* zeta;
   int zlog;
   uint32_t z3n, zc, zb;
+  // tab != 0: the coefficient form of a sharded matrix (open_coefficients): mat = the first of
+  // `rows` coefficients of each column (column stride height), invd_a / invd_b = the points'
+  // power tables (the weights), scales unnegated.  rows = 0: the low coset (height / 2).
+  uint64_t rows;
+  int tab;
 };
 // Every descriptor of ds is opened at np (1 or 2) points: one partial-sum launch over all of
 // their row chunks, one final launch over all of their columns.

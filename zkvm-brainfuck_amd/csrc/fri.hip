@@ -264,8 +264,12 @@ __global__ __launch_bounds__(OPEN_T) void k_open_partial_batch(const OpenDesc* _
   // the matrix's blocks: chunk-major, o.nslab column slabs of o.slab_w columns per row chunk
   const unsigned b = blockIdx.x - o.chunk0, slab = b % o.nslab;
   const int cb = (int)slab * o.slab_w, ce = min(o.w, cb + o.slab_w);
-  open_tile<NP, false>(o.mat, o.mat2, o.w1, o.height, o.w, o.height / 2, o.logH, o.invd_a, o.invd_b,
-                       twf, partial + o.part_off, b / o.nslab, cb, ce, o.wtab);
+  if (o.tab)  // uniform: a sharded matrix's coefficient range against the power tables
+    open_tile<NP, true>(o.mat, o.mat2, o.w1, o.height, o.w, o.rows, o.logH, o.invd_a, o.invd_b,
+                        twf, partial + o.part_off, b / o.nslab, cb, ce);
+  else
+    open_tile<NP, false>(o.mat, o.mat2, o.w1, o.height, o.w, o.rows, o.logH, o.invd_a, o.invd_b,
+                         twf, partial + o.part_off, b / o.nslab, cb, ce, o.wtab);
 }
 
 // out_k[c] = scale_k * sum_chunks partial[(chunk * w + c) * NP + k]   (one block per column)
@@ -315,10 +319,15 @@ __global__ __launch_bounds__(256) void k_open_final_batch(const OpenDesc* __rest
     sa = ef_mul_base(ef_sub(zn, ef_base(o.z3n)), o.zc);
     sb = ef_mul_base(sa, o.zb);
   }
-  // the partial sums are of x_t invd_k[t] col[t]: the weight's sign goes into the scale
+  // the partial sums are of x_t invd_k[t] col[t]: the weight's sign goes into the scale (the
+  // coefficient form's weights are the powers themselves)
+  if (!o.tab) {
+    sa = ef_neg(sa);
+    sb = ef_neg(sb);
+  }
   const int c = (int)(blockIdx.x - o.col0);
   const bool second = c >= o.w1;  // a merged descriptor's second matrix: its own outputs
-  open_final<NP>(partial + o.part_off, (int)o.nchunks, o.w, c, ef_neg(sa), ef_neg(sb),
+  open_final<NP>(partial + o.part_off, (int)o.nchunks, o.w, c, sa, sb,
                  second ? o.out_a2 - o.w1 : o.out_a, second ? o.out_b2 - o.w1 : o.out_b);
 }
 
@@ -403,6 +412,71 @@ __global__ __launch_bounds__(256) void k_pow_table(PowSquares ps, size_t j0, siz
     if (t >= count) break;
     out[t] = p;
     p = ef_mul(p, ps.sq[8]);
+  }
+}
+
+// pow_tables / inv_denoms_ranges: block b works for the job whose block range holds b
+struct PowJobDev {
+  EF sq[32];
+  size_t j0, count;
+  EF* out;
+  uint32_t block0;
+};
+__global__ __launch_bounds__(256) void k_pow_tables(const PowJobDev* __restrict__ jobs, int nj) {
+  int m = 0;
+  while (m + 1 < nj && jobs[m + 1].block0 <= blockIdx.x) m++;
+  const PowJobDev& jb = jobs[m];
+  const size_t b0 = (size_t)(blockIdx.x - jb.block0) * 256 * POW_RUN;
+  const uint64_t eb = jb.j0 + b0;
+  EF p = ef_base(ONE);
+  for (int k = 0; k < 32; k++)
+    if ((eb >> k) & 1) p = ef_mul(p, jb.sq[k]);
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    if ((threadIdx.x >> k) & 1) p = ef_mul(p, jb.sq[k]);
+  const EF step = jb.sq[8];
+#pragma unroll 4
+  for (int k = 0; k < POW_RUN; k++) {
+    const size_t t = b0 + threadIdx.x + 256 * (size_t)k;
+    if (t >= jb.count) break;
+    jb.out[t] = p;
+    p = ef_mul(p, step);
+  }
+}
+
+struct InvJobDev {
+  EF z;
+  int logH;
+  size_t t0, count;
+  EF* out;
+  uint32_t block0;
+};
+__global__ __launch_bounds__(256) void k_inv_denoms_jobs(const InvJobDev* __restrict__ jobs, int nj,
+                                                         const uint32_t* __restrict__ twf) {
+  int m = 0;
+  while (m + 1 < nj && jobs[m + 1].block0 <= blockIdx.x) m++;
+  const InvJobDev& jb = jobs[m];
+  const size_t base = ((size_t)(blockIdx.x - jb.block0) * blockDim.x + threadIdx.x) * INV_CHUNK;
+  if (base >= jb.count) return;
+  const EF z = jb.z;
+  EF d[INV_CHUNK], pre[INV_CHUNK];
+  const int cnt = (int)min((size_t)INV_CHUNK, jb.count - base);
+  EF run = ef_one();
+#pragma unroll
+  for (int k = 0; k < INV_CHUNK; k++) {
+    if (k < cnt) {
+      d[k] = ef_sub(ef_base(coset_point((uint32_t)(jb.t0 + base + k), jb.logH, twf)), z);
+      run = ef_mul(run, d[k]);
+    }
+    pre[k] = run;
+  }
+  EF inv = ef_inv(run);
+#pragma unroll
+  for (int k = INV_CHUNK - 1; k >= 0; k--) {
+    if (k < cnt) {
+      jb.out[base + k] = k ? ef_mul(inv, pre[k - 1]) : inv;
+      inv = ef_mul(inv, d[k]);
+    }
   }
 }
 
@@ -691,6 +765,54 @@ void pow_table(const EF& z, size_t j0, size_t count, EF* out, hipStream_t st) {
   KCHECK();
 }
 
+void pow_tables(const std::vector<PowJob>& jobs, hipStream_t st) {
+  if (jobs.empty()) return;
+  std::vector<PowJobDev> jd(jobs.size());
+  uint32_t blocks = 0;
+  for (size_t i = 0; i < jobs.size(); i++) {
+    const PowJob& j = jobs[i];
+    if ((j.j0 + j.count) >> 32) throw std::runtime_error("pow_tables: exponent above 2^32");
+    jd[i].sq[0] = j.z;
+    for (int k = 1; k < 32; k++) jd[i].sq[k] = ef_mul(jd[i].sq[k - 1], jd[i].sq[k - 1]);
+    jd[i].j0 = j.j0;
+    jd[i].count = j.count;
+    jd[i].out = j.out;
+    jd[i].block0 = blocks;
+    blocks += ceil_div(j.count, (size_t)256 * POW_RUN);
+  }
+  if (!blocks) return;
+  DBuf<PowJobDev> dj(jd.size());
+  upload_async(dj.p, jd.data(), jd.size() * sizeof(PowJobDev), st);
+  hipLaunchKernelGGL(k_pow_tables, dim3(blocks), dim3(256), 0, st, (const PowJobDev*)dj.p,
+                     (int)jd.size());
+  KCHECK();
+}
+
+void inv_denoms_ranges(const std::vector<InvJob>& jobs, hipStream_t st) {
+  if (jobs.empty()) return;
+  std::vector<InvJobDev> jd(jobs.size());
+  uint32_t blocks = 0;
+  int logmax = 1;
+  for (size_t i = 0; i < jobs.size(); i++) {
+    const InvJob& j = jobs[i];
+    jd[i].z = j.z;
+    jd[i].logH = j.logH;
+    jd[i].t0 = j.t0;
+    jd[i].count = j.count;
+    jd[i].out = j.out;
+    jd[i].block0 = blocks;
+    blocks += ceil_div(ceil_div(j.count, (size_t)INV_CHUNK), (size_t)256);
+    logmax = std::max(logmax, j.logH);
+  }
+  if (!blocks) return;
+  twiddles().ensure(logmax);
+  DBuf<InvJobDev> dj(jd.size());
+  upload_async(dj.p, jd.data(), jd.size() * sizeof(InvJobDev), st);
+  hipLaunchKernelGGL(k_inv_denoms_jobs, dim3(blocks), dim3(256), 0, st, (const InvJobDev*)dj.p,
+                     (int)jd.size(), (const uint32_t*)twiddles().fwd());
+  KCHECK();
+}
+
 void open_coefficients(const uint32_t* coef, size_t col_stride, int w, size_t count,
                        const EF* tab_a, const EF& scale_a, EF* out_a, const EF* tab_b,
                        const EF& scale_b, EF* out_b, hipStream_t st) {
@@ -716,7 +838,8 @@ void open_coefficients(const uint32_t* coef, size_t col_stride, int w, size_t co
 // Two descriptors of one LDE height opened at the same points read the same weights: one
 // descriptor for both (each keeps its own outputs).
 static bool mergeable(const OpenDesc& a, const OpenDesc& b) {
-  return !a.mat2 && !b.mat2 && a.height == b.height && a.logH == b.logH && a.invd_a == b.invd_a &&
+  return !a.mat2 && !b.mat2 && a.tab == b.tab && a.rows == b.rows && a.height == b.height &&
+         a.logH == b.logH && a.invd_a == b.invd_a &&
          a.invd_b == b.invd_b && a.zeta == b.zeta && a.zlog == b.zlog && a.z3n == b.z3n &&
          a.zc == b.zc && a.zb == b.zb && a.wtab == b.wtab && ef_eq(a.scale_a, b.scale_a) &&
          ef_eq(a.scale_b, b.scale_b);
@@ -729,6 +852,8 @@ void open_batch(std::vector<OpenDesc>& in, int np, hipStream_t st) {
     return !(e && *e == '0');
   }();
   std::vector<OpenDesc> ds;
+  for (OpenDesc& o : in)
+    if (!o.rows) o.rows = o.height / 2;  // barycentric: the low coset
   for (const OpenDesc& o : in) {
     if (merge && !ds.empty() && mergeable(ds.back(), o)) {
       OpenDesc& m = ds.back();
@@ -748,7 +873,7 @@ void open_batch(std::vector<OpenDesc>& in, int np, hipStream_t st) {
   // the columns of each chunk over several blocks, so it still fills the GPU; each slab of a
   // chunk computes the chunk's weights itself.
   uint64_t nch = 0;
-  for (const OpenDesc& o : ds) nch += ceil_div(o.height / 2, och);
+  for (const OpenDesc& o : ds) nch += ceil_div(o.rows, och);
   static const uint64_t FILL = [] {  // blocks: 8 per CU (BFZ_OPEN_FILL=0: no slabs, A/B)
     const char* e = std::getenv("BFZ_OPEN_FILL");
     return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)2048;
@@ -757,7 +882,7 @@ void open_batch(std::vector<OpenDesc>& in, int np, hipStream_t st) {
   uint32_t chunks = 0, cols = 0;
   uint64_t part = 0;
   for (OpenDesc& o : ds) {
-    o.nchunks = ceil_div(o.height / 2, och);
+    o.nchunks = ceil_div(o.rows, och);
     const uint32_t groups = ceil_div(o.w, 4);  // 4-column reduction groups
     o.nslab = std::min(groups, want);
     o.slab_w = 4 * (int)ceil_div(groups, o.nslab);
@@ -776,10 +901,10 @@ void open_batch(std::vector<OpenDesc>& in, int np, hipStream_t st) {
   double obytes = 0;
   std::vector<uint64_t> heights;
   for (const OpenDesc& o : ds) {
-    obytes += (double)(o.height / 2) * 4.0 * o.w;
+    obytes += (double)o.rows * 4.0 * o.w;
     if (std::find(heights.begin(), heights.end(), o.height) == heights.end()) {
       heights.push_back(o.height);
-      obytes += (double)(o.height / 2) * 16.0 * np;
+      obytes += (double)o.rows * 16.0 * np;
     }
   }
   KernelProbe& probe = open_probe();

@@ -925,6 +925,17 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     if (wtab_on) w_zeta.reset((size_t)1 << (Lmax - 1));
     inv_denoms_dev(zeta_d, Lmax, invd_zeta.p, st, w_zeta.p);
   }
+  // a sharded proof's many small opening launches (one per matrix, table and height) go out as
+  // one batch each (BFZ_OPEN_SHARD_BATCH=0: one launch per matrix / table / range, A/B)
+  static const bool sbatch = [] {
+    const char* e = std::getenv("BFZ_OPEN_SHARD_BATCH");
+    return !(e && *e == '0');
+  }();
+  std::vector<InvJob> ijobs;
+  auto inv_range = [&](const EF& z, int lh, size_t t0, size_t cnt, EF* out) {
+    if (sbatch) ijobs.push_back({z, lh, t0, cnt, out});
+    else inv_denoms_range(z, lh, t0, cnt, out, st);
+  };
   std::map<int, Invd> invd;
   for (const auto& [lh, two] : two_at) {
     const size_t H = (size_t)1 << lh;
@@ -934,35 +945,38 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     d.t0 = t0;
     if (plan.on()) {
       d.a.reset(cnt);
-      inv_denoms_range(zeta, lh, t0, cnt, d.a.p, st);
+      inv_range(zeta, lh, t0, cnt, d.a.p);
     } else {
       d.a = DBuf<EF>::borrow(invd_zeta.p, H);
     }
     const EF znext = ef_mul_base(zeta, two_adic_gen(lh - LOG_BLOWUP));
     if (two && plan.on()) {  // single GPU: read from the zeta table (prev2_pos, fri.hip)
       d.b.reset(cnt);
-      inv_denoms_range(znext, lh, t0, cnt, d.b.p, st);
+      inv_range(znext, lh, t0, cnt, d.b.p);
     }
     if (sh && rep_at[lh]) {  // the low coset only: positions [0, H / 2)
       d.fa.reset(H / 2);
-      inv_denoms_range(zeta, lh, 0, H / 2, d.fa.p, st);
+      inv_range(zeta, lh, 0, H / 2, d.fa.p);
       if (two) {
         d.fb.reset(H / 2);
-        inv_denoms_range(znext, lh, 0, H / 2, d.fb.p, st);
+        inv_range(znext, lh, 0, H / 2, d.fb.p);
       }
     }
   }
+  inv_denoms_ranges(ijobs, st);
   // Opened values.  Replicated matrices: barycentric over the low coset of the LDE.  Sharded
   // matrices: the rank's 1/G slice of sum_j c_j (z / s)^j (s = the trace domain's shift) from
   // the kept coefficients; the slices are summed across ranks below.
   DBuf<EF> opened_d(nvals);
   std::map<std::array<uint32_t, 5>, DBuf<EF>> ptabs;  // (point, log n) -> powers on the range
+  std::vector<PowJob> pjobs;
   auto ptable = [&](const EF& z, int log_n, size_t j0, size_t len) {
     const std::array<uint32_t, 5> key{z.c[0], z.c[1], z.c[2], z.c[3], (uint32_t)log_n};
     auto it = ptabs.find(key);
     if (it != ptabs.end()) return (const EF*)it->second.p;
     DBuf<EF> t(len);
-    pow_table(z, j0, len, t.p, st);
+    if (sbatch) pjobs.push_back({z, j0, len, t.p});
+    else pow_table(z, j0, len, t.p, st);
     const EF* p = t.p;
     ptabs.emplace(key, std::move(t));
     return p;
@@ -990,8 +1004,24 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
         for (int j = 0; j < mp[r][i].npts; j++)
           tab[j] = ptable(ef_mul_base(mp[r][i].pts[j], sinv), m.log_n, j0, len);
         const EF ninv = ef_base(minv(to_mont((uint32_t)(m.n % P))));
-        open_coefficients(m.coef.p + j0, m.n, m.lde.width, len, tab[0], ninv, out_a, tab[1], ninv,
-                          out_b, st);
+        if (!sbatch) {
+          open_coefficients(m.coef.p + j0, m.n, m.lde.width, len, tab[0], ninv, out_a, tab[1],
+                            ninv, out_b, st);
+          continue;
+        }
+        OpenDesc o{};  // the coefficient form in the batched launch (fri.h)
+        o.tab = 1;
+        o.mat = m.coef.p + j0;
+        o.height = m.n;  // column stride
+        o.rows = len;
+        o.w = m.lde.width;
+        o.logH = lh;
+        o.invd_a = tab[0];
+        o.invd_b = two ? tab[1] : tab[0];
+        o.scale_a = o.scale_b = ninv;
+        o.out_a = out_a;
+        o.out_b = two ? out_b : out_a;
+        (two ? open2g : open1g)[group_of(r)].push_back(o);
         continue;
       }
       const uint32_t three_n = mpow(to_mont(3), m.n);
@@ -1023,6 +1053,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
       o.out_b = two ? out_b : out_a;
       (two ? open2g : open1g)[group_of(r)].push_back(o);
     }
+  pow_tables(pjobs, st);  // before the opening batches that read them (same stream)
   for (int r = 0; r < 4; r++)
     if (!mp[r].empty()) {
       const MatPts& last = mp[r].back();
