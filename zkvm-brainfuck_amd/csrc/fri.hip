@@ -1086,7 +1086,7 @@ void gather_queries(const std::vector<GatherSeg>& segs, const uint32_t* qidx, in
                      qidx, nq, rank, out);
   KCHECK();
   if (shard && shard->world > 1) {  // owner-masked words: one sum all-reduce, device to device
-    HIP_CHECK(hipStreamSynchronize(st));
+    coll_sync(st);
     shard->allreduce_sum_u32(out, nwords);
   }
 }

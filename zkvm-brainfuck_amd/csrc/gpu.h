@@ -269,6 +269,10 @@ void staging_reset();
 // spin_sync waits for everything queued on st so far.
 void fetch(void* dst, const void* src, size_t bytes, hipStream_t st);
 void spin_sync(hipStream_t st);
+// Before a sharded proof's host-call collective: the stream drained by spinning (a blocking wait
+// wakes tens of microseconds late, and the GPU idles until the collective returns);
+// BFZ_COLL_SPIN=0: hipStreamSynchronize (A/B).
+void coll_sync(hipStream_t st);
 // Large pageable host -> device copy through double-buffered pinned chunks (runtime.hip);
 // returns when the data has arrived.
 void upload_bulk(void* dst, const void* src, size_t bytes, hipStream_t st);

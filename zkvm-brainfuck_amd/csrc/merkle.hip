@@ -400,7 +400,7 @@ static void build_sharded(MerkleTree& t, size_t h0, const std::vector<const MatR
   // layer nl - lg has G nodes; node k is ours: all-gather them device to device
   DBuf<uint32_t>& lay = t.layers[nl - lg];
   DBuf<uint32_t> all(8 * G);
-  HIP_CHECK(hipStreamSynchronize(st));
+  coll_sync(st);
   c.allgather(lay.p + 8 * k, 32, all.p);
   HIP_CHECK(hipMemcpyAsync(lay.p, all.p, 32 * G, hipMemcpyDeviceToDevice, st));
   build_layers(t, nl - lg + 1, G, sorted, next, st, fetch_root, rc);

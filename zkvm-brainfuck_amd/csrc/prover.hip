@@ -587,7 +587,7 @@ void gather_quotients(const Round& mainr, const std::vector<size_t>& hn,
       cp.push_back({part(k, plan.k), send.p + off[k], n, b, b, 4});
     }
   copy2d_batch(cp, st);
-  HIP_CHECK(hipStreamSynchronize(st));
+  coll_sync(st);
   sc.allgather(send.p, total * 4, recv.p);
   cp.clear();
   for (int j = 0; j < plan.G; j++)
@@ -1160,12 +1160,12 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   if (dev_zeta) replay();  // the openings are queued: now the host's transcript catches up
   if (plan.on()) {  // one all-gather; sharded matrices' slices summed, replicated ones kept
     DBuf<EF> all(nvals * plan.G);
-    HIP_CHECK(hipStreamSynchronize(st));
+    coll_sync(st);
     htrace().mark("sharded openings done");
     shard->allgather(opened_d.p, nvals * sizeof(EF), all.p);
     std::vector<EF> h(nvals * plan.G);
     HIP_CHECK(hipMemcpyAsync(h.data(), all.p, h.size() * sizeof(EF), hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipStreamSynchronize(st));
+    coll_sync(st);
     htrace().mark("sharded openings on host");
     for (int r = 0; r < 4; r++)
       for (size_t i = 0; i < rounds[r]->mats.size(); i++) {
@@ -1281,7 +1281,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   auto fri_sharded = [&](size_t h) { return plan.sharded(h) && h >= FRI_SHARD_MIN; };
   auto gather = [&](DBuf<EF>& v, size_t len) {  // a row-sharded vector of len values, in place
     DBuf<EF> all(len);
-    HIP_CHECK(hipStreamSynchronize(st));
+    coll_sync(st);
     shard->allgather(v.p, plan.blk(len) * sizeof(EF), all.p);
     v = std::move(all);
   };

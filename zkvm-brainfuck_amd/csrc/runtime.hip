@@ -283,6 +283,15 @@ void spin_sync(hipStream_t st) {
   }
 }
 
+void coll_sync(hipStream_t st) {
+  static const bool spin = [] {
+    const char* e = std::getenv("BFZ_COLL_SPIN");
+    return !(e && *e == '0');
+  }();
+  if (spin) spin_sync(st);
+  else HIP_CHECK(hipStreamSynchronize(st));
+}
+
 void fetch(void* dst, const void* src, size_t bytes, hipStream_t st) {
   if (!bytes) return;
   Lane& l = lane();
