@@ -459,12 +459,19 @@ def collective_ms(kind, nbytes, world):
     return (2 * XGMI_ALPHA_US * 1e-6 + 2 * (nbytes / world) / bw) * 1e3
 
 
-def collective_model(exchanges, world):
-    """Per-rank bytes and modeled time of the logged collectives of one rank's share."""
-    ms = sum(collective_ms(k, b, world) for k, b in exchanges)
+def collective_model(exchanges, world, overlaps=None):
+    """Per-rank bytes and modeled time of the logged collectives of one rank's share.  overlaps[i]
+    (bfz_shard_solo_overlaps, from the instrumented run): GPU milliseconds the rank has queued to
+    run while collective i is in flight -- already inside the share's compute time, so collective
+    i adds max(0, its time - overlaps[i])."""
+    ov = list(overlaps or []) + [0.0] * max(0, len(exchanges) - len(overlaps or []))
+    full = [collective_ms(k, b, world) for k, b in exchanges]
+    ms = sum(max(0.0, t - o) for t, o in zip(full, ov))
     recv = sum((world - 1) * b if k == 0 else 2 * (world - 1) * b / world for k, b in exchanges)
     big = sorted(((b, k) for k, b in exchanges), reverse=True)[:4]
     return {"collectives": len(exchanges),
+            "unoverlapped_ms": round(sum(full), 3),
+            "overlapped_ms": round(sum(min(t, o) for t, o in zip(full, ov)), 3),
             "allgathers": sum(1 for k, _ in exchanges if k == 0),
             "allreduces": sum(1 for k, _ in exchanges if k == 1),
             "recv_bytes_per_rank": int(recv),
@@ -509,6 +516,11 @@ def shard_solo(pk, rec, world, steps=3):
         best = _l.Timings()
         _l.check(L.bfz_record_prove_shard_solo(ctypes.c_void_p(pk.handle), rec, k, world,
                                                ctypes.byref(best)))
+        n = ctypes.c_size_t()  # the GPU work beside each collective, from this timed run
+        _l.check(L.bfz_shard_solo_overlaps(None, 0, ctypes.byref(n)))
+        ovl = (ctypes.c_double * max(n.value, 1))()
+        _l.check(L.bfz_shard_solo_overlaps(ovl, n.value, ctypes.byref(n)))
+        overlaps = [round(ovl[i], 4) for i in range(n.value)]
         wall = []
         for _ in range(steps):
             _l.check(L.bfz_synchronize())
@@ -526,12 +538,16 @@ def shard_solo(pk, rec, world, steps=3):
             cells = (best.main_cells, best.perm_cells)
         ranks.append({"rank": k, "total_ms": round(min(wall), 3),
                       "instrumented_total_ms": round(best.total_ms, 3),
+                      "collective_overlap_ms": overlaps,
                       "stages_ms": {n: round(v, 3) for n, v in best.as_dict().items()
                                     if n.endswith("_ms") and n not in ("total_ms", "lde_ms", "ntt_kernel_ms", "p2_kernel_ms")}})
     worst = max(r["total_ms"] for r in ranks)
     slow = max(ranks, key=lambda r: r["total_ms"])
+    # the overlap a collective gets is the least any rank queues beside it (every rank waits)
+    ovs = [r["collective_overlap_ms"] for r in ranks]
+    overlap = [min(o[i] if i < len(o) else 0.0 for o in ovs) for i in range(len(exchanges))]
     return {"world": world, "max_rank_ms": worst, "ranks": ranks,
-            "collectives": collective_model(exchanges, world),
+            "collectives": collective_model(exchanges, world, overlap),
             "replication": replication_tradeoff(slow["stages_ms"], cells[0], cells[1], world),
             "what": f"each rank's share of a {world}-GPU sharded proof run alone on one GPU with "
                     "no-op exchanges (bfz_record_prove_shard_solo); total_ms = best wall time of "
@@ -897,8 +913,13 @@ def main():
                     "latency_us_per_collective": XGMI_ALPHA_US,
                     "source": "build brief: 7 xGMI links x ~153 GB/s per MI355X (bidirectional "
                               "assumed); efficiency and latency assumed, not measured (no "
-                              "multi-GPU box on this pool); collectives are synchronous on the "
-                              "prover stream (no overlap)"},
+                              "multi-GPU box on this pool); a collective is a blocking host call "
+                              "while the GPU runs what the prover queued before it: the quotient "
+                              "exchange is two all-gathers, the first beside the tallest chip's "
+                              "quotient kernel, the second beside the other chips' chunk LDEs, "
+                              "and each is charged max(0, its time - that GPU time measured in "
+                              "the rank's timed run); every other collective is charged in full "
+                              "(the stream is drained before it)"},
                 "what": "one proof split over N GPUs, predicted: N = 1 is the timed single-GPU "
                         "proof; N > 1 is the slowest rank's share run alone on this GPU with "
                         "no-op exchanges (bfz_record_prove_shard_solo), before collective time",

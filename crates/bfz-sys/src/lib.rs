@@ -277,6 +277,7 @@ extern "C" {
     pub fn bfz_record_prove_shard_solo(pk: *const bfz_pk, rec: *const bfz_record, rank: c_int,
                                        world: c_int, timings: *mut bfz_timings) -> c_int;
     pub fn bfz_shard_solo_exchanges(kinds: *mut c_int, bytes: *mut u64, cap: usize, n: *mut usize) -> c_int;
+    pub fn bfz_shard_solo_overlaps(ms: *mut f64, cap: usize, n: *mut usize) -> c_int;
     pub fn bfz_device_pool_bytes(lane: c_int, bytes: *mut u64) -> c_int;
     pub fn bfz_commit_fri_sharded(d_cols: *const u32, log_n: c_int, w_local: usize, rank: c_int,
                                   world: c_int, d_send: *mut u32, d_recv: *mut u32,

@@ -367,6 +367,13 @@ int bfz_record_prove_shard_solo(const bfz_pk* pk, const bfz_record* rec, int ran
  * reference has no multi-GPU prover. */
 int bfz_shard_solo_exchanges(int* kinds, uint64_t* bytes, size_t cap, size_t* n);
 
+/* For the same collectives: ms[i] = GPU milliseconds of the work this rank has queued to run
+ * while collective i is in flight (the sharded prover issues the quotient exchange in two
+ * all-gathers, each after the work it overlaps is queued), 0 where nothing overlaps.  Measured
+ * only by a bfz_record_prove_shard_solo run WITH timings (0 otherwise).  bench.py's collective
+ * model charges max(0, collective time - ms[i]). */
+int bfz_shard_solo_overlaps(double* ms, size_t cap, size_t* n);
+
 /* Device memory held by proof lane `lane`'s buffer pool (0..3, the lanes of
  * bfz_record_prove_repeat / bfz_prove_batch; 0 = the default
  * lane): every buffer a proof on that lane allocated, in use or cached for the next proof -- the

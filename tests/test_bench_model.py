@@ -39,3 +39,15 @@ def test_replication_decision_follows_the_model():
         r = bench.replication_tradeoff(stages, 2.5e8, 2.1e8, n)
         assert r["choice"] == "replicate", (n, r)
         assert r["replicated_ms"] == pytest.approx(3.3)
+
+
+def test_overlapped_collective_is_charged_only_beyond_the_gpu_work_beside_it():
+    log = [(0, 32), (0, 64 << 20), (0, 16 << 20)]
+    full = [bench.collective_ms(k, b, 2) for k, b in log]
+    # the big all-gather runs beside 0.4 ms of GPU work, the third beside more than it lasts
+    m = bench.collective_model(log, 2, [0.0, 0.4, 10.0])
+    assert m["unoverlapped_ms"] == pytest.approx(sum(full), abs=1e-3)
+    assert m["modeled_ms"] == pytest.approx(full[0] + (full[1] - 0.4), abs=1e-3)
+    assert m["overlapped_ms"] == pytest.approx(0.4 + full[2], abs=1e-3)
+    # no overlap log (an untimed run): everything is charged
+    assert bench.collective_model(log, 2)["modeled_ms"] == pytest.approx(sum(full), abs=1e-3)

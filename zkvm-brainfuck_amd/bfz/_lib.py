@@ -125,6 +125,7 @@ SIGNATURES = [
                                         POINTER(c_size_t), POINTER(ctypes.c_double)]),
     ("bfz_shard_solo_exchanges", c_int, [POINTER(c_int), POINTER(ctypes.c_uint64), c_size_t,
                                          POINTER(c_size_t)]),
+    ("bfz_shard_solo_overlaps", c_int, [POINTER(ctypes.c_double), c_size_t, POINTER(c_size_t)]),
     ("bfz_device_pool_bytes", c_int, [c_int, POINTER(ctypes.c_uint64)]),
     ("bfz_record_prove_sharded", c_int, [c_void_p, c_void_p, c_int, c_int, ALLGATHER_FN,
                                          ALLREDUCE_FN, c_void_p, POINTER(POINTER(c_uint8)),

@@ -835,6 +835,11 @@ std::vector<std::pair<int, uint64_t>>& solo_exchange_log() {
   static auto* v = new std::vector<std::pair<int, uint64_t>>();
   return *v;
 }
+// ... and the overlapped GPU milliseconds of each (bfz_shard_solo_overlaps)
+std::vector<double>& solo_overlap_log() {
+  static auto* v = new std::vector<double>();
+  return *v;
+}
 
 // Copies of the chunked hand-over (bfz_cycles_push) run here, beside the prover stream.
 hipStream_t handover_stream() {
@@ -1158,6 +1163,17 @@ int bfz_shard_solo_exchanges(int* kinds, uint64_t* bytes, size_t cap, size_t* n)
   });
 }
 
+int bfz_shard_solo_overlaps(double* ms, size_t cap, size_t* n) {
+  return guarded([&] {
+    if (!n) throw std::runtime_error("null argument");
+    const auto& log = solo_overlap_log();
+    *n = log.size();
+    for (size_t i = 0; i < log.size() && i < cap; i++)
+      if (ms) ms[i] = log[i];
+    return 0;
+  });
+}
+
 int bfz_record_prove_shard_solo(const bfz_pk* pk, const bfz_record* rec, int rank, int world,
                                 bfz_timings* t) {
   return guarded([&] {
@@ -1172,14 +1188,25 @@ int bfz_record_prove_shard_solo(const bfz_pk* pk, const bfz_record* rec, int ran
     // collective-time model (bfz_shard_solo_exchanges)
     auto& log = solo_exchange_log();
     log.clear();
-    c.allgather = [&log](const void*, size_t bytes, void*) { log.push_back({0, bytes}); };
-    c.allreduce_sum_u32 = [&log](uint32_t*, size_t n) { log.push_back({1, n * 4}); };
+    std::vector<const double*> ov;  // the overlap slot of each collective (filled by the events)
+    c.allgather = [&log, &ov, &c](const void*, size_t bytes, void*) {
+      log.push_back({0, bytes});
+      ov.push_back(c.pending_overlap);
+    };
+    c.allreduce_sum_u32 = [&log, &ov](uint32_t*, size_t n) {
+      log.push_back({1, n * 4});
+      ov.push_back(nullptr);
+    };
     ShardScope scope(&c);
     bfz::ProveOptions o = opts();
     o.timing = t != nullptr;  // t == nullptr: no stage events or kernel probes (wall-clock runs)
     bfz::StageTimes st;
     (void)bfz::prove_events(*pk->pk, rec->ev, o, t ? &st : nullptr);  // not a proof: discarded
     if (t) fill_timings(st, t);
+    auto& olog = solo_overlap_log();  // the proof's events have resolved into the slots
+    olog.assign(ov.size(), 0.0);
+    for (size_t i = 0; i < ov.size(); i++)
+      if (ov[i]) olog[i] = *ov[i];
     return 0;
   });
 }

@@ -273,6 +273,9 @@ void spin_sync(hipStream_t st);
 // wakes tens of microseconds late, and the GPU idles until the collective returns);
 // BFZ_COLL_SPIN=0: hipStreamSynchronize (A/B).
 void coll_sync(hipStream_t st);
+// Timed runs only: the stream busy for `us` microseconds (a one-lane spin on the wall clock),
+// so the work queued behind it runs back to back (runtime.hip).
+void gpu_delay(double us, hipStream_t st);
 // Large pageable host -> device copy through double-buffered pinned chunks (runtime.hip);
 // returns when the data has arrived.
 void upload_bulk(void* dst, const void* src, size_t bytes, hipStream_t st);

@@ -1,6 +1,7 @@
 // Poseidon2 Merkle commitment on the device: MerkleTreeMmcs<.., PaddingFreeSponge<Perm,16,8,8>,
 // TruncatedPermutation<Perm,2,8,16>, 8> (crates/stark/src/kb31_poseidon2.rs:24-28).
 #pragma once
+#include <deque>
 #include <functional>
 #include <vector>
 
@@ -38,6 +39,11 @@ struct ShardCtx {
   // timing-only run of one rank's share (bfz_record_prove_shard_solo): the exchanges are
   // no-ops, so the data after them is not the proof's and its consistency checks are skipped
   bool solo = false;
+  // timing runs of a solo share: GPU milliseconds of the work that runs beside the next
+  // collective (set just before it, filled when the proof's events resolve; slots live in
+  // overlap_store) -- bench.py's collective model subtracts them (bfz_shard_solo_overlaps)
+  mutable double* pending_overlap = nullptr;
+  mutable std::deque<double> overlap_store;
 };
 constexpr size_t SHARD_MIN_LEAVES = 1024;
 ShardCtx*& shard_ctx();

@@ -94,6 +94,9 @@ struct StageTimes {          // milliseconds, measured with HIP events on the pr
   double main_idft = 0, main_dft = 0, main_hash = 0;
   // base-field cells (sum of n x w) of the main and permutation traces
   double main_cells = 0, perm_cells = 0;
+  // timed runs of a solo share: the spins that isolate the collective-overlap windows (taken
+  // back out of quotient and total when the events resolve)
+  double spin = 0;
 };
 
 std::unique_ptr<ProvingKey> setup(const std::string& program_src);

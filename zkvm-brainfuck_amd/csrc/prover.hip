@@ -485,6 +485,8 @@ struct ProofScope {
     if (!ev.on) return;
     ev.end(e_total, stream(), &tms->total);
     ev.collect();
+    tms->quotient -= tms->spin;  // the overlap-window spins of a solo share's timed run
+    tms->total -= tms->spin;
     KernelProbe& pr = ntt_probe();
     pr.collect();
     pr.on = false;
@@ -561,42 +563,72 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
                                const ProveOptions& opt, ProofScope& ps, Challenger* after = nullptr);
 
 // Sharded chips' quotient values: rank j computed LDE positions [j b, (j+1) b) (b = 2n / G),
-// which land in chunk (j b) / n at rows [(j b) mod n, + b) of its 4 columns.  One all-gather of
-// every sharded chip's part completes qv on every rank (the chunk LDEs need whole columns).
-void gather_quotients(const Round& mainr, const std::vector<size_t>& hn,
-                      std::vector<DBuf<uint32_t>>& qv, const Plan& plan, const ShardCtx& sc,
-                      hipStream_t st) {
-  const int nc = (int)hn.size();
-  std::vector<size_t> off(nc, 0);
+// which land in chunk (j b) / n at rows [(j b) mod n, + b) of its 4 columns.  An all-gather of
+// the chips' parts completes qv on every rank (the chunk LDEs need whole columns).  One exchange
+// = pack (one batched copy, then an event), the all-gather once the event has fired (the stream
+// keeps running what was queued after the pack), unpack.
+struct QuotXchg {
+  std::vector<int> chips;
+  std::vector<size_t> off;
   size_t total = 0;
-  for (int k = 0; k < nc; k++)
-    if (mainr.mats[k].sharded) {
-      off[k] = total;
-      total += 4 * plan.blk(2 * hn[k]);
-    }
-  if (!total) return;
-  auto part = [&](int k, int rank) {  // first word of rank's part (chunk column 0) in qv[k]
-    const size_t n = hn[k], b = plan.blk(2 * n), t0 = (size_t)rank * b;
-    return qv[k].p + (t0 / n) * 4 * n + (t0 % n);
-  };
-  DBuf<uint32_t> send(total), recv(total * plan.G);
-  std::vector<Copy2D> cp;  // pack this rank's parts, then (after the all-gather) unpack the others
-  for (int k = 0; k < nc; k++)
-    if (mainr.mats[k].sharded) {
-      const size_t n = hn[k], b = plan.blk(2 * n);
-      cp.push_back({part(k, plan.k), send.p + off[k], n, b, b, 4});
-    }
+  DBuf<uint32_t> send, recv;
+  hipEvent_t ready = nullptr;
+};
+static uint32_t* quot_part(std::vector<DBuf<uint32_t>>& qv, const std::vector<size_t>& hn,
+                           const Plan& plan, int k, int rank) {  // rank's part (chunk column 0)
+  const size_t n = hn[k], b = plan.blk(2 * n), t0 = (size_t)rank * b;
+  return qv[k].p + (t0 / n) * 4 * n + (t0 % n);
+}
+static void quot_pack(QuotXchg& x, std::vector<DBuf<uint32_t>>& qv, const std::vector<size_t>& hn,
+                      const Plan& plan, hipStream_t st) {
+  x.off.assign(x.chips.size(), 0);
+  x.total = 0;
+  for (size_t i = 0; i < x.chips.size(); i++) {
+    x.off[i] = x.total;
+    x.total += 4 * plan.blk(2 * hn[x.chips[i]]);
+  }
+  if (!x.total) return;
+  x.send.reset(x.total);
+  x.recv.reset(x.total * plan.G);
+  std::vector<Copy2D> cp;
+  for (size_t i = 0; i < x.chips.size(); i++) {
+    const int k = x.chips[i];
+    const size_t n = hn[k], b = plan.blk(2 * n);
+    cp.push_back({quot_part(qv, hn, plan, k, plan.k), x.send.p + x.off[i], n, b, b, 4});
+  }
   copy2d_batch(cp, st);
-  coll_sync(st);
-  sc.allgather(send.p, total * 4, recv.p);
-  cp.clear();
+  HIP_CHECK(hipEventCreateWithFlags(&x.ready, hipEventDisableTiming));
+  HIP_CHECK(hipEventRecord(x.ready, st));
+}
+// overlap (timing runs of a rank's share): where the GPU time of the work queued between the
+// pack and this call goes (bench.py subtracts it from the collective's modeled time)
+static void quot_exchange(QuotXchg& x, const ShardCtx& sc, double* overlap) {
+  if (!x.total) return;
+  for (;;) {  // the send buffer is complete; later work stays queued on the stream
+    const hipError_t e = hipEventQuery(x.ready);
+    if (e == hipSuccess) break;
+    if (e != hipErrorNotReady) HIP_CHECK(e);
+  }
+  HIP_CHECK(hipEventDestroy(x.ready));
+  x.ready = nullptr;
+  sc.pending_overlap = overlap;
+  sc.allgather(x.send.p, x.total * 4, x.recv.p);
+  sc.pending_overlap = nullptr;
+}
+static void quot_unpack(QuotXchg& x, std::vector<DBuf<uint32_t>>& qv,
+                        const std::vector<size_t>& hn, const Plan& plan, hipStream_t st) {
+  if (!x.total) return;
+  std::vector<Copy2D> cp;
   for (int j = 0; j < plan.G; j++)
-    for (int k = 0; k < nc; k++)
-      if (mainr.mats[k].sharded && j != plan.k) {
+    for (size_t i = 0; i < x.chips.size(); i++)
+      if (j != plan.k) {
+        const int k = x.chips[i];
         const size_t n = hn[k], b = plan.blk(2 * n);
-        cp.push_back({recv.p + (size_t)j * total + off[k], part(k, j), b, n, b, 4});
+        cp.push_back({x.recv.p + (size_t)j * x.total + x.off[i], quot_part(qv, hn, plan, k, j), b,
+                      n, b, 4});
       }
   copy2d_batch(cp, st);
+  x.send.free();
 }
 }  // namespace
 
@@ -740,7 +772,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   challenge_quot(dc_d.p, permr.tree.layers.back().p, cums_d.p, nc, pc_d.p, qp_d.p, tg, st);
   htrace().mark("quotient challenge");
   std::vector<DBuf<uint32_t>> qv(nc);  // Q on 3 H_2n: 2 chunks x 4 columns of n rows
-  for (int k = 0; k < nc; k++) {
+  auto quot_chip = [&](int k) {
     const int c = chip[k];
     const size_t n = hn[k];
     const int logn = log2i(n);
@@ -777,7 +809,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
       quotient_into(c, in, logn + 1, qp,
                     QuotOut{{quotr.mats[2 * k].lde.buf.p, quotr.mats[2 * k + 1].lde.buf.p + n}, N}, st,
                     qp_d.p + k);
-      continue;
+      return;
     }
     // sharded: this rank's points only; next rows from the next-residue shards
     qv[k].reset(8 * n);
@@ -786,13 +818,8 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
     std::copy(mm.nmap.begin(), mm.nmap.end(), in.nmain);
     std::copy(pm.nmap.begin(), pm.nmap.end(), in.nperm);
     quotient_rows(c, in, logn + 1, qp, qv[k].p, st, qp_d.p + k);
-  }
-  if (plan.on()) gather_quotients(mainr, hn, qv, plan, *shard, st);
-  for (int k = 0; k < nc; k++) {  // the next-row shards are done with
-    mainr.mats[k].nxt.free();
-    permr.mats[k].nxt.free();
-  }
-  for (int k = 0; k < nc; k++) {
+  };
+  auto chunk_ldes = [&](int k) {
     const size_t n = hn[k];
     const uint32_t w2n = two_adic_gen(log2i(n) + 1);
     if (!mainr.mats[k].sharded) {  // the other half of each chunk LDE
@@ -808,13 +835,89 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
           tms->lde_calls++;
         }
       }
-      continue;
+      return;
     }
     for (int cc = 0; cc < 2; cc++) {
       const uint32_t dshift = mmul(to_mont(3), cc ? w2n : ONE);  // split_domains: shift * g^cc
       lde_into(quotr.mats[2 * k + cc], qv[k].p + (size_t)4 * cc * n, n, 4, dshift, st, &ev, tms,
                &plan);
     }
+  };
+  auto free_next = [&] {  // the next-row shards are done with
+    for (int k = 0; k < nc; k++) {
+      mainr.mats[k].nxt.free();
+      permr.mats[k].nxt.free();
+    }
+  };
+  // Sharded: two exchanges -- every sharded chip but the tallest, then the tallest -- so the first
+  // all-gather runs while the GPU computes the tallest chip's quotient and the second while it
+  // runs the other chips' chunk LDEs (the collectives are host calls; the stream keeps working
+  // through what was queued before them).  BFZ_QUOT_PIPE=0: one exchange after every kernel.
+  static const bool pipe = [] {
+    const char* e = std::getenv("BFZ_QUOT_PIPE");
+    return !(e && *e == '0');
+  }();
+  int big = -1;
+  if (plan.on())
+    for (int k = 0; k < nc; k++)
+      if (mainr.mats[k].sharded && (big < 0 || hn[k] > hn[big])) big = k;
+  if (big < 0) {  // one GPU, or no sharded chip
+    for (int k = 0; k < nc; k++) quot_chip(k);
+    free_next();
+    for (int k = 0; k < nc; k++) chunk_ldes(k);
+  } else if (!pipe) {
+    for (int k = 0; k < nc; k++) quot_chip(k);
+    QuotXchg x;
+    for (int k = 0; k < nc; k++)
+      if (mainr.mats[k].sharded) x.chips.push_back(k);
+    quot_pack(x, qv, hn, plan, st);
+    quot_exchange(x, *shard, nullptr);
+    quot_unpack(x, qv, hn, plan, st);
+    free_next();
+    for (int k = 0; k < nc; k++) chunk_ldes(k);
+  } else {
+    // overlap slots (timing runs of a solo share only): filled when the proof's events resolve
+    auto slot = [&]() -> double* {
+      if (!ev.on || !shard->solo) return nullptr;
+      shard->overlap_store.push_back(0.0);
+      return &shard->overlap_store.back();
+    };
+    QuotXchg xa, xb;
+    for (int k = 0; k < nc; k++)
+      if (k != big) {
+        quot_chip(k);
+        if (mainr.mats[k].sharded) xa.chips.push_back(k);
+      }
+    quot_pack(xa, qv, hn, plan, st);
+    double* w1 = slot();
+    // timed runs: the window's work is queued behind a 2 ms spin, so it runs back to back as in a
+    // real run (queued before the blocking collective) and its span is its GPU time
+    if (w1) {
+      hipEvent_t sb = ev.begin(st);
+      gpu_delay(2000.0, st);
+      ev.end(sb, st, &tms->spin);
+    }
+    hipEvent_t b1 = w1 ? ev.begin(st) : nullptr;
+    quot_chip(big);
+    xb.chips.push_back(big);
+    quot_pack(xb, qv, hn, plan, st);
+    if (w1) ev.end(b1, st, w1);
+    free_next();
+    quot_exchange(xa, *shard, w1);
+    quot_unpack(xa, qv, hn, plan, st);
+    double* w2 = slot();
+    if (w2) {
+      hipEvent_t sb = ev.begin(st);
+      gpu_delay(2000.0, st);
+      ev.end(sb, st, &tms->spin);
+    }
+    hipEvent_t b2 = w2 ? ev.begin(st) : nullptr;
+    for (int k = 0; k < nc; k++)
+      if (k != big) chunk_ldes(k);
+    if (w2) ev.end(b2, st, w2);
+    quot_exchange(xb, *shard, w2);
+    quot_unpack(xb, qv, hn, plan, st);
+    chunk_ldes(big);
   }
   qv.clear();
   span.begin("commit to quotient traces");  // prover.rs:410

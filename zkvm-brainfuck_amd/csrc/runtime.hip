@@ -439,3 +439,27 @@ void copy2d_batch(const std::vector<Copy2D>& v, hipStream_t st) {
   }
 }
 }  // namespace bfz
+
+namespace bfz {
+// ------------------------------------------------------------------ timed-run helper
+// Keeps the stream busy for `us` microseconds (one lane, the constant-rate wall clock), so that
+// work the host queues meanwhile then runs back to back: a timed run measures the GPU time of a
+// window the way a real run executes it (queued ahead of a blocking collective), without the
+// launch gaps the host's probe bookkeeping would leave in it.
+__global__ __launch_bounds__(64) void k_delay(long long ticks) {
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+void gpu_delay(double us, hipStream_t st) {
+  static const long long khz = [] {
+    int dev = 0, r = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&r, hipDeviceAttributeWallClockRate, dev) != hipSuccess || r <= 0)
+      r = 100000;  // 100 MHz
+    return (long long)r;
+  }();
+  hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, st, (long long)(us * (double)khz / 1000.0));
+  KCHECK();
+}
+}  // namespace bfz
