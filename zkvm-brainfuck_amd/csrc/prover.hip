@@ -573,6 +573,12 @@ struct QuotXchg {
   size_t total = 0;
   DBuf<uint32_t> send, recv;
   hipEvent_t ready = nullptr;
+  QuotXchg() = default;
+  QuotXchg(const QuotXchg&) = delete;
+  QuotXchg& operator=(const QuotXchg&) = delete;
+  ~QuotXchg() {  // an exchange abandoned by an error between its pack and its all-gather
+    if (ready) (void)hipEventDestroy(ready);
+  }
 };
 static uint32_t* quot_part(std::vector<DBuf<uint32_t>>& qv, const std::vector<size_t>& hn,
                            const Plan& plan, int k, int rank) {  // rank's part (chunk column 0)
