@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <functional>
 #include <atomic>
+#include <chrono>
 #include <map>
 #include <mutex>
 #include <unordered_map>
@@ -72,11 +73,18 @@ class DevicePool {
       return p;
     }
     void* p = nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
     HIP_CHECK(hipMalloc(&p, bytes));
+    malloc_ns_ += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                      std::chrono::steady_clock::now() - t0).count();
+    mallocs_++;
     size_of_[p] = bytes;
     held_ += bytes;
     return p;
   }
+  // hipMalloc calls made by this pool so far and their host time (diagnostics: host trace)
+  uint64_t mallocs() const { return mallocs_; }
+  double malloc_ms() const { return malloc_ns_ * 1e-6; }
   size_t bytes() {  // device memory this pool holds (in use + cached)
     std::lock_guard<std::mutex> lk(mu_);
     return held_;
@@ -106,6 +114,7 @@ class DevicePool {
   std::map<size_t, std::vector<void*>> free_;
   std::unordered_map<void*, size_t> size_of_;
   size_t held_ = 0;
+  std::atomic<uint64_t> mallocs_{0}, malloc_ns_{0};
   std::mutex mu_;
 };
 
@@ -273,6 +282,9 @@ void spin_sync(hipStream_t st);
 // wakes tens of microseconds late, and the GPU idles until the collective returns);
 // BFZ_COLL_SPIN=0: hipStreamSynchronize (A/B).
 void coll_sync(hipStream_t st);
+// The calling thread's lane's pinned staging arena, fetch mailbox and spin event, allocated now
+// rather than inside its first proof (setup calls it; runtime.hip).
+void lane_host_reserve();
 // Timed runs only: the stream busy for `us` microseconds (a one-lane spin on the wall clock),
 // so the work queued behind it runs back to back (runtime.hip).
 void gpu_delay(double us, hipStream_t st);

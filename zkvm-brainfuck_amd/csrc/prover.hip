@@ -219,6 +219,14 @@ struct Mailbox {
     HIP_CHECK(hipEventRecord(ev, st));
     pending = true;
   }
+  void reserve(size_t bytes) {  // setup: the pinned box and event before the first proof
+    if (!ev) HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    if (bytes > cap && !pending) {
+      if (box) HIP_CHECK(hipHostFree(box));
+      cap = std::max(bytes, (size_t)4096);
+      HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&box), cap, hipHostMallocDefault));
+    }
+  }
   void wait(void* dst, size_t bytes) {
     for (;;) {
       const hipError_t e = hipEventQuery(ev);
@@ -389,8 +397,34 @@ void commit_lde(CMat& cm, const uint32_t* evals, size_t n, int w, uint32_t domai
 }
 
 // ------------------------------------------------------------------------ setup
+// The quotient-roots mailbox of each lane (the API lock is held: see open_impl's gbox).
+static Mailbox* roots_boxes() {
+  static Mailbox boxes[MAX_LANES];
+  return boxes;
+}
+
+// The host-side buffers a proof on the calling thread's lane uses -- pinned staging arena, fetch
+// and roots mailboxes, the opened-value and proof-tail boxes, the group events -- allocated at
+// setup: a first proof that pins them itself spends about a millisecond per buffer.
+static void warm_lane_host() {
+  lane_host_reserve();
+  Lane& ln = lane();
+  roots_boxes()[ln.id].reserve(4096);
+  for (int g = 0; g < Lane::NGEV; g++)
+    if (!ln.gev[g]) HIP_CHECK(hipEventCreateWithFlags(&ln.gev[g], hipEventDisableTiming));
+  if (!ln.gbox) {
+    ln.gcap = 4096;  // EF values; a proof with more regrows it
+    HIP_CHECK(hipHostMalloc(&ln.gbox, ln.gcap * sizeof(EF), hipHostMallocDefault));
+  }
+  if (!ln.tbox) {
+    ln.tcap = (size_t)1 << 18;  // words of the proof tail; a longer tail regrows it
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&ln.tbox), ln.tcap * 4, hipHostMallocDefault));
+  }
+}
+
 std::unique_ptr<ProvingKey> setup(const std::string& src) {
   ResidentScope rs;  // the key lives beside the tables, outside every lane's working set
+  warm_lane_host();
   twiddles().ensure(TWIDDLE_LOG_MAX);  // every transform size a proof can use (device-built)
   auto pk = std::make_unique<ProvingKey>();
   pk->program = Program::parse(src);
@@ -938,8 +972,7 @@ std::vector<uint8_t> open_impl(const ProvingKey& pk, MainData& md, Challenger ch
   const bool dev_zeta = !plan.on();
   EF* const zeta_d = cums_d.p + nc + 9;
   if (dev_zeta) challenge_zeta(dc_d.p, quotr.tree.layers.back().p, zeta_d, st);
-  static Mailbox roots_boxes[MAX_LANES];  // per lane: the API lock is held (see open_impl's gbox)
-  Mailbox& roots_box = roots_boxes[lane().id];
+  Mailbox& roots_box = roots_boxes()[lane().id];
   roots_box.post(cums_d.p, (nc + 10) * sizeof(EF), st);
   EF zeta = ef_zero();
   std::vector<EF> cums(nc + 10);  // [0, nc): the chips' cumulative sums (written into the proof)
@@ -1666,6 +1699,9 @@ std::vector<uint8_t> prove_events(const ProvingKey& pk, const DeviceEvents& ev,
     HIP_CHECK(hipEventRecord(a, st));
   }
   htrace().mark("proof start", true);
+  static const bool pool_diag = std::getenv("BFZ_HOST_TRACE") != nullptr;
+  const uint64_t m0 = lane().pool.mallocs();
+  const double t0 = lane().pool.malloc_ms();
   Span span("prove_shard");  // prover.rs:575
   DeviceTraces dt;
   {
@@ -1676,6 +1712,9 @@ std::vector<uint8_t> prove_events(const ProvingKey& pk, const DeviceEvents& ev,
   if (timing) HIP_CHECK(hipEventRecord(b, st));
   auto proof = prove_device(pk, dt, opt, times);
   htrace().mark("proof returned");
+  if (pool_diag)  // the proof's hipMalloc calls (a first proof fills the lane's pool)
+    std::fprintf(stderr, "pool: %llu hipMalloc in this proof, %.3f ms of host time\n",
+                 (unsigned long long)(lane().pool.mallocs() - m0), lane().pool.malloc_ms() - t0);
   if (timing) {
     float ms = 0;
     HIP_CHECK(hipEventElapsedTime(&ms, a, b));

@@ -283,6 +283,19 @@ void spin_sync(hipStream_t st) {
   }
 }
 
+void lane_host_reserve() {
+  Lane& l = lane();
+  if (!l.stage) {
+    l.stage_cap = (size_t)8 << 20;
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&l.stage), l.stage_cap, hipHostMallocDefault));
+  }
+  if (!l.box) {
+    l.box_cap = (size_t)1 << 16;
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&l.box), l.box_cap, hipHostMallocDefault));
+  }
+  if (!l.spin) HIP_CHECK(hipEventCreateWithFlags(&l.spin, hipEventDisableTiming));
+}
+
 void coll_sync(hipStream_t st) {
   static const bool spin = [] {
     const char* e = std::getenv("BFZ_COLL_SPIN");
