@@ -332,8 +332,11 @@ void bfz_host_free(void* p);
  * callbacks (torch.distributed / RCCL on the host side).  Every rank returns the same proof,
  * byte-identical to bfz_record_prove's.  The
  * callbacks return 0 on success.  Their buffers (send / recv / data) are DEVICE pointers on the
- * rank's GPU (the library's stream is synchronized before each call and the data must be in
- * place when the callback returns): ncclAllGather / ncclAllReduce run on them directly. */
+ * rank's GPU: ncclAllGather / ncclAllReduce run on them directly.  When a callback is entered the
+ * send data is complete; the library's stream is drained first except at the two quotient
+ * all-gathers, where later GPU work is already queued to run beside the collective (a callback
+ * that synchronizes the whole device waits for that work too, which is correct).  The received
+ * data must be in place when the callback returns. */
 typedef int (*bfz_allgather_fn)(void* ctx, const void* send, size_t bytes, void* recv);
 typedef int (*bfz_allreduce_u32_fn)(void* ctx, uint32_t* data, size_t n);
 /* `count` proofs of one record back to back with `inflight` (1..4) of them in flight, each on

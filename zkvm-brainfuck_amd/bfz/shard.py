@@ -29,7 +29,8 @@ class _DeviceSpan:
 class Collectives:
     """ctypes callbacks over a torch.distributed process group.
 
-    libbfz passes DEVICE pointers on the rank's GPU (its stream already synchronized).  With the
+    libbfz passes DEVICE pointers on the rank's GPU (the send data complete; at the two quotient
+    all-gathers later GPU work is still queued, which _sync's device-wide wait covers).  With the
     nccl backend (RCCL) the collective runs on views of those buffers, device to device over
     xGMI; with gloo (several test ranks sharing one GPU) the data goes through host tensors."""
 

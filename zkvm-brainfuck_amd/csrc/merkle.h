@@ -31,7 +31,9 @@ struct MerkleTree {
 struct ShardCtx {
   int rank = 0, world = 1;
   // Every buffer below is DEVICE memory on this rank's GPU (RCCL moves it over xGMI with no host
-  // copy).  The prover stream is synchronized before a call; the data is in place on return.
+  // copy).  The send data is complete when a call is made (the prover stream is drained first,
+  // except before the two pipelined quotient all-gathers, where later work stays queued); the
+  // received data is in place on return.
   // all-gather `bytes` from every rank into recv (world * bytes, rank order)
   std::function<void(const void* send, size_t bytes, void* recv)> allgather;
   // element-wise sum over ranks, in place
