@@ -112,3 +112,30 @@ def test_register_fold_halving_steps(lg):
             u = k0 + i0 * D
             got[u] = y[i0] * pow(a, u, P) % P
     assert got == ref
+
+
+@pytest.mark.parametrize("logn", [11, 12, 14])
+def test_logup_running_sum_tiles_cover_natural_rows_in_order(logn):
+    """logup.hip k_phi_sums / k_phi_write: natural row i = x 2^(L-5) + z is stored at
+    t = rev(z) 32 + rev5(x); a tile (all 32 x, 64 consecutive z) reads whole 32-row storage runs,
+    and tile rows (x, b) taken row-major are consecutive natural ranges -- so a flat scan of the
+    tile sums in that order gives every tile row's natural-order prefix."""
+    n = 1 << logn
+    Z = n >> 5
+    nt = Z // 64
+    seen = set()
+    for b in range(nt):
+        for zl in range(64):
+            run = [(_brev(b * 64 + zl, logn - 5) << 5) | xr for xr in range(32)]
+            assert run == list(range(run[0], run[0] + 32))  # one contiguous storage run
+            for xr in range(32):
+                x = _brev(xr, 5)
+                i = x * Z + b * 64 + zl
+                assert _brev(i, logn) == run[xr]
+                seen.add(run[xr])
+    assert len(seen) == n
+    order = []  # tile rows row-major: natural ranges [x Z + 64 b, + 64)
+    for x in range(32):
+        for b in range(nt):
+            order.append(x * Z + 64 * b)
+    assert order == list(range(0, n, 64))
