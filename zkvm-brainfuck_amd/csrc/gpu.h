@@ -17,6 +17,7 @@
 #include <map>
 #include <mutex>
 #include <unordered_map>
+#include <unordered_set>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -58,13 +59,19 @@ __device__ __forceinline__ uint32_t dbitrev(uint32_t x, int bits) {
 // shape reuses cached buffers.  Buffers are never released (trim() is not called by the prover):
 // a process that proves shapes whose buffers differ by more than 2x holds a set per size class
 // (tests/test_gpu.py test_pool_reuse_across_shapes measures it).
+// New buffers below SLAB_BIG are carved from 256 MiB slabs (4 KiB granules), so the first proof
+// of a process makes a few dozen hipMalloc calls instead of ~400 between its launches
+// (BFZ_POOL_SLABS=0: one hipMalloc per buffer, as before).
 class DevicePool {
  public:
+  static constexpr size_t SLAB = (size_t)256 << 20, SLAB_BIG = (size_t)32 << 20, GRAIN = 4096;
   // (locked: a buffer may be released from another lane's thread than the one that allocated it)
   void* alloc(size_t bytes) {
     std::lock_guard<std::mutex> lk(mu_);
     bytes = (bytes + 255) & ~(size_t)255;
     if (bytes == 0) bytes = 256;
+    const bool carve = bytes < SLAB_BIG && slabs_on();
+    if (carve) bytes = (bytes + GRAIN - 1) & ~(GRAIN - 1);
     auto it = free_.lower_bound(bytes);
     if (it != free_.end() && it->first <= 2 * bytes) {
       void* p = it->second.back();
@@ -72,14 +79,26 @@ class DevicePool {
       if (it->second.empty()) free_.erase(it);
       return p;
     }
-    void* p = nullptr;
-    const auto t0 = std::chrono::steady_clock::now();
-    HIP_CHECK(hipMalloc(&p, bytes));
-    malloc_ns_ += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
-                      std::chrono::steady_clock::now() - t0).count();
-    mallocs_++;
+    if (carve) {
+      if (slab_left_ < bytes) {
+        // the old slab's tail becomes a free buffer of its own size (taken by a later request
+        // of half that size or more)
+        if (slab_left_ >= GRAIN) {
+          size_of_[slab_next_] = slab_left_;
+          free_[slab_left_].push_back(slab_next_);
+        }
+        slab_next_ = (uint8_t*)device_malloc(SLAB);
+        slab_left_ = SLAB;
+      }
+      void* p = slab_next_;
+      slab_next_ += bytes;
+      slab_left_ -= bytes;
+      size_of_[p] = bytes;
+      return p;
+    }
+    void* p = device_malloc(bytes);
     size_of_[p] = bytes;
-    held_ += bytes;
+    own_.insert(p);
     return p;
   }
   // hipMalloc calls made by this pool so far and their host time (diagnostics: host trace)
@@ -96,23 +115,52 @@ class DevicePool {
     if (it == size_of_.end()) return;
     free_[it->second].push_back(p);
   }
-  void trim() {
+  void trim() {  // frees the cached buffers that have an allocation of their own (not slab pieces)
     std::lock_guard<std::mutex> lk(mu_);
-    for (auto& kv : free_)
-      for (void* p : kv.second) {
-        (void)hipFree(p);
-        held_ -= kv.first;
-        size_of_.erase(p);
+    for (auto kv = free_.begin(); kv != free_.end();) {
+      auto& v = kv->second;
+      for (size_t i = 0; i < v.size();) {
+        if (!own_.count(v[i])) {
+          i++;
+          continue;
+        }
+        (void)hipFree(v[i]);
+        held_ -= kv->first;
+        size_of_.erase(v[i]);
+        own_.erase(v[i]);
+        v[i] = v.back();
+        v.pop_back();
       }
-    free_.clear();
+      kv = v.empty() ? free_.erase(kv) : std::next(kv);
+    }
   }
   ~DevicePool() {}
 
  private:
+  static bool slabs_on() {
+    static const bool on = [] {
+      const char* e = std::getenv("BFZ_POOL_SLABS");
+      return !(e && e[0] == '0' && !e[1]);
+    }();
+    return on;
+  }
+  void* device_malloc(size_t bytes) {  // (mu_ held)
+    void* p = nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    HIP_CHECK(hipMalloc(&p, bytes));
+    malloc_ns_ += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                      std::chrono::steady_clock::now() - t0).count();
+    mallocs_++;
+    held_ += bytes;
+    return p;
+  }
   // a proof allocates and releases a few hundred buffers of some tens of sizes: an ordered map of
   // the free sizes (empty lists erased) for the best-fit lookup, a hash map for the releases
   std::map<size_t, std::vector<void*>> free_;
   std::unordered_map<void*, size_t> size_of_;
+  std::unordered_set<void*> own_;  // buffers with a hipMalloc of their own (trim() may free them)
+  uint8_t* slab_next_ = nullptr;   // the current slab's unused tail
+  size_t slab_left_ = 0;
   size_t held_ = 0;
   std::atomic<uint64_t> mallocs_{0}, malloc_ns_{0};
   std::mutex mu_;
