@@ -107,6 +107,10 @@ int bfz_init(int device) {
                                std::to_string(bound) + " (one process per GPU)");
     HIP_CHECK(hipSetDevice(device));
     (void)bfz::stream();
+    // every kernel a proof launches, looked up now rather than between the first proof's launches
+    const double pre_ms = bfz::preload_kernels();
+    if (pre_ms > 0 && std::getenv("BFZ_HOST_TRACE"))
+      std::fprintf(stderr, "preload: kernels looked up in %.2f ms\n", pre_ms);
     bound = device;
     return 0;
   });

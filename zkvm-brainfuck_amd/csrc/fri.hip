@@ -1091,4 +1091,22 @@ void gather_queries(const std::vector<GatherSeg>& segs, const uint32_t* qidx, in
   }
 }
 
+// kernels a proof launches (gpu.h PreloadKernels)
+static PreloadKernels preload_fri{
+    (const void*)&k_inv_denoms,
+    (const void*)&k_open_partial_batch<1>,
+    (const void*)&k_open_partial_batch<2>,
+    (const void*)&k_open_final_batch<1>,
+    (const void*)&k_open_final_batch<2>,
+    (const void*)&k_reduce,
+    (const void*)&k_reduce_prep,
+    (const void*)&k_fri_fold_dev,
+    (const void*)&k_fold_leaves,
+    (const void*)&k_fri_challenge,
+    (const void*)&k_fri_tail,
+    (const void*)&k_fri_finish,
+    (const void*)&k_grind,
+    (const void*)&k_sample_queries,
+    (const void*)&k_gather_segs};
+
 }  // namespace bfz

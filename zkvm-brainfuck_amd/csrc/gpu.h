@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <functional>
+#include <initializer_list>
 #include <atomic>
 #include <chrono>
 #include <map>
@@ -165,6 +166,19 @@ class DevicePool {
   std::atomic<uint64_t> mallocs_{0}, malloc_ns_{0};
   std::mutex mu_;
 };
+
+// Kernel preloading.  The first launch of a kernel loads its file's code object onto the device
+// and builds the kernel's launch object: host work that otherwise lands between a fresh
+// process's first proof's launches.  Each .hip file registers the kernels a proof launches
+// (a static PreloadKernels list); bfz_init runs hipFuncGetAttributes on every one of them, the
+// same lookup a first launch makes (BFZ_PRELOAD=0: lazily, at the first launch).
+void preload_register(const void* kernel);
+struct PreloadKernels {
+  PreloadKernels(std::initializer_list<const void*> ks) {
+    for (const void* k : ks) preload_register(k);
+  }
+};
+double preload_kernels();  // host ms spent (0 when disabled or already done)
 
 // A proof lane: the device context one proof runs in -- its stream, the stream-ordered buffer
 // pool of that stream, the pinned staging arena of its in-proof uploads and its transcript

@@ -395,4 +395,22 @@ void challenge_zeta(DevChallenger* ch, const uint32_t* root, EF* zeta, hipStream
   KCHECK();
 }
 
+// kernels a proof launches (gpu.h PreloadKernels)
+static PreloadKernels preload_logup{
+    (const void*)&k_perm_rows<0>,
+    (const void*)&k_perm_rows<1>,
+    (const void*)&k_perm_rows<2>,
+    (const void*)&k_perm_rows<3>,
+    (const void*)&k_perm_rows<4>,
+    (const void*)&k_perm_rows<5>,
+    (const void*)&k_perm_rows<6>,
+    (const void*)&k_perm_rows<7>,
+    (const void*)&k_write_phi,
+    (const void*)&k_scan_block,
+    (const void*)&k_scan_add,
+    (const void*)&k_phi_sums,
+    (const void*)&k_phi_write,
+    (const void*)&k_challenge_perm,
+    (const void*)&k_challenge_zeta};
+
 }  // namespace bfz

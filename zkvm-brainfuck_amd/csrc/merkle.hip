@@ -484,4 +484,13 @@ void poseidon2_batch_small(uint32_t* states, size_t n, hipStream_t st) {
   KCHECK();
 }
 
+// kernels a proof launches (gpu.h PreloadKernels)
+static PreloadKernels preload_merkle{
+    (const void*)&k_hash_leaves,
+    (const void*)&k_compress,
+    (const void*)&k_compress_top,
+    (const void*)&k_compress_lanes,
+    (const void*)&k_hash_rows8_lanes,
+    (const void*)&k_hash_rows8};
+
 }  // namespace bfz

@@ -1262,4 +1262,40 @@ void transpose_bitrev(const uint32_t* rowmajor, size_t n, int w, uint32_t* colma
   KCHECK();
 }
 
+// kernels a proof launches (gpu.h PreloadKernels)
+static PreloadKernels preload_ntt{
+    (const void*)&k_lde_tiny,
+    (const void*)&k_transpose_bitrev,
+    (const void*)&k_lde_mid<14>,
+    (const void*)&k_lde_mid<15>,
+    (const void*)&k_lde_mid<16>,
+    (const void*)&k_lde_mid<17>,
+    (const void*)&k_lde_mid<18>,
+    (const void*)&k_lde_mid<19>,
+    (const void*)&k_lde_mid<20>,
+    (const void*)&k_lde_mid<21>,
+    (const void*)&k_lde_mid<22>,
+    (const void*)&k_lde_mid<23>,
+    (const void*)&k_ntt_tile<true, 8, false, false, false>,
+    (const void*)&k_ntt_tile<false, 8, true, false, false>,
+    (const void*)&k_ntt_tile<false, 8, false, false, false>,
+    (const void*)&k_ntt_tile<true, 9, false, false, false>,
+    (const void*)&k_ntt_tile<false, 9, true, false, false>,
+    (const void*)&k_ntt_tile<false, 9, false, false, false>,
+    (const void*)&k_ntt_tile<true, 10, false, false, false>,
+    (const void*)&k_ntt_tile<false, 10, true, false, false>,
+    (const void*)&k_ntt_tile<false, 10, false, false, false>,
+    (const void*)&k_ntt_tile<true, 11, false, false, false>,
+    (const void*)&k_ntt_tile<false, 11, true, false, false>,
+    (const void*)&k_ntt_tile<false, 11, false, false, false>,
+    (const void*)&k_ntt_tile<true, 12, false, false, false>,
+    (const void*)&k_ntt_tile<false, 12, true, false, false>,
+    (const void*)&k_ntt_tile<false, 12, false, false, false>,
+    (const void*)&k_ntt_tile<true, 13, false, false, false>,
+    (const void*)&k_ntt_tile<false, 13, true, false, false>,
+    (const void*)&k_ntt_tile<false, 13, false, false, false>,
+    (const void*)&k_ntt_tile<true, 14, false, true, true>,
+    (const void*)&k_ntt_tile<false, 14, true, true, true>,
+    (const void*)&k_ntt_tile<false, 14, false, true, true>};
+
 }  // namespace bfz

@@ -1738,4 +1738,7 @@ std::vector<uint8_t> prove(const ProvingKey& pk, const uint8_t* in, size_t nin,
   return prove_events(pk, ev, opt, times);
 }
 
+// kernels a proof launches (gpu.h PreloadKernels)
+static PreloadKernels preload_prover{(const void*)&k_pack_fri_tail};
+
 }  // namespace bfz

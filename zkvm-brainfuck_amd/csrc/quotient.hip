@@ -327,4 +327,17 @@ int num_constraints(int chip) {
   return counts[chip];
 }
 
+// kernels a proof launches (gpu.h PreloadKernels)
+static PreloadKernels preload_quotient{
+    (const void*)&k_quotient<0>,
+    (const void*)&k_quotient<1>,
+    (const void*)&k_quotient<2>,
+    (const void*)&k_quotient<3>,
+    (const void*)&k_quotient<4>,
+    (const void*)&k_quotient<5>,
+    (const void*)&k_quotient<6>,
+    (const void*)&k_quotient<7>,
+    (const void*)&k_sel_inv,
+    (const void*)&k_challenge_quot};
+
 }  // namespace bfz

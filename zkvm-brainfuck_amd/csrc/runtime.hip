@@ -58,6 +58,27 @@ DevicePool& resident_pool() {
 ResidentScope::ResidentScope() : prev(tl_pool) { tl_pool = &resident_pool(); }
 ResidentScope::~ResidentScope() { tl_pool = prev; }
 
+static std::vector<const void*>& preload_list() {
+  static auto* v = new std::vector<const void*>();  // filled by static initialisers
+  return *v;
+}
+void preload_register(const void* kernel) { preload_list().push_back(kernel); }
+double preload_kernels() {
+  static std::once_flag once;
+  double ms = 0;
+  std::call_once(once, [&] {
+    const char* e = std::getenv("BFZ_PRELOAD");
+    if (e && e[0] == '0' && !e[1]) return;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (const void* k : preload_list()) {
+      hipFuncAttributes a;
+      HIP_CHECK(hipFuncGetAttributes(&a, k));
+    }
+    ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  });
+  return ms;
+}
+
 void run_lanes(int n, const std::function<void(int)>& body) {
   std::exception_ptr err;
   std::mutex mu;
@@ -475,4 +496,9 @@ void gpu_delay(double us, hipStream_t st) {
   hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, st, (long long)(us * (double)khz / 1000.0));
   KCHECK();
 }
+// kernels a proof launches (gpu.h PreloadKernels)
+static PreloadKernels preload_runtime{
+    (const void*)&k_copy2d_batch<4>,
+    (const void*)&k_copy2d_batch<1>};
+
 }  // namespace bfz

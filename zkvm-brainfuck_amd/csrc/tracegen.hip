@@ -693,4 +693,16 @@ void generate_traces_device(const DeviceEvents& ev, DeviceTraces& dt, hipStream_
   }
 }
 
+// kernels a proof launches (gpu.h PreloadKernels)
+static PreloadKernels preload_tracegen{
+    (const void*)&k_deps,
+    (const void*)&k_trace_cpu,
+    (const void*)&k_trace_addsub,
+    (const void*)&k_trace_jump,
+    (const void*)&k_trace_memory,
+    (const void*)&k_trace_meminstr,
+    (const void*)&k_trace_io,
+    (const void*)&k_trace_program,
+    (const void*)&k_trace_byte};
+
 }  // namespace bfz
