@@ -88,6 +88,8 @@ typedef struct {
   double main_cells, perm_cells;
 } bfz_timings;
 
+/* Binds the process to `device` and looks up every kernel a proof launches (code objects and
+ * launch objects, ~5 ms), so none of that runs between the first proof's launches. */
 int bfz_init(int device);
 const char* bfz_last_error(void);
 /* Hash of the sources the library was built from (bfz/srchash.py); bfz/_lib.py refuses a
